@@ -1,0 +1,138 @@
+"""Synthetic pangenome FASTA generator (splitmix64, numpy-vectorised).
+
+The reference ships no benchmark inputs; the
+configurations named in BASELINE.json are rebuilt here from the model stated in
+SURVEY.md §8(d): a random base genome plus per-genome SNPs and short indels,
+uppercase ACGT, 60-column lines, ``\\n`` line ends and a trailing newline.
+
+Everything is deterministic in (seed, genome index), so every rank of a
+multi-GPU run can build its own shard without communication.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+GAMMA = np.uint64(0x9E3779B97F4A7C15)
+M1 = np.uint64(0xBF58476D1CE4E5B9)
+M2 = np.uint64(0x94D049BB133111EB)
+DEFAULT_SEED = 0x5EED2026
+ACGT = np.frombuffer(b"ACGT", dtype=np.uint8)
+
+
+def splitmix64(seed: int, stream: int, n: int) -> np.ndarray:
+    """n outputs of splitmix64 started at state ``seed ^ mix(stream)``."""
+    with np.errstate(over="ignore"):
+        base = np.uint64((seed ^ (stream * 0xD1B54A32D192ED03)) & 0xFFFFFFFFFFFFFFFF)
+        z = base + (np.arange(1, n + 1, dtype=np.uint64) * GAMMA)
+        z = (z ^ (z >> np.uint64(30))) * M1
+        z = (z ^ (z >> np.uint64(27))) * M2
+        return z ^ (z >> np.uint64(31))
+
+
+def uniform(seed: int, stream: int, n: int) -> np.ndarray:
+    return (splitmix64(seed, stream, n) >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+
+
+def base_genome(length: int, seed: int = DEFAULT_SEED) -> np.ndarray:
+    """Random ACGT digits (0..3) of a base genome."""
+    return (splitmix64(seed, 1, length) >> np.uint64(62)).astype(np.uint8)
+
+
+def variant(base: np.ndarray, index: int, snp: float, indel: float,
+            seed: int = DEFAULT_SEED) -> np.ndarray:
+    """One mutated copy of ``base`` (digits 0..3): SNPs then 1-10 bp indels."""
+    n = base.shape[0]
+    s = seed + 7919 * (index + 1)
+    g = base.copy()
+    if snp > 0:
+        u = uniform(s, 2, n)
+        pos = np.nonzero(u < snp)[0]
+        shift = (splitmix64(s, 3, pos.shape[0]) % np.uint64(3)).astype(np.uint8) + 1
+        g[pos] = (g[pos] + shift) & 3
+    if indel > 0:
+        u = uniform(s, 4, n)
+        pos = np.nonzero(u < indel)[0]
+        r = splitmix64(s, 5, pos.shape[0])
+        lens = (r % np.uint64(10)).astype(np.int64) + 1
+        ins = ((r >> np.uint64(8)) & np.uint64(1)).astype(bool)
+        # deletions: drop [p, p+len)
+        dpos, dlen = pos[~ins], lens[~ins]
+        keep = np.ones(n, dtype=bool)
+        if dpos.shape[0]:
+            idx = np.concatenate([np.arange(p, min(p + l, n)) for p, l in zip(dpos, dlen)])
+            keep[idx] = False
+        # insertions before position p (in original coordinates)
+        ipos, ilen = pos[ins], lens[ins]
+        if ipos.shape[0]:
+            total = int(ilen.sum())
+            ib = (splitmix64(s, 6, total) >> np.uint64(62)).astype(np.uint8)
+            offs = np.repeat(ipos, ilen)
+            out_idx = np.concatenate([np.nonzero(keep)[0], offs])
+            out_val = np.concatenate([g[keep], ib])
+            order = np.argsort(out_idx, kind="stable")
+            return out_val[order]
+        return g[keep]
+    return g
+
+
+def to_fasta_lines(name: bytes, digits: np.ndarray, width: int = 60) -> bytes:
+    """Format one record: ``>name\\n`` then ``width``-column lines with ``\\n``."""
+    seq = ACGT[digits]
+    n = seq.shape[0]
+    full = n // width
+    rem = n - full * width
+    body = np.empty(full * (width + 1) + (rem + 1 if rem else 0), dtype=np.uint8)
+    if full:
+        v = body[: full * (width + 1)].reshape(full, width + 1)
+        v[:, :width] = seq[: full * width].reshape(full, width)
+        v[:, width] = 10
+    if rem:
+        body[full * (width + 1): full * (width + 1) + rem] = seq[full * width:]
+        body[-1] = 10
+    return b">" + name + b"\n" + body.tobytes()
+
+
+def pangenome(n_genomes: int, genome_len: int, snp: float = 1e-3, indel: float = 1e-4,
+              seed: int = DEFAULT_SEED, first_index: int = 0,
+              records_per_genome: int = 1, width: int = 60) -> bytes:
+    """FASTA bytes of ``n_genomes`` variants of one base genome.
+
+    ``first_index`` lets ranks of a weak-scaling run draw disjoint genomes of the
+    same population (rank r uses indices r*n .. r*n+n-1).
+    """
+    base = base_genome(genome_len, seed)
+    parts = []
+    for gi in range(first_index, first_index + n_genomes):
+        v = variant(base, gi, snp, indel, seed)
+        if records_per_genome == 1:
+            parts.append(to_fasta_lines(b"g%d" % gi, v, width))
+        else:
+            cuts = np.linspace(0, v.shape[0], records_per_genome + 1).astype(np.int64)
+            for j in range(records_per_genome):
+                parts.append(to_fasta_lines(b"g%d_c%d" % (gi, j), v[cuts[j]:cuts[j + 1]], width))
+    return b"".join(parts)
+
+
+# Named workloads of BASELINE.json "configs" (SURVEY.md §8(d) table).
+CONFIGS = {
+    # C2: synthetic stand-in for E. coli K-12 MG1655 (4,641,652 bp) with 7 inserted
+    # 5 kb repeat copies (rRNA-operon-like).
+    "c2": dict(kind="ecoli", genome_len=4_641_652),
+    # C3: 100 x 5 Mbp variants, 0.1% SNP, 0.01% indels -> 0.5 Gbp.
+    "c3": dict(kind="pan", n_genomes=100, genome_len=5_000_000, snp=1e-3, indel=1e-4),
+    # C4: 1000 x 5 Mbp (5 Gbp), sharded 125 genomes per GPU at 8 GPUs.
+    "c4": dict(kind="pan", n_genomes=1000, genome_len=5_000_000, snp=1e-3, indel=1e-4),
+}
+
+
+def ecoli_like(length: int = 4_641_652, seed: int = DEFAULT_SEED, repeats: int = 7,
+               repeat_len: int = 5000) -> bytes:
+    g = base_genome(length - repeats * repeat_len, seed ^ 0xEC011)
+    rep = base_genome(repeat_len, seed ^ 0x5EE7)
+    cut = np.linspace(0, g.shape[0], repeats + 2).astype(np.int64)[1:-1]
+    parts, prev = [], 0
+    for c in cut:
+        parts += [g[prev:c], rep]
+        prev = c
+    parts.append(g[prev:])
+    return to_fasta_lines(b"NC_000913.3 synthetic E. coli K-12 MG1655 stand-in", np.concatenate(parts))
