@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Gbp/s of the k-mer -> rdBG build at k=27 on MI355X (BASELINE.json metric).
+
+One step = one pass of the hot path over this rank's synthetic pangenome
+shard, FASTA already resident in HBM: K1 parse -> K3 dBG insert (both
+strands, the reference's default -c 2) -> [N>1: owner all-to-all over RCCL
+and OR-merge] -> K5 degree scan + rdBG compaction, ending with the rdBG key
+count on the host.  Weak scaling: every rank owns the same number of genomes
+(C3 = 100 x 5 Mbp per GPU; 8 GPUs = 800 genomes, C4-scale).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK = 8.0e12         # MI355X HBM3E, B/s (MI355X_MICROARCH.md)
+K = 27
+
+
+def workload(config: str, rank: int, world: int):
+    from pangenome_amd import synth
+    if config == "c2":
+        return synth.ecoli_like(), "C2: synthetic E. coli K-12 stand-in, 4,641,652 bp, 1 record"
+    if config == "c3":
+        n = 100
+        return (synth.pangenome(n, 5_000_000, snp=1e-3, indel=1e-4, first_index=rank * n),
+                "C3: 100 x 5 Mbp variants (0.1%% SNP, 0.01%% indel) per GPU; %d genomes total" % (n * world))
+    if config == "c4":
+        n = 1000 // world
+        return (synth.pangenome(n, 5_000_000, snp=1e-3, indel=1e-4, first_index=rank * n),
+                "C4: 1000 x 5 Mbp variants sharded %d per GPU" % n)
+    if config == "small":
+        return synth.pangenome(10, 1_000_000, first_index=rank * 10), "small: 10 x 1 Mbp per GPU"
+    raise SystemExit("unknown --config %s" % config)
+
+
+def cpu_baseline(config: str):
+    """The oracle's faithful single-core restatement (same oakht hash, probe
+    sequence, growth and 3 probes per occurrence as kmer_numba.py) on a bounded
+    prefix of the same workload: ~10-30 s of CPU work."""
+    from oracle import oracle
+    from pangenome_amd import synth
+    if config == "c2":
+        fa, sample = synth.ecoli_like(), "whole C2 genome (4.64 Mbp)"
+    else:
+        g = 12
+        fa = synth.pangenome(g, 5_000_000, snp=1e-3, indel=1e-4)
+        sample = "first %d of the C3 genomes (%.0f Mbp), dBG + rdBG, k=27, -c 2" % (g, g * 5.0)
+    r = oracle.OracleRun(fa, K, 2)
+    t_dbg, t_rdbg = r.timings()
+    return {"value": r.n_bases() / (t_dbg + t_rdbg) / 1e9, "unit": "Gbp/s", "cores": 1, "kind": "port",
+            "sample": sample, "t_dbg_s": round(t_dbg, 3), "t_rdbg_s": round(t_rdbg, 3),
+            "cpu": _cpu_model(), "nproc": os.cpu_count()}
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d (launch N>1 with torch.distributed.run)" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=device)
+
+    from pangenome_amd._lib import Context
+    from pangenome_amd.dist import exchange_and_reduce
+
+    fasta, desc = workload(args.config, rank, world)
+    d_fasta = torch.frombuffer(bytearray(fasta), dtype=torch.uint8).to(device)
+    nbytes = len(fasta)
+    del fasta
+    torch.cuda.synchronize()
+    ctx = Context(K, local)
+
+    def step():
+        ctx.set_fasta_device(d_fasta.data_ptr(), nbytes, keepalive=d_fasta)
+        ctx.parse()
+        st_b = ctx.build_dbg(None, 0, True)
+        if world == 1:
+            st = ctx.build_rdbg()
+            return st_b, st, st.n_dbg, st.n_rdbg, 0
+        n_dbg, n_rdbg, _, sent = exchange_and_reduce(ctx, world, rank, device, bool(st_b.sentinel))
+        return st_b, ctx.stats(), n_dbg, n_rdbg, sent
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ins_ms, scan_ms, parse_ms = [], [], []
+    last = None
+    for _ in range(args.steps):
+        last = step()
+        ins_ms.append(last[0].ms_insert)
+        scan_ms.append(last[1].ms_scan)
+        parse_ms.append(last[0].ms_parse)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([last[0].n_bases, last[0].n_windows // 2, nbytes], dtype=torch.int64, device=device)
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        bases_all, wfw_all, bytes_all = [int(x) for x in tot.tolist()]
+    else:
+        bases_all, wfw_all, bytes_all = last[0].n_bases, last[0].n_windows // 2, nbytes
+
+    st_b, st_r, n_dbg, n_rdbg, sent = last
+    ms_step = 1e3 * elapsed / args.steps
+    value = bases_all * args.steps / elapsed / 1e9
+
+    # roofline of the dominant kernel, K3 k_insert (this rank): algorithmic
+    # bytes = 1 B class code per base + 20 B per forward window (8 B key + 2 B
+    # mask on each strand); duration = HIP events on the
+    # context's stream, averaged over the timed steps
+    ins_avg = float(np.mean(ins_ms))
+    ins_bytes = st_b.n_bases + 20 * (st_b.n_windows // 2)
+    achieved = ins_bytes / (ins_avg * 1e-3)
+    traffic = None
+    tp = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    if os.path.isfile(tp):
+        traffic = json.load(open(tp)).get("k_insert_hbm_bytes_per_launch")
+    # whole-path algorithmic fraction, SURVEY.md §8(d): F + 20 W + 10 D + 8 R
+    path_bytes = bytes_all + 20 * wfw_all + 10 * n_dbg + 8 * n_rdbg
+
+    out = {
+        "metric": "Gbp/s k-mer->rdBG build at k=27; bit-exact region table vs numba ref",
+        "value": round(value, 4),
+        "unit": "Gbp/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 pangenome generator, pangenome_amd/synth.py)",
+        "config": {"workload": desc, "k": K, "strands": "-c 2 (dBG both strands)",
+                   "bases_per_gpu": st_b.n_bases, "fasta_bytes_per_gpu": nbytes,
+                   "parallelism": "record-sharded, owner all-to-all" if world > 1 else "single GPU"},
+        "roofline": {"kernel": "k_insert (K3)", "bound": "hbm", "achieved": round(achieved / 1e9, 2),
+                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
+                     "traffic": traffic, "alg_bytes_per_launch": ins_bytes,
+                     "avg_launch_ms": round(ins_avg, 4)},
+        "path": {"alg_bytes": path_bytes, "frac_of_hbm": round(path_bytes / (elapsed / args.steps) /
+                                                             (world * HBM_PEAK), 5),
+                 "ms_parse": round(float(np.mean(parse_ms)), 3), "ms_insert": round(ins_avg, 3),
+                 "ms_scan": round(float(np.mean(scan_ms)), 3), "n_dbg": n_dbg, "n_rdbg": n_rdbg,
+                 "table_slots": st_b.table_capacity, "exchange_bytes_sent_rank0": sent},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.config)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,131 @@
+/*
+ * pangenome.h — C ABI of libpangenome_hip.so, the MI355X (gfx950) build of
+ * Rinoahu/pangenome's k-mer -> dBG -> rdBG -> region-table hot path.
+ *
+ * The reference (kmer_numba.py) has no FFI: its seams are Python functions.
+ * Each entry point below replaces one of them; the Python host
+ * (pangenome_amd/kmer.py) binds this header through ctypes and keeps the
+ * reference's CLI, file contracts and printing.  INTEGRATION.md shows the
+ * binding a maintainer of the reference would add.
+ *
+ * Conventions
+ *   - every int-returning call returns PG_OK (0) or a negative error code and
+ *     records a message for pg_last_error() (thread-local); no exception or
+ *     abort crosses the ABI;
+ *   - calls are synchronous: results are on the host (or in the caller's
+ *     device buffer) when they return;
+ *   - a pg_ctx owns all device working memory (one HIP stream on one device);
+ *     it is not re-entrant — use one per thread / per GPU;
+ *   - host arrays are caller-owned; `*_cap` arguments give their capacity in
+ *     elements and the call fails with PG_ERANGE if it is too small (query
+ *     sizes first with a NULL pointer where documented).
+ */
+#ifndef PANGENOME_H
+#define PANGENOME_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PG_OK 0
+#define PG_EINVAL (-22)
+#define PG_ENOMEM (-12)
+#define PG_ERANGE (-34)
+#define PG_EDEVICE (-5)
+
+typedef struct pg_ctx pg_ctx;
+
+/* What one build did, for throughput and roofline accounting.  Kernel times
+ * are HIP-event durations on the context's stream. */
+typedef struct pg_stats {
+  uint64_t n_bytes;        /* FASTA bytes parsed                                  */
+  uint64_t n_records;      /* records (header lines)                              */
+  uint64_t n_bases;        /* sequence bases over all records (forward strand)     */
+  uint64_t n_windows;      /* k-mer windows inserted (both strands when rc)        */
+  uint64_t n_dbg;          /* dBG keys (reference's non-canonical count)           */
+  uint64_t n_rdbg;         /* rdBG keys                                            */
+  uint64_t n_slots;        /* occupied canonical slots                             */
+  uint64_t table_capacity; /* slots in the device hash table                       */
+  double ms_parse;         /* K1 wall (host-timed, includes its small D2H syncs)  */
+  double ms_clear;         /* table memset                                        */
+  double ms_insert;        /* K3 k_insert                                         */
+  double ms_scan;          /* K5 k_reduce                                         */
+  uint64_t sentinel;       /* 1 if the n<k key (2^64-1) is in the dBG              */
+} pg_stats;
+
+/* Context on HIP device `device` for k-mer length k (clamped to [1, 27] as
+ * seq2rdbg does, kmer_numba.py:1236). */
+int pg_create(pg_ctx** out, int device, int k);
+void pg_destroy(pg_ctx* ctx);
+const char* pg_last_error(void);
+int pg_get_k(const pg_ctx* ctx);
+
+/* ---- input: the mmapped FASTA the reference reads with seq2bytes
+ *      (kmer_numba.py:117-119).  Host bytes are copied to HBM; device bytes
+ *      (16-byte aligned) are used in place and must outlive the parse. */
+int pg_set_fasta(pg_ctx* ctx, const uint8_t* host_bytes, uint64_t nbytes);
+int pg_set_fasta_device(pg_ctx* ctx, const uint8_t* device_bytes, uint64_t nbytes);
+
+/* K1: readline_jit_ + seqio_jit_ (kmer_numba.py:122-172) on the device. */
+int pg_parse(pg_ctx* ctx, uint64_t* n_records, uint64_t* n_bases);
+/* Per-record table (arrays of n_records): compacted sequence length, header
+ * byte span (qid = bytes[hdr_start : hdr_start+hdr_len], '>' included,
+ * :160) and seqio's resume pointer (:153). Any pointer may be NULL. */
+int pg_records(const pg_ctx* ctx, int64_t* seq_len, int64_t* hdr_start, int64_t* hdr_len, int64_t* ptr);
+
+/* K3: seq2rdbg's dBG pass (kmer_numba.py:1234-1268 -> seq2dbg_jit_ :1202-1230
+ * -> build_dbg :1052-1090 -> add_kmer :1036-1047).  rec_flags (NULL = all)
+ * holds one byte per record: bit0 = record is part of the pass (the host
+ * applies -n and the checkpoint/resume rules); extra_empty = number of extra
+ * empty records the reference's resume yields (each adds the n<k sentinel).
+ * rc0 != 0 inserts the reverse strand too (-c bit 1, :2110). */
+int pg_build_dbg(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0, pg_stats* stats);
+
+/* K5: dbg2rdbg (kmer_numba.py:1313-1321 -> build_rdbg_jit_ :1292-1309).
+ * Marks members in the device table and materialises the rdBG keys. */
+int pg_build_rdbg(pg_ctx* ctx, uint64_t* n_rdbg, pg_stats* stats);
+
+/* dump()'s keys/values (kmer_numba.py:243-261) of the dBG, unordered.
+ * keys == NULL: only *n is set. */
+int pg_dbg_export(pg_ctx* ctx, uint64_t* keys, uint16_t* masks, uint64_t cap, uint64_t* n);
+/* rdBG keys, unordered. keys == NULL: only *n is set. */
+int pg_rdbg_export(pg_ctx* ctx, uint64_t* keys, uint64_t cap, uint64_t* n);
+
+/* ---- multi-GPU exchange (one process per GPU; the caller moves the bytes
+ *      with RCCL).  Replaces nothing in the reference, which is single-core. */
+/* Owner-partition this rank's local dBG into `nparts` contiguous runs of
+ * 16-byte records (d_out device buffer, capacity out_cap records).
+ * counts[nparts] receives run lengths; d_out == NULL only counts. */
+int pg_dbg_partition(pg_ctx* ctx, int nparts, void* d_out, uint64_t out_cap, uint64_t* counts);
+/* OR-merge received 16-byte records (device pointer) into a fresh owner
+ * table; sentinel != 0 adds the n<k key.  Follow with pg_build_rdbg. */
+int pg_dbg_merge(pg_ctx* ctx, const void* d_records, uint64_t n, uint64_t capacity_hint, int sentinel);
+
+/* ---- edge pass: rdbg_edge_weight_jit_ (kmer_numba.py:1808-1827) ->
+ *      rdbg_edge_weight (:1446-1518).  rec_flags as above (walked records);
+ *      rc1 != 0 also walks the reverse strand (-c bit 0, :2141). */
+int pg_edges(pg_ctx* ctx, const uint8_t* rec_flags, int rc1, uint64_t* n_edges);
+/* Edges ordered by first occurrence: 4 x uint64 (n0, v0, n1, v1) per edge,
+ * the number of walks containing it, and the walk of its first occurrence
+ * (2 * record + strand) — what the host needs to emulate the order reversal
+ * of the reference's dump/reload checkpoints (kmer_numba.py:1881-1887). */
+int pg_edges_export(pg_ctx* ctx, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap);
+
+/* ---- region rows: seqs2path_jit_ (kmer_numba.py:1830-1849) -> seq2path_jit_
+ *      (:1523-1573).  Labels are the host-built label_dct (:1918-1944):
+ *      (key, value) -> label. */
+int pg_set_labels(pg_ctx* ctx, const int64_t* key, const int64_t* value, const int64_t* label, uint64_t n);
+int pg_rows(pg_ctx* ctx, const uint8_t* rec_flags, int rc1, uint64_t* n_rows);
+/* rows: 5 x int64 per row (record index, start, end, strand +1/-1, label),
+ * in print order. */
+int pg_rows_export(pg_ctx* ctx, int64_t* rows5, uint64_t cap);
+
+/* Timings and counters of the last build (see pg_stats). */
+int pg_get_stats(const pg_ctx* ctx, pg_stats* stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PANGENOME_H */

@@ -1,0 +1,212 @@
+"""ctypes binding of include/pangenome.h (libpangenome_hip.so).
+
+There is no CPU fallback: if the in-tree HIP library is missing or no HIP
+device is usable, every call raises.  Build it with ``python -c "import
+__graft_entry__ as g; g.build()"`` (or ``make -C pangenome_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpangenome_hip.so")
+
+PG_OK = 0
+
+
+class PgStats(C.Structure):
+    _fields_ = [
+        ("n_bytes", C.c_uint64), ("n_records", C.c_uint64), ("n_bases", C.c_uint64),
+        ("n_windows", C.c_uint64), ("n_dbg", C.c_uint64), ("n_rdbg", C.c_uint64),
+        ("n_slots", C.c_uint64), ("table_capacity", C.c_uint64),
+        ("ms_parse", C.c_double), ("ms_clear", C.c_double), ("ms_insert", C.c_double),
+        ("ms_scan", C.c_double), ("sentinel", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# every symbol include/pangenome.h declares, with (restype, argtypes)
+_P, _U8P, _U64P = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)
+_I64P, _U16P = C.POINTER(C.c_int64), C.POINTER(C.c_uint16)
+_SP = C.POINTER(PgStats)
+SIGNATURES = {
+    "pg_create": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int]),
+    "pg_destroy": (None, [_P]),
+    "pg_last_error": (C.c_char_p, []),
+    "pg_get_k": (C.c_int, [_P]),
+    "pg_set_fasta": (C.c_int, [_P, _P, C.c_uint64]),
+    "pg_set_fasta_device": (C.c_int, [_P, _P, C.c_uint64]),
+    "pg_parse": (C.c_int, [_P, _U64P, _U64P]),
+    "pg_records": (C.c_int, [_P, _P, _P, _P, _P]),
+    "pg_build_dbg": (C.c_int, [_P, _P, C.c_int, C.c_int, _SP]),
+    "pg_build_rdbg": (C.c_int, [_P, _U64P, _SP]),
+    "pg_dbg_export": (C.c_int, [_P, _P, _P, C.c_uint64, _U64P]),
+    "pg_rdbg_export": (C.c_int, [_P, _P, C.c_uint64, _U64P]),
+    "pg_dbg_partition": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
+    "pg_dbg_merge": (C.c_int, [_P, _P, C.c_uint64, C.c_uint64, C.c_int]),
+    "pg_edges": (C.c_int, [_P, _P, C.c_int, _U64P]),
+    "pg_edges_export": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
+    "pg_set_labels": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
+    "pg_rows": (C.c_int, [_P, _P, C.c_int, _U64P]),
+    "pg_rows_export": (C.c_int, [_P, _P, C.c_uint64]),
+    "pg_get_stats": (C.c_int, [_P, _SP]),
+}
+
+_lib = None
+
+
+class PangenomeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the in-tree HIP library (raises if it is not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.isfile(LIB_PATH):
+            raise ImportError(
+                "libpangenome_hip.so is not built (%s); run __graft_entry__.build() "
+                "or `make -C pangenome_amd/csrc` — there is no CPU fallback" % LIB_PATH)
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str):
+    if rc != PG_OK:
+        msg = load().pg_last_error()
+        raise PangenomeError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else "?"))
+
+
+def ptr(a: np.ndarray | None):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One pg_ctx: one HIP device, one stream, all device buffers."""
+
+    def __init__(self, k: int, device: int = 0):
+        self.lib = load()
+        h = C.c_void_p()
+        check(self.lib.pg_create(C.byref(h), device, k), "pg_create")
+        self.h = h
+        self.k = self.lib.pg_get_k(h)
+        self.n_records = 0
+        self.n_bases = 0
+        self._keepalive = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.pg_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- input
+    def set_fasta(self, data):
+        """Host bytes (bytes / bytearray / np.uint8 array / mmap)."""
+        arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        check(self.lib.pg_set_fasta(self.h, ptr(arr), arr.shape[0]), "pg_set_fasta")
+
+    def set_fasta_device(self, dev_ptr: int, nbytes: int, keepalive=None):
+        self._keepalive = keepalive
+        check(self.lib.pg_set_fasta_device(self.h, C.c_void_p(dev_ptr), nbytes), "pg_set_fasta_device")
+
+    def parse(self):
+        nr, nb = C.c_uint64(), C.c_uint64()
+        check(self.lib.pg_parse(self.h, C.byref(nr), C.byref(nb)), "pg_parse")
+        self.n_records, self.n_bases = nr.value, nb.value
+        return self.n_records, self.n_bases
+
+    def records(self):
+        R = self.n_records
+        out = [np.empty(R, np.int64) for _ in range(4)]
+        check(self.lib.pg_records(self.h, *[ptr(a) for a in out]), "pg_records")
+        return dict(seq_len=out[0], hdr_start=out[1], hdr_len=out[2], ptr=out[3])
+
+    # ---------------------------------------------------------------- dBG
+    def build_dbg(self, rec_flags=None, extra_empty: int = 0, rc0: bool = True) -> PgStats:
+        st = PgStats()
+        f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
+        check(self.lib.pg_build_dbg(self.h, ptr(f), int(extra_empty), int(bool(rc0)), C.byref(st)),
+              "pg_build_dbg")
+        return st
+
+    def build_rdbg(self) -> PgStats:
+        st = PgStats()
+        n = C.c_uint64()
+        check(self.lib.pg_build_rdbg(self.h, C.byref(n), C.byref(st)), "pg_build_rdbg")
+        return st
+
+    def stats(self) -> PgStats:
+        st = PgStats()
+        check(self.lib.pg_get_stats(self.h, C.byref(st)), "pg_get_stats")
+        return st
+
+    def dbg(self):
+        n = C.c_uint64()
+        check(self.lib.pg_dbg_export(self.h, None, None, 0, C.byref(n)), "pg_dbg_export")
+        keys = np.empty(n.value, np.uint64)
+        masks = np.empty(n.value, np.uint16)
+        check(self.lib.pg_dbg_export(self.h, ptr(keys), ptr(masks), n.value, C.byref(n)), "pg_dbg_export")
+        o = np.argsort(keys, kind="stable")
+        return keys[o], masks[o]
+
+    def rdbg(self):
+        n = C.c_uint64()
+        check(self.lib.pg_rdbg_export(self.h, None, 0, C.byref(n)), "pg_rdbg_export")
+        keys = np.empty(n.value, np.uint64)
+        check(self.lib.pg_rdbg_export(self.h, ptr(keys), n.value, C.byref(n)), "pg_rdbg_export")
+        return np.sort(keys)
+
+    # ------------------------------------------------------ multi-GPU hooks
+    def partition(self, nparts: int, d_out: int | None = None, out_cap: int = 0):
+        counts = np.zeros(nparts, np.uint64)
+        check(self.lib.pg_dbg_partition(self.h, nparts, None if d_out is None else C.c_void_p(d_out),
+                                        out_cap, ptr(counts)), "pg_dbg_partition")
+        return counts
+
+    def merge(self, d_records: int, n: int, capacity_hint: int = 0, sentinel: bool = False):
+        check(self.lib.pg_dbg_merge(self.h, C.c_void_p(d_records) if n else None, n, capacity_hint,
+                                    int(bool(sentinel))), "pg_dbg_merge")
+
+    # -------------------------------------------------------------- walks
+    def edges(self, rec_flags=None, rc1: bool = False):
+        n = C.c_uint64()
+        f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
+        check(self.lib.pg_edges(self.h, ptr(f), int(bool(rc1)), C.byref(n)), "pg_edges")
+        m = n.value
+        t = np.empty((m, 4), np.uint64)
+        cnt = np.empty(m, np.int64)
+        walk = np.empty(m, np.int64)
+        if m:
+            check(self.lib.pg_edges_export(self.h, ptr(t), ptr(cnt), ptr(walk), m), "pg_edges_export")
+        return t, cnt, walk
+
+    def set_labels(self, keys, vals, ids):
+        keys = np.ascontiguousarray(keys, np.int64)
+        vals = np.ascontiguousarray(vals, np.int64)
+        ids = np.ascontiguousarray(ids, np.int64)
+        check(self.lib.pg_set_labels(self.h, ptr(keys), ptr(vals), ptr(ids), keys.shape[0]), "pg_set_labels")
+
+    def rows(self, rec_flags=None, rc1: bool = False):
+        n = C.c_uint64()
+        f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
+        check(self.lib.pg_rows(self.h, ptr(f), int(bool(rc1)), C.byref(n)), "pg_rows")
+        out = np.empty((n.value, 5), np.int64)
+        if n.value:
+            check(self.lib.pg_rows_export(self.h, ptr(out), n.value), "pg_rows_export")
+        return out

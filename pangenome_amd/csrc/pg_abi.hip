@@ -1,0 +1,260 @@
+// pg_abi.hip — extern "C" entry points of include/pangenome.h.
+#include <chrono>
+#include <cstring>
+#include <string>
+
+#include "../../include/pangenome.h"
+#include "pg_internal.h"
+
+struct pg_ctx {
+  pg::Ctx c;
+};
+
+static thread_local std::string g_err;
+
+template <class F>
+static int guard(F&& f) {
+  try {
+    f();
+    return PG_OK;
+  } catch (const pg::Error& e) {
+    g_err = e.what();
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_err = "out of host memory";
+    return PG_ENOMEM;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return PG_EDEVICE;
+  }
+}
+
+static void fill_stats(const pg::Ctx& c, pg_stats* s) {
+  if (!s) return;
+  s->n_bytes = c.n_bytes;
+  s->n_records = c.n_records;
+  s->n_bases = c.n_bases;
+  s->n_windows = c.windows_total;
+  s->n_dbg = c.n_dbg;
+  s->n_rdbg = c.n_rdbg;
+  s->n_slots = c.n_canon;
+  s->table_capacity = c.cap;
+  s->ms_parse = c.ms_parse;
+  s->ms_clear = c.ms_clear;
+  s->ms_insert = c.ms_insert;
+  s->ms_scan = c.ms_scan;
+  s->sentinel = c.sentinel;
+}
+
+extern "C" {
+
+const char* pg_last_error(void) { return g_err.c_str(); }
+
+int pg_create(pg_ctx** out, int device, int k) {
+  return guard([&] {
+    if (!out) throw pg::Error(PG_EINVAL, "pg_create: out is NULL");
+    int n = 0;
+    PG_HIP(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) throw pg::Error(PG_EINVAL, "pg_create: no HIP device " + std::to_string(device));
+    PG_HIP(hipSetDevice(device));
+    auto* x = new pg_ctx();
+    x->c.device = device;
+    x->c.k = k < 1 ? 1 : (k > 27 ? 27 : k);
+    PG_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
+    *out = x;
+  });
+}
+
+void pg_destroy(pg_ctx* x) {
+  if (!x) return;
+  pg::Ctx& c = x->c;
+  (void)hipSetDevice(c.device);
+  (void)hipStreamSynchronize(c.stream);
+  pg::DevBuf* bufs[] = {&c.fasta_own, &c.blk_nl, &c.blk_nl_off, &c.nl_pos, &c.line_start, &c.line_off,
+                        &c.line_contrib, &c.line_hdr, &c.hdr_lines, &c.n_sel, &c.rec_start, &c.rec_len,
+                        &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.flags,
+                        &c.rdbg_keys, &c.tiles, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
+                        &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt};
+  for (auto* b : bufs) b->release();
+  c.t0.destroy();
+  c.t1.destroy();
+  (void)hipStreamDestroy(c.stream);
+  delete x;
+}
+
+int pg_get_k(const pg_ctx* x) { return x ? x->c.k : -1; }
+
+int pg_set_fasta(pg_ctx* x, const uint8_t* host, uint64_t n) {
+  return guard([&] {
+    if (!x || (!host && n)) throw pg::Error(PG_EINVAL, "pg_set_fasta: bad arguments");
+    pg::Ctx& c = x->c;
+    PG_HIP(hipSetDevice(c.device));
+    c.fasta_own.reserve(n + 64);
+    if (n) PG_HIP(hipMemcpyAsync(c.fasta_own.p, host, n, hipMemcpyHostToDevice, c.stream));
+    c.sync();
+    c.d_fasta = c.fasta_own.as<uint8_t>();
+    c.n_bytes = n;
+    c.parsed = c.built = c.reduced = false;
+  });
+}
+
+int pg_set_fasta_device(pg_ctx* x, const uint8_t* dev, uint64_t n) {
+  return guard([&] {
+    if (!x || (!dev && n)) throw pg::Error(PG_EINVAL, "pg_set_fasta_device: bad arguments");
+    pg::Ctx& c = x->c;
+    PG_HIP(hipSetDevice(c.device));
+    if (reinterpret_cast<uintptr_t>(dev) % 16 != 0) {
+      c.fasta_own.reserve(n + 64);
+      PG_HIP(hipMemcpyAsync(c.fasta_own.p, dev, n, hipMemcpyDeviceToDevice, c.stream));
+      c.sync();
+      c.d_fasta = c.fasta_own.as<uint8_t>();
+    } else {
+      c.d_fasta = dev;
+    }
+    c.n_bytes = n;
+    c.parsed = c.built = c.reduced = false;
+  });
+}
+
+int pg_parse(pg_ctx* x, uint64_t* n_records, uint64_t* n_bases) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_parse: ctx is NULL");
+    pg::Ctx& c = x->c;
+    PG_HIP(hipSetDevice(c.device));
+    if (!c.d_fasta && c.n_bytes) throw pg::Error(PG_EINVAL, "pg_parse: no FASTA set");
+    auto t0 = std::chrono::steady_clock::now();
+    pg::parse_fasta(c);
+    c.ms_parse = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c.built = c.reduced = false;
+    if (n_records) *n_records = c.n_records;
+    if (n_bases) *n_bases = c.n_bases;
+  });
+}
+
+int pg_records(const pg_ctx* x, int64_t* seq_len, int64_t* hdr_start, int64_t* hdr_len, int64_t* ptr) {
+  return guard([&] {
+    if (!x || !x->c.parsed) throw pg::Error(PG_EINVAL, "pg_records: not parsed");
+    const pg::Ctx& c = x->c;
+    const size_t R = c.n_records;
+    if (seq_len && R) std::memcpy(seq_len, c.h_rec_len.data(), 8 * R);
+    if (hdr_start && R) std::memcpy(hdr_start, c.h_rec_hdr_start.data(), 8 * R);
+    if (hdr_len && R) std::memcpy(hdr_len, c.h_rec_hdr_len.data(), 8 * R);
+    if (ptr && R) std::memcpy(ptr, c.h_rec_ptr.data(), 8 * R);
+  });
+}
+
+int pg_build_dbg(pg_ctx* x, const uint8_t* rec_flags, int extra_empty, int rc0, pg_stats* stats) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_build_dbg: ctx is NULL");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::build_dbg(x->c, rec_flags, extra_empty, rc0 != 0);
+    fill_stats(x->c, stats);
+  });
+}
+
+int pg_build_rdbg(pg_ctx* x, uint64_t* n_rdbg, pg_stats* stats) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_build_rdbg: ctx is NULL");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::build_rdbg(x->c);
+    if (n_rdbg) *n_rdbg = x->c.n_rdbg;
+    fill_stats(x->c, stats);
+  });
+}
+
+int pg_get_stats(const pg_ctx* x, pg_stats* stats) {
+  return guard([&] {
+    if (!x || !stats) throw pg::Error(PG_EINVAL, "pg_get_stats: bad arguments");
+    fill_stats(x->c, stats);
+  });
+}
+
+int pg_dbg_export(pg_ctx* x, uint64_t* keys, uint16_t* masks, uint64_t cap, uint64_t* n) {
+  return guard([&] {
+    if (!x || !n) throw pg::Error(PG_EINVAL, "pg_dbg_export: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    const uint64_t total = pg::export_dbg(x->c, nullptr, nullptr, 0);
+    *n = total;
+    if (keys) {
+      if (cap < total || !masks) throw pg::Error(PG_ERANGE, "pg_dbg_export: buffer too small");
+      pg::export_dbg(x->c, keys, masks, cap);
+    }
+  });
+}
+
+int pg_rdbg_export(pg_ctx* x, uint64_t* keys, uint64_t cap, uint64_t* n) {
+  return guard([&] {
+    if (!x || !n) throw pg::Error(PG_EINVAL, "pg_rdbg_export: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    *n = pg::export_rdbg(x->c, nullptr, 0);
+    if (keys) {
+      if (cap < *n) throw pg::Error(PG_ERANGE, "pg_rdbg_export: buffer too small");
+      pg::export_rdbg(x->c, keys, cap);
+    }
+  });
+}
+
+int pg_dbg_partition(pg_ctx* x, int nparts, void* d_out, uint64_t out_cap, uint64_t* counts) {
+  return guard([&] {
+    if (!x || !counts) throw pg::Error(PG_EINVAL, "pg_dbg_partition: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    const uint64_t total = pg::partition_dbg(x->c, nparts, nullptr, 0, counts);
+    if (d_out) {
+      if (out_cap < total) throw pg::Error(PG_ERANGE, "pg_dbg_partition: output too small");
+      pg::partition_dbg(x->c, nparts, d_out, out_cap, counts);
+    }
+  });
+}
+
+int pg_dbg_merge(pg_ctx* x, const void* d_records, uint64_t n, uint64_t cap_hint, int sentinel) {
+  return guard([&] {
+    if (!x || (!d_records && n)) throw pg::Error(PG_EINVAL, "pg_dbg_merge: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::merge_dbg(x->c, d_records, n, cap_hint, sentinel);
+  });
+}
+
+int pg_edges(pg_ctx* x, const uint8_t* rec_flags, int rc1, uint64_t* n_edges) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_edges: ctx is NULL");
+    PG_HIP(hipSetDevice(x->c.device));
+    const uint64_t n = pg::walk_edges(x->c, rec_flags, rc1 != 0);
+    if (n_edges) *n_edges = n;
+  });
+}
+
+int pg_edges_export(pg_ctx* x, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap) {
+  return guard([&] {
+    if (!x || !tuples || !counts || !first_walk) throw pg::Error(PG_EINVAL, "pg_edges_export: bad arguments");
+    if (cap < x->c.n_edges) throw pg::Error(PG_ERANGE, "pg_edges_export: buffer too small");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::export_edges(x->c, tuples, counts, first_walk, cap);
+  });
+}
+
+int pg_set_labels(pg_ctx* x, const int64_t* key, const int64_t* value, const int64_t* label, uint64_t n) {
+  return guard([&] {
+    if (!x || (n && (!key || !value || !label))) throw pg::Error(PG_EINVAL, "pg_set_labels: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::set_labels(x->c, key, value, label, n);
+  });
+}
+
+int pg_rows(pg_ctx* x, const uint8_t* rec_flags, int rc1, uint64_t* n_rows) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_rows: ctx is NULL");
+    PG_HIP(hipSetDevice(x->c.device));
+    const uint64_t n = pg::walk_rows(x->c, rec_flags, rc1 != 0);
+    if (n_rows) *n_rows = n;
+  });
+}
+
+int pg_rows_export(pg_ctx* x, int64_t* rows5, uint64_t cap) {
+  return guard([&] {
+    if (!x || !rows5) throw pg::Error(PG_EINVAL, "pg_rows_export: bad arguments");
+    if (cap < x->c.n_rows) throw pg::Error(PG_ERANGE, "pg_rows_export: buffer too small");
+    if (x->c.n_rows) std::memcpy(rows5, x->c.h_rows.data(), 8 * 5 * x->c.n_rows);
+  });
+}
+
+}  // extern "C"

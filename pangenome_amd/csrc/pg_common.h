@@ -1,0 +1,102 @@
+// pg_common.h — device-side encoding, table layout and hashing shared by the
+// pangenome HIP kernels (gfx950 / CDNA4, wave64).
+//
+// Byte classes.  The reference looks every sequence byte up in three 256-entry
+// tables: the base-5 digit `alpha` (kmer_numba.py:763-768), the neighbour mask
+// `lastc` (:736-743) and, for the reverse strand, `lastc[tab_rev_bytes[b]]`
+// (:191-195).  All three are functions of seven byte classes, so the parse
+// kernel rewrites the FASTA into one class code per base and every later
+// kernel derives digits and masks from the code with packed-constant shifts
+// (no table loads on the hot path).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace pg {
+
+enum : uint8_t {
+  CLS_A = 0,      // A a
+  CLS_C = 1,      // C c
+  CLS_G = 2,      // G g
+  CLS_T = 3,      // T t
+  CLS_N = 4,      // N n
+  CLS_DOLLAR = 5, // '$'  (lastc 32; its reverse complement is 'N')
+  CLS_OTHER = 6,  // anything else: IUPAC, '\r', '#', ... (lastc 0, digit 4, RC 'N')
+};
+
+// alpha digit per class: A0 C2 G1 T3, others 4
+__host__ __device__ __forceinline__ uint32_t digit_fw(uint32_t c) { return (0x04443120u >> (4u * c)) & 0xFu; }
+// alpha of tab_rev(byte): A->T 3, C->G 1, G->C 2, T->A 0, others 4
+__host__ __device__ __forceinline__ uint32_t digit_rc(uint32_t c) { return (0x04440213u >> (4u * c)) & 0xFu; }
+// lastc per class: A1 C8 G4 T2 N16 $32 other0
+__host__ __device__ __forceinline__ uint32_t lam_fw(uint32_t c) {
+  return (uint32_t)((0x0000201002040801ull >> (8u * c)) & 0xFFu);
+}
+// lastc of tab_rev(byte): A->T 2, C->G 4, G->C 8, T->A 1, N/$/other -> N 16
+__host__ __device__ __forceinline__ uint32_t lam_rc(uint32_t c) {
+  return (uint32_t)((0x0010101001080402ull >> (8u * c)) & 0xFFu);
+}
+// class of tab_rev(byte) (used for the explicit reverse strand of short records)
+__host__ __device__ __forceinline__ uint32_t comp_class(uint32_t c) {
+  return (0x04440123u >> (4u * c)) & 0xFu;   // A->T C->G G->C T->A, N/$/other -> N
+}
+
+constexpr int OFFBIT = 6;        // offbit (:745): dBG masks and label lookups
+constexpr int EDGE_OFFBIT = 5;   // :1814 passes bits(=5) into rdbg_edge_weight's offbit
+constexpr uint32_t LAM_DOLLAR = 32;   // '$' end marker
+constexpr uint32_t LAM_HASH = 0;      // '#' start marker
+constexpr uint64_t SENTINEL = ~0ull;  // the n<k key (-1 stored in a uint64 array, :1038)
+
+// ------------------------------------------------------------------ table
+// One canonical k-mer per 16-byte slot.  A key X and its reverse complement
+// rc(X) share the slot of c = min(X, rc(X)); the slot keeps the reference's
+// 12-bit OR-mask of each orientation separately (A for c, B for rc(c)), so the
+// dBG exported from it is exactly the reference's non-canonical dBG
+// (kmer_numba.py:1036-1047, :1215-1221).  key1 = c + 1, so an all-zero slot is
+// empty and the table is cleared by one memset (c < 5^27 < 2^63).
+struct alignas(16) Slot {
+  unsigned long long key1;
+  unsigned int mask;   // [0,12) A | 1<<12 presA | 1<<13 rdbgA | [16,28) B | 1<<28 presB | 1<<29 rdbgB
+  unsigned int aux;
+};
+constexpr uint32_t PRES_A = 1u << 12, RDBG_A = 1u << 13;
+constexpr uint32_t PRES_B = 1u << 28, RDBG_B = 1u << 29;
+constexpr uint32_t MASK12 = 0xFFFu;
+
+__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
+  k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// modular inverse of 5 mod 2^64: (K - d) is a multiple of 5 when d is K's low
+// base-5 digit, so K / 5 == (K - d) * INV5 exactly, with one 64-bit multiply
+constexpr uint64_t INV5 = 0xCCCCCCCCCCCCCCCDull;
+
+__host__ __device__ __forceinline__ uint64_t pow5(int e) {
+  uint64_t r = 1;
+  for (int i = 0; i < e; ++i) r *= 5;
+  return r;
+}
+
+// reverse complement of a base-5 key of k digits (digit j has weight 5^j)
+__host__ __device__ __forceinline__ uint64_t rc_key(uint64_t x, int k) {
+  uint64_t r = 0;
+  for (int j = 0; j < k; ++j) {
+    uint64_t q = x / 5;
+    uint32_t d = (uint32_t)(x - q * 5);
+    x = q;
+    uint32_t rd = d < 4 ? 3u - d : 4u;
+    r = r * 5 + rd;
+  }
+  return r;
+}
+
+// rdBG rule (build_rdbg_jit_ :1300-1305): drop iff exactly one predecessor
+// bit and exactly one successor bit
+__host__ __device__ __forceinline__ bool rdbg_member(uint32_t m12) {
+  return !(__builtin_popcount(m12 >> OFFBIT) == 1 && __builtin_popcount(m12 & 63u) == 1);
+}
+
+}  // namespace pg

@@ -1,0 +1,156 @@
+// pg_internal.h — host-side context shared by the pangenome HIP translation
+// units.  Not part of the public ABI (include/pangenome.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pg_common.h"
+
+namespace pg {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define PG_HIP(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e_ = (x);                                                                \
+    if (e_ != hipSuccess)                                                               \
+      throw ::pg::Error(-5, std::string(#x) + ": " + hipGetErrorString(e_));            \
+  } while (0)
+
+// A growable device buffer (never shrinks; reused across calls so the steady
+// state does no hipMalloc).
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void reserve(size_t bytes) {
+    if (bytes <= cap) return;
+    if (p) PG_HIP(hipFree(p));
+    p = nullptr;
+    size_t nb = bytes + bytes / 8 + 256;
+    PG_HIP(hipMalloc(&p, nb));
+    cap = nb;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+// Per-kernel timing on the context's stream (HIP events), so callers can
+// price the dominant kernel against the HBM roofline.
+struct Timer {
+  hipEvent_t a = nullptr, b = nullptr;
+  void init() {
+    if (!a) { PG_HIP(hipEventCreate(&a)); PG_HIP(hipEventCreate(&b)); }
+  }
+  void start(hipStream_t s) { PG_HIP(hipEventRecord(a, s)); }
+  void stop(hipStream_t s) { PG_HIP(hipEventRecord(b, s)); }
+  double ms() {
+    float t = 0;
+    PG_HIP(hipEventSynchronize(b));
+    PG_HIP(hipEventElapsedTime(&t, a, b));
+    return (double)t;
+  }
+  void destroy() {
+    if (a) { (void)hipEventDestroy(a); (void)hipEventDestroy(b); }
+    a = b = nullptr;
+  }
+};
+
+struct Ctx {
+  int device = 0;
+  int k = 27;
+  hipStream_t stream = nullptr;
+
+  // ---- input FASTA (device-resident; either owned or borrowed)
+  DevBuf fasta_own;
+  const uint8_t* d_fasta = nullptr;
+  uint64_t n_bytes = 0;
+
+  // ---- parse products (K1)
+  DevBuf blk_nl, blk_nl_off;      // per-chunk newline counts / offsets
+  DevBuf nl_pos;                  // newline (line terminator) positions, int64
+  DevBuf line_start, line_off, line_contrib;   // per line
+  DevBuf line_hdr;                // uint8 per line: header flag
+  DevBuf hdr_lines;               // int64 line index of each record header
+  DevBuf n_sel;                   // device counters
+  DevBuf rec_start, rec_len;      // int64 per record: compacted offset / length
+  DevBuf rec_hdr, rec_ptr;        // int64 per record: header byte span packed, `ptr` emulation
+  DevBuf rec_flag;                // uint8 per record: take part in the current pass
+  DevBuf cls;                     // uint8 per base: class code (records concatenated)
+  DevBuf scratch;                 // rocPRIM temp storage
+  uint64_t n_lines = 0, n_records = 0, n_bases = 0, n_nl = 0;
+  std::vector<int64_t> h_rec_start, h_rec_len, h_rec_hdr_start, h_rec_hdr_len, h_rec_ptr;
+  bool parsed = false;
+
+  // ---- dBG table (K3) and rdBG (K5)
+  DevBuf table;
+  uint64_t cap = 0;               // slots (power of two)
+  uint64_t cap_hint = 0;          // learned from the previous build
+  DevBuf flags;                   // [0] sentinel seen, [1] overflow, [2..] counters
+  DevBuf rdbg_keys;
+  uint64_t n_dbg = 0, n_rdbg = 0, n_canon = 0, sentinel = 0;
+  bool built = false, reduced = false;
+  int rc0 = 1;
+  uint64_t windows_fw = 0, windows_total = 0;
+
+  // ---- walk passes (edges / labels)
+  DevBuf tiles;                   // per-record tiles for ordered compaction
+  DevBuf tile_cnt, tile_off;      // per tile x strand counts / offsets
+  DevBuf occ;                     // member / hit occurrences, walk ordered
+  DevBuf edge_tab, pair_tab;      // edge table and (edge, walk) dedup set
+  DevBuf edge_out;
+  uint64_t edge_cap = 0, pair_cap = 0, n_edges = 0;
+  DevBuf lab_tab;                 // label table
+  uint64_t lab_cap = 0;
+  DevBuf walk_hits_off, rows_buf, rows_cnt;
+  uint64_t n_rows = 0;
+  std::vector<int64_t> h_rows;    // rec, start, end, strand, label
+
+  // timings of the last calls (ms, HIP events on `stream`)
+  Timer t0, t1;
+  double ms_parse = 0, ms_clear = 0, ms_insert = 0, ms_short = 0, ms_scan = 0;
+  double ms_total_build = 0;
+
+  void sync() { PG_HIP(hipStreamSynchronize(stream)); }
+};
+
+// pg_parse.hip
+void parse_fasta(Ctx& c);
+// pg_dbg.hip
+void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0);
+void build_rdbg(Ctx& c);
+uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap);
+uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap);
+uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts);
+void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel);
+// pg_walk.hip
+uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1);
+void export_edges(Ctx& c, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap);
+void set_labels(Ctx& c, const int64_t* key, const int64_t* val, const int64_t* id, uint64_t n);
+uint64_t walk_rows(Ctx& c, const uint8_t* h_rec_flag, int rc1);
+
+// helpers
+inline uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536u) {
+  uint64_t g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (unsigned)g;
+}
+
+}  // namespace pg

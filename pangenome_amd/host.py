@@ -1,0 +1,244 @@
+"""Host-side logic of the drop-in: which records each pass visits, the label
+dictionary, the `.xyz` text and the printed rows.
+
+The device does every per-base step; what stays here is what is plain Python
+(or loop control) in the reference too:
+
+* the record loops of the three passes with their `-n` limit, their
+  2**33-base checkpoints and what resuming from a checkpoint does
+  (seq2rdbg :1251-1266 + seq2dbg_jit_ :1204-1230; seq2graph :1876-1890 +
+  rdbg_edge_weight_jit_ :1809-1827; seqs2path_jit_ :1831-1849);
+* the `.xyz` writer (:1893-1904), the label dictionary (:1918-1944) and the
+  row printer (:1946-1949).
+"""
+from __future__ import annotations
+
+import ast
+import operator
+
+import numpy as np
+
+CHUNK = 2 ** 33          # entry_point :2073
+NEVER = 2 ** 63
+
+
+# ------------------------------------------------------------------ -n parsing
+_OPS = {ast.Add: operator.add, ast.Sub: operator.sub, ast.Mult: operator.mul,
+        ast.Div: operator.truediv, ast.Pow: operator.pow, ast.FloorDiv: operator.floordiv,
+        ast.USub: operator.neg, ast.UAdd: operator.pos}
+
+
+def eval_number(text: str) -> int:
+    """``int(eval(args['-n']))`` (:1997) for the numeric expressions it is given
+    ('5e8', '2**63', '10**9'), without evaluating arbitrary code."""
+    def ev(node):
+        if isinstance(node, ast.Expression):
+            return ev(node.body)
+        if isinstance(node, ast.Constant) and isinstance(node.value, (int, float)):
+            return node.value
+        if isinstance(node, ast.BinOp) and type(node.op) in _OPS:
+            return _OPS[type(node.op)](ev(node.left), ev(node.right))
+        if isinstance(node, ast.UnaryOp) and type(node.op) in _OPS:
+            return _OPS[type(node.op)](ev(node.operand))
+        raise ValueError("unsupported -n expression: %r" % text)
+    return int(ev(ast.parse(text, mode="eval")))
+
+
+def ns_hit(N: int, Ns: int) -> bool:
+    # numba compares int64 N with Ns; Ns >= 2**63 arrives as uint64 and the
+    # mixed comparison never succeeds
+    return Ns < NEVER and N > Ns
+
+
+# ----------------------------------------------------------------- pass plans
+class FileShape:
+    """What the pass planner needs to know about the FASTA beyond the records."""
+
+    def __init__(self, first_byte: int, last_line_has_nl: bool, first_header_at: int,
+                 record_header_is_last_unterminated: bool):
+        self.first_byte = first_byte
+        self.last_line_has_nl = last_line_has_nl
+        self.first_header_at = first_header_at            # byte offset of record 0's header
+        self.last_header_unterminated = record_header_is_last_unterminated
+
+    @classmethod
+    def from_bytes(cls, buf, hdr_start: np.ndarray, hdr_len: np.ndarray):
+        n = len(buf)
+        first = buf[0] if n else -1
+        last_nl = n > 0 and buf[n - 1] == 10
+        R = hdr_start.shape[0]
+        fh = int(hdr_start[0]) if R else -1
+        # the last record's header is the file's final, newline-less line
+        lhu = bool(R) and int(hdr_start[-1] + hdr_len[-1]) >= n - 1 and not last_nl
+        return cls(first, last_nl, fh, lhu)
+
+
+def _resumed_records(pos: int, R: int, shape: FileShape):
+    """Records one seqio_jit_ call yields when restarted at the `ptr` of record
+    pos-1 (:1240, :1860): readline_jit_ starts its first line at byte 0, so
+    that line is the file's prefix up to the end of record pos's header line.
+    If the file does not start with '>', that prefix is a sequence line, qid
+    is never set and record pos is lost; when record pos-1 was the last one the
+    prefix runs to EOF and, starting with '>', yields one extra empty record.
+    A first line without '\\n' is never yielded (`end > start > 0`)."""
+    if pos < R:
+        if pos == R - 1 and shape.last_header_unterminated:
+            return []                                  # no '\n' after ptr: nothing at all
+        lost = shape.first_byte != ord(">")
+        return list(range(pos + (1 if lost else 0), R))
+    if shape.last_line_has_nl and shape.first_byte == ord(">"):
+        return ["extra"]
+    return []
+
+
+def plan_dbg(seq_len: np.ndarray, shape: FileShape, rc0: bool, Ns: int, chunk: int = CHUNK):
+    """seq2rdbg (:1251-1266) over seq2dbg_jit_ (:1204-1230): which records the
+    dBG pass inserts, and how many extra empty records it meets."""
+    R = seq_len.shape[0]
+    flags = np.zeros(R, np.uint8)
+    extra = 0
+    mult = 2 if rc0 else 1
+    recs = list(range(R))
+    N = 0
+    while True:
+        Nl = chk = 0
+        done, last = 1, None
+        for r in recs:
+            n = 0 if r == "extra" else int(seq_len[r])
+            if r == "extra":
+                extra += 1
+            else:
+                flags[r] = 1
+            Nl += n * mult
+            chk += n * mult
+            if chk > chunk:
+                done, last = -1, r
+                break
+            if ns_hit(Nl, Ns):
+                break
+        if done != -1:
+            break
+        recs = _resumed_records(last + 1, R, shape)
+        N += Nl
+        if ns_hit(N, Ns):
+            break
+    return flags, extra
+
+
+def plan_edges(seq_len: np.ndarray, shape: FileShape, Ns: int, chunk: int = CHUNK):
+    """seq2graph (:1876-1890) over rdbg_edge_weight_jit_ (:1809-1827): walked
+    records and, per record, the checkpoint segment it belongs to."""
+    R = seq_len.shape[0]
+    flags = np.zeros(R, np.uint8)
+    segment = np.full(R, -1, np.int64)
+    recs = list(range(R))
+    N = 0
+    seg = 0
+    n_checkpoints = 0
+    while True:
+        chk = 0
+        done, last = 1, None
+        for r in recs:
+            n = 0 if r == "extra" else int(seq_len[r])
+            if r != "extra":
+                flags[r] = 1
+                segment[r] = seg
+            N += n
+            if ns_hit(N, Ns):
+                break
+            chk += n
+            if chk > chunk:
+                done, last = -1, r
+                break
+        if done != -1:
+            break
+        n_checkpoints += 1
+        seg += 1
+        recs = _resumed_records(last + 1, R, shape)
+    return flags, segment, n_checkpoints
+
+
+def plan_rows(seq_len: np.ndarray, shape: FileShape, buf, Ns: int):
+    """seqs2path_jit_ (:1831-1849).  It hands `isfasta` (True) to seqio_jit_'s
+    offset slot (:1833), so line scanning starts at byte 1; that differs from
+    byte 0 only when the file starts with '\\n' and record 0's header is the
+    next line — that record is then lost."""
+    R = seq_len.shape[0]
+    flags = np.zeros(R, np.uint8)
+    first = 0
+    if R and len(buf) > 1 and buf[0] == 10 and shape.first_header_at == 1:
+        first = 1
+    N = 0
+    for r in range(first, R):
+        flags[r] = 1
+        N += int(seq_len[r])
+        if ns_hit(N, Ns):
+            break
+    return flags
+
+
+def edge_order(walk_first: np.ndarray, segment_of_record: np.ndarray, n_checkpoints: int) -> np.ndarray:
+    """Iteration order of the edge Dict: first occurrence, reversed at every
+    dump/reload checkpoint (dict2array pops LIFO, :229; array2dict re-inserts,
+    :264-286).  Input rows are in first-occurrence order; returns the
+    permutation into the reference's order."""
+    m = walk_first.shape[0]
+    idx = np.arange(m, dtype=np.int64)
+    if m == 0 or n_checkpoints == 0:
+        return idx
+    seg = segment_of_record[walk_first // 2]
+    order = np.zeros(0, np.int64)
+    for s in range(n_checkpoints + 1):
+        order = np.concatenate([order, idx[seg == s]])
+        if s < n_checkpoints:
+            order = order[::-1]
+    return order
+
+
+# -------------------------------------------------------------------- text
+def xyz_text(tuples: np.ndarray, counts: np.ndarray) -> str:
+    """`"%d_%d\\t%d_%d\\t%d\\n"` per edge (:1901)."""
+    return "".join("%d_%d\t%d_%d\t%d\n" % (a, b, c, d, e)
+                   for (a, b, c, d), e in zip(tuples.tolist(), counts.tolist()))
+
+
+def label_dict(mcl_text: str, xyz_lines) -> dict:
+    """seq2graph :1918-1944: `.mcl` line index, then unseen `.xyz` nodes."""
+    lab = {}
+    flag = 0
+    for line in mcl_text.splitlines(keepends=True):
+        for tok in line[:-1].split("\t"):
+            lab[tuple(map(int, tok.split("_")[:2]))] = flag
+        flag += 1
+    for line in xyz_lines:
+        j, k = line[:-1].split("\t")[:2]
+        kj = tuple(map(int, j.split("_")[:2]))
+        if kj not in lab:
+            lab[kj] = flag
+            flag += 1
+        kk = tuple(map(int, k.split("_")[:2]))
+        if kk not in lab:
+            lab[kk] = flag
+            flag += 1
+    return lab
+
+
+def label_arrays(lab: dict):
+    n = len(lab)
+    keys = np.fromiter((a for a, _ in lab.keys()), dtype=np.int64, count=n)
+    vals = np.fromiter((b for _, b in lab.keys()), dtype=np.int64, count=n)
+    ids = np.fromiter(lab.values(), dtype=np.int64, count=n)
+    return keys, vals, ids
+
+
+def format_rows(rows: np.ndarray, buf, hdr_start: np.ndarray, hdr_len: np.ndarray):
+    """`print('%s\\t%d\\t%d\\t%s\\t%d')` (:1947-1949); qid = header line minus '>'."""
+    names = {}
+    out = []
+    for r, s, e, strand, lab in rows.tolist():
+        q = names.get(r)
+        if q is None:
+            hs, hl = int(hdr_start[r]), int(hdr_len[r])
+            q = names[r] = bytes(buf[hs:hs + hl]).decode()[1:]
+        out.append("%s\t%d\t%d\t%s\t%d" % (q, s, e, "+" if strand == 1 else "-", lab))
+    return out

@@ -1,0 +1,188 @@
+"""Drop-in for kmer_numba.py's k-mer -> dBG -> rdBG -> region-table path.
+
+Same names, arguments and side files as the reference; every per-base step
+runs in libpangenome_hip.so on an MI355X (pangenome_amd/csrc).  Mirrors:
+
+  seq_chk      kmer_numba.py:873-885     file type sniffing
+  seq2bytes    :117-119                  memory-map the input
+  seq2rdbg     :1234-1268                dBG build (K1 parse + K3 insert)
+  dbg2rdbg     :1313-1321                rdBG (K5 degree scan + compaction)
+  seq2graph    :1853-1951                edges -> .xyz -> mcl -> labels -> rows
+  entry_point  :1971-2146                CLI (-i -k -n -c -r -d -R -D)
+
+Usage:  python -m pangenome_amd -i genomes.fa -k 27 > result.tab
+"""
+from __future__ import annotations
+
+import os
+import sys
+from time import time
+
+import numpy as np
+
+from . import host
+from ._lib import Context
+
+
+# --------------------------------------------------------------- input files
+def seq_chk(qry):
+    """:873-885 — 'fasta' if a header starts the first 40 characters."""
+    with open(qry, "r") as f:
+        seq = f.read(2 * 20)
+    if seq[0].startswith(">") or "\n>" in seq:
+        return "fasta"
+    if seq[0].startswith("@") or "\n@" in seq:
+        return "fastq"
+    return None
+
+
+def seq2bytes(fn):
+    """:117-119 (read-only here: nothing is written back to the input)."""
+    return np.memmap(fn, mode="r", dtype=np.uint8) if os.path.getsize(fn) else np.zeros(0, np.uint8)
+
+
+class DeviceGraph:
+    """The device-resident dBG/rdBG of one input (what the reference keeps in
+    its `oakht` tables), plus the parsed record table the later passes reuse."""
+
+    def __init__(self, qry, kmer, device=0, data=None):
+        self.qry = qry
+        self.k = min(max(1, int(kmer)), 27)                    # :1236
+        self.buf = seq2bytes(qry) if data is None else data
+        self.ctx = Context(self.k, device)
+        self.ctx.set_fasta(self.buf)
+        self.ctx.parse()
+        rec = self.ctx.records()
+        self.seq_len, self.hdr_start, self.hdr_len = rec["seq_len"], rec["hdr_start"], rec["hdr_len"]
+        self.shape = host.FileShape.from_bytes(self.buf, self.hdr_start, self.hdr_len)
+        self.stats = None
+        self.reduced = False
+
+    @property
+    def size(self):
+        return self.stats.n_dbg if self.stats else 0
+
+    def dbg_items(self):
+        """(keys, masks) sorted by key — dump()'s content (:243-261)."""
+        return self.ctx.dbg()
+
+    def rdbg_keys(self):
+        return self.ctx.rdbg()
+
+
+# ------------------------------------------------------------------- passes
+def seq2rdbg(qry, kmer=13, bits=5, Ns=1e6, chunk=2 ** 32, brkpt="./breakpoint", saved="dBG_disk",
+             hashfunc=None, jit=True, rc=True, device=0):
+    """:1234-1268.  Returns the device dBG."""
+    if brkpt and os.path.isfile(brkpt):
+        raise NotImplementedError("resuming a dBG checkpoint (-r) is not supported by the GPU build")
+    if seq_chk(qry) != "fasta":
+        raise ValueError("%s: only FASTA input is supported (the reference's FASTQ branch is "
+                         "broken, kmer_numba.py:174-186)" % qry)
+    g = DeviceGraph(qry, kmer, device)
+    flags, extra = host.plan_dbg(g.seq_len, g.shape, bool(rc), int(Ns), int(chunk))
+    g.stats = g.ctx.build_dbg(flags, extra, bool(rc))
+    return g
+
+
+def dbg2rdbg(kmer_dict):
+    """:1313-1321.  Reduces in place on the device and returns the same graph."""
+    kmer_dict.stats = kmer_dict.ctx.build_rdbg()
+    kmer_dict.reduced = True
+    return kmer_dict
+
+
+def rdbg_edges(g: DeviceGraph, Ns, chunk, rc):
+    """Edge Dict of rdbg_edge_weight_jit_ (:1808-1827) in its iteration order."""
+    flags, segment, ncp = host.plan_edges(g.seq_len, g.shape, int(Ns), int(chunk))
+    tuples, counts, walk_first = g.ctx.edges(flags, bool(rc))
+    order = host.edge_order(walk_first, segment, ncp)
+    return tuples[order], counts[order]
+
+
+def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_dict=None, saved=None,
+              hashfunc=None, jit=True, chunk=2 ** 33, rc=False, cluster=True, out=None):
+    """:1853-1951: edge weights -> `<qry>_rdbg_weight.xyz` -> mcl (or reuse)
+    -> label dictionary -> print the region rows."""
+    out = out or sys.stdout
+    if brkpt and os.path.isfile(brkpt):
+        raise NotImplementedError("resuming an edge checkpoint (-R) is not supported by the GPU build")
+    g = rdbg_dict
+    tuples, counts = rdbg_edges(g, Ns, chunk, rc)
+    oname = qry + "_rdbg_weight.xyz"
+    xyz = host.xyz_text(tuples, counts)
+    with open(oname, "w") as f:
+        f.write(xyz)
+    if cluster:
+        if os.path.isfile("%s.mcl" % oname):
+            print("# the mcl has been ran", file=out)
+        else:
+            out.flush()
+            os.system("mcl %s --abc -I 1.5 -te 8 -o %s.mcl -q x -V all" % (oname, oname))
+    with open(oname + ".mcl", "r") as f:
+        mcl_text = f.read()
+    lab = host.label_dict(mcl_text, xyz.splitlines(keepends=True))
+    g.ctx.set_labels(*host.label_arrays(lab))
+    flags = host.plan_rows(g.seq_len, g.shape, g.buf, int(Ns))
+    rows = g.ctx.rows(flags, bool(rc))
+    text = host.format_rows(rows, g.buf, g.hdr_start, g.hdr_len)
+    if text:
+        out.write("\n".join(text) + "\n")
+    return lab
+
+
+# ---------------------------------------------------------------------- CLI
+def manual_print(out=None):
+    out = out or sys.stdout
+    for line in ("Usage:", "  pyhton this.py -i qry.fsa -k 10 -n 1000000", "Parameters:",
+                 "  -i: query sequences in fasta format", "  -k: kmer length",
+                 "  -d: the de bruijn graph", "  -r: break point of de bruijn graph",
+                 "  -D: the reduced de bruijn graph", "  -R: break point of reduced de bruijn graph",
+                 "  -n: length of query sequences for pan-genomic analysis",
+                 "  -c: complementary reverse sequence. 00,01,10,11"):
+        print(line, file=out)
+
+
+def parse_args(argv):
+    """:1983-1997 — same flag handling, including `-k27` and skipped unknowns."""
+    args = {"-i": "", "-k": "50", "-n": "2**63", "-r": "", "-d": "", "-R": "", "-D": "", "-c": "2"}
+    N = len(argv)
+    for i in range(1, N):
+        k = argv[i]
+        if k in args:
+            args[k] = argv[i + 1]
+        elif k[:2] in args and len(k) > 2:
+            args[k[:2]] = k[2:]
+    return args
+
+
+def entry_point(argv, out=None, device=0):
+    out = out or sys.stdout
+    args = parse_args(argv)
+    qry, kmer, Ns = args["-i"], int(args["-k"]), host.eval_number(args["-n"])
+    bkt, dbs, rbk, rc, rdb = args["-r"], args["-d"], args["-R"], int(args["-c"]), args["-D"]
+    if not qry:
+        manual_print(out)
+        raise SystemExit()
+    chunk = 2 ** 33
+    if dbs or rdb:
+        raise NotImplementedError("-d/-D (loading an npz dBG/rdBG) is not supported by the GPU build yet")
+    print("# build the dBG", file=out)
+    st = time()
+    rc0 = (rc >> 1) == 1
+    kmer_dict = seq2rdbg(qry, kmer, 5, Ns, brkpt=bkt, chunk=chunk, rc=rc0, device=device)
+    print("# finished in", time() - st, "seconds", file=out)
+    print("# build the reduced dBG", file=out)
+    st = time()
+    rdbg_dict = dbg2rdbg(kmer_dict)
+    print("# finished in", time() - st, "seconds", file=out)
+    print("# find fr", file=out)
+    st = time()
+    rc1 = (rc & 1) == 1
+    seq2graph(qry, kmer=kmer, bits=5, Ns=Ns, rdbg_dict=rdbg_dict, chunk=chunk, brkpt=rbk, rc=rc1, out=out)
+    print("# finished in", time() - st, "seconds", file=out)
+    return 0
+
+
+def main():
+    return entry_point(sys.argv)

@@ -1,0 +1,96 @@
+"""CPU-side checks of the drop-in boundary and the host logic (no GPU calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "pangenome.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(pg_\w+)\s*\(", text, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from pangenome_amd import _lib
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), s
+    # and the ctypes binding covers exactly the header
+    assert sorted(_lib.SIGNATURES) == syms
+
+
+def test_no_device_fails_loudly():
+    """Without a GPU the product raises; it never falls back to a CPU path."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    from pangenome_amd import _lib
+    with pytest.raises(_lib.PangenomeError):
+        _lib.Context(27)
+
+
+def test_eval_number():
+    from pangenome_amd.host import eval_number
+    assert eval_number("2**63") == 2 ** 63
+    assert eval_number("5e8") == 500000000
+    assert eval_number("1000") == 1000
+    with pytest.raises(ValueError):
+        eval_number("__import__('os')")
+
+
+def test_parse_args_reference_forms():
+    from pangenome_amd.kmer import parse_args
+    a = parse_args(["x", "-i", "f.fa", "-k27", "--weird", "-c", "3"])
+    assert a["-i"] == "f.fa" and a["-k"] == "27" and a["-c"] == "3" and a["-n"] == "2**63"
+
+
+def test_plan_dbg_checkpoints():
+    from pangenome_amd import host
+    lens = np.array([10, 10, 10, 10], np.int64)
+    shape_gt = host.FileShape(ord(">"), True, 0, False)
+    shape_junk = host.FileShape(ord("j"), True, 20, False)
+    # chunk 25 with rc (20 per record): checkpoint after record 1 and record 3
+    f, extra = host.plan_dbg(lens, shape_gt, True, 2 ** 63, chunk=25)
+    assert f.tolist() == [1, 1, 1, 1] and extra == 1           # resume at EOF -> empty record
+    f, extra = host.plan_dbg(lens, shape_junk, True, 2 ** 63, chunk=25)
+    assert f.tolist() == [1, 1, 0, 1] and extra == 0           # record after the checkpoint lost
+    # -n: the dBG pass counts both strands; stops after the record that crosses
+    f, _ = host.plan_dbg(lens, shape_gt, True, 30)
+    assert f.tolist() == [1, 1, 0, 0]
+    f, _ = host.plan_dbg(lens, shape_gt, False, 30)
+    assert f.tolist() == [1, 1, 1, 1]
+
+
+def test_plan_edges_and_rows():
+    from pangenome_amd import host
+    lens = np.array([10, 10, 10], np.int64)
+    shape = host.FileShape(ord(">"), True, 0, False)
+    f, seg, ncp = host.plan_edges(lens, shape, 2 ** 63, chunk=15)
+    assert f.tolist() == [1, 1, 1] and seg.tolist() == [0, 0, 1] and ncp == 1
+    assert host.plan_rows(lens, shape, b">a\n", 15).tolist() == [1, 1, 0]
+    # a file starting with '\n' then record 0's header: lost in the label pass
+    assert host.plan_rows(lens, host.FileShape(10, True, 1, False), b"\n>a\n", 2 ** 63).tolist() == [0, 1, 1]
+
+
+def test_edge_order_reversal():
+    from pangenome_amd import host
+    walk_first = np.array([0, 0, 2, 4, 4], np.int64)        # records 0, 0, 1, 2, 2
+    seg = np.array([0, 1, 1], np.int64)
+    order = host.edge_order(walk_first, seg, 1)
+    # segment 0 = [0, 1] reversed -> [1, 0], then append [2, 3, 4]
+    assert order.tolist() == [1, 0, 2, 3, 4]
+
+
+def test_label_dict_matches_oracle(oracle_mod):
+    from pangenome_amd import host
+    xyz = "1_2\t3_4\t1\n3_4\t5_6\t2\n7_8\t1_2\t1\n"
+    mcl = "3_4\t9_9\n"
+    a = host.label_dict(mcl, xyz.splitlines(keepends=True))
+    k, v, i = oracle_mod.label_table(xyz, mcl)
+    assert a == {(int(x), int(y)): int(z) for x, y, z in zip(k, v, i)}

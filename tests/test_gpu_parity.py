@@ -1,0 +1,158 @@
+"""GPU parity: libpangenome_hip.so against the reference's goldens and the oracle.
+
+Every test here goes through the C ABI (pangenome_amd._lib -> pangenome.h) on
+an MI355X.  Integer/byte work: all comparisons are bit-exact.
+"""
+import io
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import Fixture, fixture_names
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def km():
+    from pangenome_amd import kmer
+    return kmer
+
+
+def rows_of(text):
+    return [ln for ln in text.split("\n") if len(ln.split("\t")) == 5 and ln.split("\t")[3] in ("+", "-")]
+
+
+def run_stages(km, fasta: bytes, k, c, ns, mcl_text, tmp_path, edge_chunk=2 ** 33):
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text(mcl_text)
+    Ns = ns if ns is not None else 2 ** 63
+    out = io.StringIO()
+    g = km.seq2rdbg(str(q), k, 5, Ns, brkpt="", chunk=2 ** 33, rc=(c >> 1) == 1)
+    dk, dm = g.dbg_items()
+    km.dbg2rdbg(g)
+    rk = g.rdbg_keys()
+    km.seq2graph(str(q), kmer=k, bits=5, Ns=Ns, rdbg_dict=g, chunk=edge_chunk, brkpt="", rc=(c & 1) == 1, out=out)
+    xyz = (tmp_path / "input.fsa_rdbg_weight.xyz").read_text()
+    return dict(dbg_keys=dk, dbg_masks=dm, rdbg_keys=rk, xyz=xyz, rows=rows_of(out.getvalue()), graph=g)
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_golden(km, name, tmp_path):
+    fx = Fixture(name)
+    got = run_stages(km, fx.fasta, fx.k, fx.c, fx.ns, fx.mcl, tmp_path, fx.edge_chunk)
+    assert np.array_equal(got["dbg_keys"], fx.dbg_keys)
+    assert np.array_equal(got["dbg_masks"], fx.dbg_masks)
+    assert np.array_equal(got["rdbg_keys"], fx.rdbg_keys)
+    assert got["xyz"] == fx.xyz
+    assert got["rows"] == fx.rows
+
+
+def test_cli_entry_point(km, tmp_path):
+    fx = Fixture("pan8_k27_c3")
+    q = tmp_path / "in.fa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "in.fa_rdbg_weight.xyz.mcl").write_text("")
+    out = io.StringIO()
+    km.entry_point(["kmer_numba.py", "-i", str(q), "-k27", "-c", "3", "--unknown"], out=out)
+    text = out.getvalue()
+    assert "# the mcl has been ran" in text
+    assert rows_of(text) == fx.rows
+
+
+def _random_fasta(rng, n_rec, k):
+    """Random records exercising every length class around k and odd bytes."""
+    alphabet = np.frombuffer(b"ACGTACGTACGTACGTacgtNnRY$#", dtype=np.uint8)
+    parts = []
+    for r in range(n_rec):
+        n = int(rng.choice([0, 1, k - 1, k, k + 1, k + 2, k + 3, 2 * k, 500, 3000]))
+        seq = alphabet[rng.integers(0, alphabet.shape[0], n)].tobytes()
+        width = int(rng.choice([7, 60, 1000]))
+        body = b"".join(seq[i:i + width] + b"\n" for i in range(0, n, width))
+        parts.append(b">r%d desc\n" % r + body)
+    return b"".join(parts)
+
+
+@pytest.mark.parametrize("k", [1, 5, 11, 27])
+@pytest.mark.parametrize("c", [0, 3])
+def test_random_vs_oracle(km, oracle_mod, tmp_path, k, c):
+    rng = np.random.default_rng(1000 * k + c)
+    fasta = _random_fasta(rng, 40, k)
+    ref = oracle_mod.run_pipeline(fasta, k, c)
+    got = run_stages(km, fasta, k, c, None, "", tmp_path)
+    assert np.array_equal(got["dbg_keys"], ref["dbg_keys"])
+    assert np.array_equal(got["dbg_masks"], ref["dbg_masks"])
+    assert np.array_equal(got["rdbg_keys"], ref["rdbg_keys"])
+    assert got["xyz"] == ref["xyz"]
+    assert got["rows"] == ref["rows"]
+
+
+@pytest.mark.parametrize("c", [0, 1, 2, 3])
+def test_pangenome_vs_oracle(km, oracle_mod, tmp_path, c):
+    from pangenome_amd import synth
+    fasta = synth.pangenome(12, 60_000, snp=0.005, indel=5e-4, seed=77 + c)
+    ref = oracle_mod.run_pipeline(fasta, 27, c)
+    got = run_stages(km, fasta, 27, c, None, "", tmp_path)
+    assert np.array_equal(got["dbg_keys"], ref["dbg_keys"])
+    assert np.array_equal(got["dbg_masks"], ref["dbg_masks"])
+    assert np.array_equal(got["rdbg_keys"], ref["rdbg_keys"])
+    assert got["xyz"] == ref["xyz"]
+    assert got["rows"] == ref["rows"]
+
+
+def test_edge_checkpoint_reversal_vs_oracle(km, oracle_mod, tmp_path):
+    from pangenome_amd import synth
+    fasta = b"junk before header\n" + synth.pangenome(9, 20_000, snp=0.01, indel=1e-3, seed=5)
+    ref = oracle_mod.run_pipeline(fasta, 21, 3, edge_chunk=25_000)
+    got = run_stages(km, fasta, 21, 3, None, "", tmp_path, edge_chunk=25_000)
+    assert got["xyz"] == ref["xyz"]
+    assert got["rows"] == ref["rows"]
+
+
+def test_device_resident_input_and_repeat(km):
+    """Input already in HBM (the bench path): two builds are identical."""
+    import torch
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    fasta = synth.pangenome(20, 100_000, seed=9)
+    d = torch.frombuffer(bytearray(fasta), dtype=torch.uint8).to("cuda:0")
+    torch.cuda.synchronize()
+    ctx = Context(27)
+    res = []
+    for _ in range(2):
+        ctx.set_fasta_device(d.data_ptr(), d.numel(), keepalive=d)
+        ctx.parse()
+        ctx.build_dbg(None, 0, True)
+        st = ctx.build_rdbg()
+        res.append((st.n_dbg, st.n_rdbg, ctx.rdbg()))
+    assert res[0][0] == res[1][0] and res[0][1] == res[1][1]
+    assert np.array_equal(res[0][2], res[1][2])
+
+
+def test_full_size_properties(km):
+    """C3-shaped input (100 genomes is too slow for the oracle; use 40 x 5 Mbp):
+    size-independent invariants of the reference's dBG."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    fasta = synth.pangenome(40, 5_000_000, seed=123)
+    ctx = Context(27)
+    ctx.set_fasta(fasta)
+    R, B = ctx.parse()
+    assert R == 40
+    ctx.build_dbg(None, 0, True)
+    st = ctx.build_rdbg()
+    keys, masks = ctx.dbg()
+    assert st.n_dbg == keys.shape[0]
+    # both strands inserted: the key set is closed under reverse complement
+    # (no N here, so no palindromes at odd k): n_dbg == 2 * occupied slots
+    assert st.n_dbg == 2 * st.n_slots
+    # every key has a nonzero mask with at most one '#' start (pred 0) ... and
+    # the rdBG is exactly the keys whose mask is not (1 pred bit and 1 succ bit)
+    pc = np.array([bin(i).count("1") for i in range(64)], np.int64)
+    member = ~((pc[(masks >> 6) & 63] == 1) & (pc[masks & 63] == 1))
+    assert np.array_equal(np.sort(keys[member]), ctx.rdbg())
+    # record lengths agree with a host parse
+    lens = [len(b"".join(rec.split(b"\n")[1:])) for rec in fasta.split(b">")[1:]]
+    assert ctx.records()["seq_len"].tolist() == lens

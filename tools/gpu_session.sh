@@ -1,0 +1,27 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench. Each GPU step has its own time
+# limit; a fault/abort/timeout ends the session (exit codes other than 0/1).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+run() {  # name timeout cmd...
+  local name=$1 lim=$2; shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$lim" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"; tail -n 15 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
+    testsall) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 900 python bench.py ;;
+    benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
+    benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
