@@ -72,6 +72,14 @@ def load():
             raise ImportError(
                 "libpangenome_hip.so is not built (%s); run __graft_entry__.build() "
                 "or `make -C pangenome_amd/csrc` — there is no CPU fallback" % LIB_PATH)
+        # One HIP runtime per process: torch ships its own libamdhip64.so.7
+        # (same SONAME as /opt/rocm's).  Whichever loads first serves both, and
+        # torch's build refuses the system one, so let torch load it first;
+        # device buffers from torch (bench, multi-GPU exchange) then share it.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
             fn = getattr(lib, name)

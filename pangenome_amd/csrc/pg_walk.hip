@@ -228,15 +228,25 @@ __global__ void __launch_bounds__(WBLOCK) k_walk_write(WalkArgs a, uint64_t nrun
 }
 
 // ------------------------------------------------------------ edge table
+// Memory-side reads of words other lanes publish with atomics.  Device-scope
+// atomics execute beyond the XCD's L2 and do not refresh it, so a plain (or
+// relaxed atomic) load can keep returning a stale 0 from L2; an idempotent
+// read-modify-write such as atomicAdd(p, 0) may be rewritten into such a load
+// by the compiler.  A compare-and-swap of 0 with 0 cannot be, and returns the
+// memory-side value (it writes 0 only where 0 already is).
 __device__ __forceinline__ unsigned long long atomic_read64(unsigned long long* p) {
-  return atomicAdd(p, 0ull);
+  return atomicCAS(p, 0ull, 0ull);
 }
-__device__ __forceinline__ unsigned atomic_read32(unsigned* p) { return atomicAdd(p, 0u); }
+__device__ __forceinline__ unsigned atomic_read32(unsigned* p) { return atomicCAS(p, 0u, 0u); }
 
 // Find-or-insert the edge (n0, v0, n1, v1).  Slots are claimed by CAS on
 // n0+1 and completed with atomic stores; every field goes from 0 to its final
-// value exactly once, so a nonzero plain read is final and a zero read is
-// re-checked with an atomic (memory-side) read.  Returns the slot or ~0.
+// value once, so a nonzero read is final.  Nothing ever waits: an occurrence
+// that meets a claimed slot whose other fields are not visible yet returns
+// EDGE_RETRY and is re-run by the next launch (all claims of a launch are
+// published when it ends).  Spinning instead deadlocks: the compiler lays the
+// winner's publish out after the loop, behind its waiting wave-mates.
+constexpr uint64_t EDGE_RETRY = ~0ull - 1;
 __device__ uint64_t edge_find_or_insert(EdgeSlot* __restrict__ tab, uint64_t capmask, uint64_t n0, uint32_t v0,
                                         uint64_t n1, uint32_t v1, unsigned* err) {
   const unsigned long long a = n0 + 1ull, bkey = n1 + 1ull;
@@ -244,25 +254,21 @@ __device__ uint64_t edge_find_or_insert(EdgeSlot* __restrict__ tab, uint64_t cap
   uint64_t slot = fmix64(n0 * 0x9e3779b97f4a7c15ull ^ fmix64(n1 ^ ((uint64_t)vv << 40))) & capmask;
   for (uint64_t probe = 0; probe <= capmask; ++probe) {
     EdgeSlot* s = tab + slot;
-    unsigned long long w0 = s->n0p1;
-    bool won = false;
+    unsigned long long w0 = s->n0p1;          // a stale plain read can only show 0
     if (w0 == 0ull) {
       w0 = atomicCAS(&s->n0p1, 0ull, a);
-      if (w0 == 0ull) { won = true; w0 = a; }
-    }
-    if (won) {
-      atomicExch(&s->vv, vv);
-      atomicExch(&s->n1p1, bkey);
-      return slot;
+      if (w0 == 0ull) {
+        atomicExch(&s->vv, vv);
+        atomicExch(&s->n1p1, bkey);
+        return slot;
+      }
     }
     if (w0 == a) {
       unsigned long long w1 = s->n1p1;
       unsigned w2 = s->vv;
-      for (int spin = 0; (w1 == 0ull || w2 == 0u) && spin < (1 << 22); ++spin) {
-        w1 = atomic_read64(&s->n1p1);
-        w2 = atomic_read32(&s->vv);
-      }
-      if (w1 == 0ull || w2 == 0u) { atomicOr(err, 1u); return ~0ull; }
+      if (w1 == 0ull) w1 = atomic_read64(&s->n1p1);
+      if (w2 == 0u) w2 = atomic_read32(&s->vv);
+      if (w1 == 0ull || w2 == 0u) return EDGE_RETRY;
       if (w1 == bkey && w2 == vv) return slot;
     }
     slot = (slot + 1) & capmask;
@@ -290,13 +296,20 @@ __device__ __forceinline__ bool pair_insert(unsigned long long* __restrict__ set
   return false;
 }
 
-__global__ void k_edges(const Occ* __restrict__ occ, uint64_t m, EdgeSlot* __restrict__ tab, uint64_t capmask,
-                        unsigned long long* __restrict__ pairs, uint64_t pair_capmask, unsigned* err) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i + 1 < m;
-       i += (uint64_t)gridDim.x * blockDim.x) {
+// one launch over occurrence indices (all of them, or a retry list)
+__global__ void k_edges(const Occ* __restrict__ occ, uint64_t m, const unsigned long long* __restrict__ list,
+                        uint64_t nlist, EdgeSlot* __restrict__ tab, uint64_t capmask,
+                        unsigned long long* __restrict__ pairs, uint64_t pair_capmask,
+                        unsigned long long* __restrict__ retry, unsigned long long* __restrict__ nretry,
+                        unsigned* err) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < nlist;
+       j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = list ? list[j] : j;
+    if (i + 1 >= m) continue;
     const Occ a = occ[i], b = occ[i + 1];
     if (a.walk != b.walk) continue;
     const uint64_t s = edge_find_or_insert(tab, capmask, a.key, a.v, b.key, b.v, err);
+    if (s == EDGE_RETRY) { retry[atomicAdd(nretry, 1ull)] = i; continue; }
     if (s == ~0ull) continue;
     atomicMax(&tab[s].first, ~(unsigned long long)i);   // zeroed slots: max of ~i == ~(min i)
     if (pair_insert(pairs, pair_capmask, (s << 32) | a.walk, err)) atomicAdd(&tab[s].count, 1u);
@@ -523,10 +536,29 @@ uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1) {
   c.edge_out.reserve(sizeof(EdgeOut) * (m + 1));
   unsigned long long n_out = 0;
   if (m > 1) {
-    hipLaunchKernelGGL(k_edges, dim3(grid_for(m, 256, 16384)), dim3(256), 0, c.stream, c.occ.as<Occ>(), m,
-                       c.edge_tab.as<EdgeSlot>(), ecap - 1, c.pair_tab.as<unsigned long long>(), ecap - 1,
-                       err.as<unsigned>());
-    PG_HIP(hipGetLastError());
+    DevBuf rb;
+    rb.reserve(8 * 2 * (m + 2));
+    unsigned long long* lists[2] = {rb.as<unsigned long long>(), rb.as<unsigned long long>() + (m + 1)};
+    DevBuf nr;
+    nr.reserve(16);
+    const unsigned long long* cur = nullptr;
+    uint64_t ncur = m;
+    for (int round = 0; ncur && round < 64; ++round) {
+      unsigned long long* out = lists[round & 1];
+      PG_HIP(hipMemsetAsync(nr.p, 0, 8, c.stream));
+      hipLaunchKernelGGL(k_edges, dim3(grid_for(ncur, 256, 16384)), dim3(256), 0, c.stream, c.occ.as<Occ>(), m,
+                         cur, ncur, c.edge_tab.as<EdgeSlot>(), ecap - 1, c.pair_tab.as<unsigned long long>(),
+                         ecap - 1, out, nr.as<unsigned long long>(), err.as<unsigned>());
+      PG_HIP(hipGetLastError());
+      unsigned long long nn = 0;
+      PG_HIP(hipMemcpyAsync(&nn, nr.p, 8, hipMemcpyDeviceToHost, c.stream));
+      c.sync();
+      cur = out;
+      ncur = nn;
+    }
+    if (ncur) throw Error(-5, "pg_edges: edge insert did not converge");
+    rb.release();
+    nr.release();
     DevBuf cnt;
     cnt.reserve(8);
     PG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
