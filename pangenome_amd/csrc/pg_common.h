@@ -99,4 +99,37 @@ __host__ __device__ __forceinline__ bool rdbg_member(uint32_t m12) {
   return !(__builtin_popcount(m12 >> OFFBIT) == 1 && __builtin_popcount(m12 & 63u) == 1);
 }
 
+// exclusive scan over a block of BLOCK threads (BLOCK/64 waves); lds holds
+// BLOCK/64 words; every thread must call it
+template <int BLOCK>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, uint32_t& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < BLOCK / 64; ++w) {
+    uint32_t s = lds[w];
+    pre += (w < wid) ? s : 0u;
+    tot += s;
+  }
+  __syncthreads();
+  total = tot;
+  return pre + x - v;
+}
+
+// bijective XCD-aware remap (cdna_hip_programming.md §5.5 T1): blocks b,
+// b+8, b+16, ... share an XCD under round-robin dispatch; give them
+// consecutive work items so an XCD's L2 sees contiguous work
+__device__ __forceinline__ uint64_t xcd_swizzle(uint64_t b, uint64_t nb) {
+  const uint64_t q = nb / 8, r = nb % 8, x = b % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 }  // namespace pg

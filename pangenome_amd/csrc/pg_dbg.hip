@@ -12,7 +12,15 @@
 // mask in one 12-bit field and the reverse mask in the other (pg_common.h).
 // That halves the random HBM probes against inserting the two strands as the
 // reference does, while the exported dBG stays exactly the reference's.
+//
+// Homology-aware order.  A pangenome repeats each k-mer once per genome at
+// nearly the same offset, so K3 walks tiles of TILE windows stripe-major
+// (stripe j of every record, then stripe j+1, ...) and remaps blocks so one
+// stripe's tiles run on one XCD: the first genome's probe of a slot misses,
+// the other genomes' probes of it hit that XCD's L2 / the Infinity Cache.
+#include <algorithm>
 #include <cstring>
+#include <numeric>
 #include <rocprim/rocprim.hpp>
 
 #include "pg_internal.h"
@@ -20,13 +28,18 @@
 namespace pg {
 
 constexpr int IBLOCK = 256;
+constexpr int IW = 16;                        // windows per thread
+constexpr int TILE = IBLOCK * IW;             // windows per tile (one block)
 constexpr int MAX_PROBE = 4096;
-constexpr int N_CNT = 64;          // spread counters (one 64-byte line each)
+constexpr int N_CNT = 64;                     // spread counters (one 64-byte line each)
 
 // flags layout (uint32 words): [0] sentinel seen, [1] overflow, [16*(1+i)] counter i
 __device__ __forceinline__ unsigned* counter(unsigned* flags, int i) { return flags + 16 * (1 + i); }
 
 // Insert/OR one canonical key.  Returns 1 if this call created the slot.
+// Plain loads may be stale (atomics run beyond the XCD's L2), but a slot only
+// ever goes empty -> key and masks only gain bits: a stale empty is settled
+// by the CAS's return value, a stale mask only costs a redundant atomicOr.
 __device__ __forceinline__ int table_or(Slot* __restrict__ table, uint64_t capmask, uint64_t c,
                                         uint32_t mw, unsigned* flags) {
   const unsigned long long key1 = (unsigned long long)c + 1ull;
@@ -52,82 +65,8 @@ __device__ __forceinline__ int table_or(Slot* __restrict__ table, uint64_t capma
   return 0;
 }
 
-__device__ __forceinline__ uint64_t find_record(const long long* __restrict__ rec_start, uint64_t R, uint64_t p) {
-  // last r with rec_start[r] <= p; 0 when p precedes record 0 (the caller
-  // skips positions before rec_start[r])
-  uint64_t lo = 0, hi = R;
-  while (lo < hi) {
-    uint64_t mid = (lo + hi) >> 1;
-    if ((uint64_t)rec_start[mid] <= p) lo = mid + 1; else hi = mid;
-  }
-  return lo == 0 ? 0 : lo - 1;
-}
-
-// K3: one thread per run of W consecutive positions of the compacted stream.
-template <int W, bool RC>
-__global__ void __launch_bounds__(IBLOCK)
-k_insert(const uint8_t* __restrict__ cls, uint64_t total,
-         const long long* __restrict__ rec_start, const long long* __restrict__ rec_len,
-         const uint8_t* __restrict__ rec_flag, uint64_t R, int k, uint64_t shift,
-         Slot* __restrict__ table, uint64_t capmask, unsigned* __restrict__ flags) {
+__device__ __forceinline__ void block_count(unsigned created, unsigned* flags) {
   __shared__ unsigned red[IBLOCK / 64];
-  const uint64_t nruns = (total + W - 1) / W;
-  unsigned created = 0;
-  for (uint64_t run = blockIdx.x * (uint64_t)IBLOCK + threadIdx.x; run < nruns;
-       run += (uint64_t)gridDim.x * IBLOCK) {
-    const uint64_t p0 = run * W;
-    const uint64_t p1 = p0 + W < total ? p0 + W : total;
-    uint64_t r = find_record(rec_start, R, p0);
-    long long rs = 0, rn = -1; bool rf = false;
-    if (r < R) { rs = rec_start[r]; rn = rec_len[r]; rf = rec_flag[r] != 0; }
-    bool have = false;
-    uint64_t K = 0, Kr = 0;
-    for (uint64_t p = p0; p < p1; ++p) {
-      while (r < R && (long long)p >= rs + rn) {
-        ++r;
-        if (r < R) { rs = rec_start[r]; rn = rec_len[r]; rf = rec_flag[r] != 0; }
-        have = false;
-      }
-      if (r >= R || (long long)p < rs) { have = false; continue; }
-      const long long q = (long long)p - rs;
-      if (!rf || rn < k + 2 || q > rn - k) { have = false; continue; }
-      if (!have) {
-        K = 0; Kr = 0;
-        uint64_t pw = 1;
-        for (int j = 0; j < k; ++j) {              // k2n_jit (:975-985), both strands
-          const uint32_t cj = cls[p + j];
-          K += (uint64_t)digit_fw(cj) * pw;
-          Kr = Kr * 5 + digit_rc(cj);
-          pw *= 5;
-        }
-        have = true;
-      } else {                                     // Nu // 5 + alpha * 5^(k-1) (:1072)
-        const uint32_t dout = cls[p - 1], din = cls[p + k - 1];
-        K = (K - digit_fw(dout)) * INV5 + (uint64_t)digit_fw(din) * shift;
-        Kr = (Kr - (uint64_t)digit_rc(dout) * shift) * 5 + digit_rc(din);
-      }
-      const long long last = rn - k;
-      // forward window q: pred '#' at q==0, s[q-2] at the last window (:1080 quirk), else s[q-1]
-      const uint32_t fpred = q == 0 ? LAM_HASH : lam_fw(cls[p - (q == last ? 2 : 1)]);
-      const uint32_t fsucc = q == last ? LAM_DOLLAR : lam_fw(cls[p + k]);
-      uint32_t mf = (fpred << OFFBIT) | fsucc | PRES_A;
-      uint64_t c;
-      uint32_t mw;
-      if (RC) {
-        // its twin: reverse-strand window n-k-q, same boundary rules on that strand
-        const uint32_t rpred = q == last ? LAM_HASH : lam_rc(cls[p + k + (q == 0 ? 1 : 0)]);
-        const uint32_t rsucc = q == 0 ? LAM_DOLLAR : lam_rc(cls[p - 1]);
-        const uint32_t mr = (rpred << OFFBIT) | rsucc | PRES_A;
-        if (K < Kr)      { c = K;  mw = mf | (mr << 16); }
-        else if (K > Kr) { c = Kr; mw = mr | (mf << 16); }
-        else             { c = K;  mw = mf | mr; }
-      } else {
-        if (K <= Kr) { c = K; mw = mf; } else { c = Kr; mw = mf << 16; }
-      }
-      created += (unsigned)table_or(table, capmask, c, mw, flags);
-    }
-  }
-  // block-reduce the new-slot count, one atomic per block on a spread counter
   unsigned x = created;
   for (int o = 32; o > 0; o >>= 1) x += __shfl_down(x, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = x;
@@ -139,85 +78,155 @@ k_insert(const uint8_t* __restrict__ cls, uint64_t total,
   }
 }
 
+// K3.  One block per tile (record, stripe j): windows [j*TILE, (j+1)*TILE) of
+// a record with n >= k+2; thread t takes IW consecutive windows and rolls the
+// keys of both strands across them.
+template <bool RC>
+__global__ void __launch_bounds__(IBLOCK)
+k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__ tiles,
+         const long long* __restrict__ rec_start, const long long* __restrict__ rec_len, int k, uint64_t shift,
+         Slot* __restrict__ table, uint64_t capmask, unsigned* __restrict__ flags) {
+  const unsigned long long tile = tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
+  const int r = (int)(tile >> 32);
+  const long long rs = rec_start[r], rn = rec_len[r];
+  const long long last = rn - k;                              // last window index
+  const long long q0 = (long long)(tile & 0xFFFFFFFFull) * TILE + (long long)threadIdx.x * IW;
+  const long long q1 = q0 + IW <= last + 1 ? q0 + IW : last + 1;
+  unsigned created = 0;
+  uint64_t K = 0, Kr = 0;
+  for (long long q = q0; q < q1; ++q) {
+    const uint64_t p = (uint64_t)(rs + q);
+    if (q == q0) {
+      uint64_t pw = 1;
+      for (int j = 0; j < k; ++j) {                // k2n_jit (:975-985), both strands
+        const uint32_t cj = cls[p + j];
+        K += (uint64_t)digit_fw(cj) * pw;
+        Kr = Kr * 5 + digit_rc(cj);
+        pw *= 5;
+      }
+    } else {                                       // Nu // 5 + alpha * 5^(k-1) (:1072)
+      const uint32_t dout = cls[p - 1], din = cls[p + k - 1];
+      K = (K - digit_fw(dout)) * INV5 + (uint64_t)digit_fw(din) * shift;
+      Kr = (Kr - (uint64_t)digit_rc(dout) * shift) * 5 + digit_rc(din);
+    }
+    // forward window q: pred '#' at q==0, s[q-2] at the last window (:1080 quirk), else s[q-1]
+    const uint32_t fpred = q == 0 ? LAM_HASH : lam_fw(cls[p - (q == last ? 2 : 1)]);
+    const uint32_t fsucc = q == last ? LAM_DOLLAR : lam_fw(cls[p + k]);
+    const uint32_t mf = (fpred << OFFBIT) | fsucc | PRES_A;
+    uint64_t c;
+    uint32_t mw;
+    if (RC) {
+      // its twin: reverse-strand window n-k-q, same boundary rules on that strand
+      const uint32_t rpred = q == last ? LAM_HASH : lam_rc(cls[p + k + (q == 0 ? 1 : 0)]);
+      const uint32_t rsucc = q == 0 ? LAM_DOLLAR : lam_rc(cls[p - 1]);
+      const uint32_t mr = (rpred << OFFBIT) | rsucc | PRES_A;
+      if (K < Kr)      { c = K;  mw = mf | (mr << 16); }
+      else if (K > Kr) { c = Kr; mw = mr | (mf << 16); }
+      else             { c = K;  mw = mf | mr; }
+    } else {
+      if (K <= Kr) { c = K; mw = mf; } else { c = Kr; mw = mf << 16; }
+    }
+    created += (unsigned)table_or(table, capmask, c, mw, flags);
+  }
+  block_count(created, flags);
+}
+
 // one reference window of an explicit strand (used for records with n <= k+1)
 __device__ __forceinline__ void oriented_or(Slot* table, uint64_t capmask, int k, uint64_t x,
-                                            uint32_t m12, unsigned* flags) {
+                                            uint32_t m12, unsigned* flags, unsigned& created) {
   const uint64_t xr = rc_key(x, k);
   const uint32_t m = m12 | PRES_A;
-  if (x <= xr) (void)table_or(table, capmask, x, m, flags);
-  else (void)table_or(table, capmask, xr, m << 16, flags);
+  if (x <= xr) created += (unsigned)table_or(table, capmask, x, m, flags);
+  else created += (unsigned)table_or(table, capmask, xr, m << 16, flags);
 }
 
 // build_dbg for one strand of length n in {k, k+1}.  strand 0: s[i] = cls[rs+i];
 // strand 1: s[i] = comp_class(cls[rs+n-1-i]) (tab_rev(reversed(s)), :1217).
 __device__ void short_strand(const uint8_t* cls, long long rs, long long n, int strand, int k,
-                             uint64_t shift, Slot* table, uint64_t capmask, unsigned* flags) {
+                             uint64_t shift, Slot* table, uint64_t capmask, unsigned* flags, unsigned& created) {
   auto S = [&](long long i) -> uint32_t {
     return strand == 0 ? (uint32_t)cls[rs + i] : comp_class(cls[rs + n - 1 - i]);
   };
   uint64_t K0 = 0, pw = 1;
   for (int j = 0; j < k; ++j) { K0 += (uint64_t)digit_fw(S(j)) * pw; pw *= 5; }
   if (n == k) {                                            // :1084-1085
-    oriented_or(table, capmask, k, K0, (LAM_HASH << OFFBIT) | LAM_DOLLAR, flags);
+    oriented_or(table, capmask, k, K0, (LAM_HASH << OFFBIT) | LAM_DOLLAR, flags, created);
     return;
   }
   // n == k+1 (:1061-1082): the loop never runs and numba reads its variable as 0
-  oriented_or(table, capmask, k, K0, (LAM_HASH << OFFBIT) | lam_fw(S(k)), flags);
+  oriented_or(table, capmask, k, K0, (LAM_HASH << OFFBIT) | lam_fw(S(k)), flags, created);
   const uint64_t K1 = K0 / 5 + (uint64_t)digit_fw(S(1)) * shift;   // alpha[seq[0+1]]
-  oriented_or(table, capmask, k, K1, (lam_fw(S(1)) << OFFBIT) | LAM_DOLLAR, flags);  // seq[0-k] == s[1]
+  oriented_or(table, capmask, k, K1, (lam_fw(S(1)) << OFFBIT) | LAM_DOLLAR, flags, created);  // seq[0-k] == s[1]
 }
 
-__global__ void k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start,
-                        const long long* __restrict__ rec_len, const uint8_t* __restrict__ rec_flag,
-                        uint64_t R, int k, uint64_t shift, int rc, Slot* table, uint64_t capmask,
-                        unsigned* flags) {
+__global__ void __launch_bounds__(IBLOCK)
+k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start,
+        const long long* __restrict__ rec_len, const uint8_t* __restrict__ rec_flag, uint64_t R, int k,
+        uint64_t shift, int rc, Slot* table, uint64_t capmask, unsigned* flags) {
+  unsigned created = 0;
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R;
        r += (uint64_t)gridDim.x * blockDim.x) {
     if (!rec_flag[r]) continue;
     const long long n = rec_len[r];
     if (n > k + 1) continue;
     if (n < k) { atomicOr(flags, 1u); continue; }          // key -1, mask '$' (:1087-1088)
-    short_strand(cls, rec_start[r], n, 0, k, shift, table, capmask, flags);
-    if (rc) short_strand(cls, rec_start[r], n, 1, k, shift, table, capmask, flags);
+    short_strand(cls, rec_start[r], n, 0, k, shift, table, capmask, flags, created);
+    if (rc) short_strand(cls, rec_start[r], n, 1, k, shift, table, capmask, flags, created);
   }
+  block_count(created, flags);
 }
 
 // Extra empty records that the reference's checkpoint/resume yields (see
-// DESIGN.md): each adds the n<k sentinel.
+// pangenome_amd/host.py): each adds the n<k sentinel.
 __global__ void k_set_flag(unsigned* flags) { atomicOr(flags, 1u); }
 
-// K5: degree scan.  Marks rdBG membership in the slot and compacts the rdBG
-// keys (forward orientation c, reverse orientation rc(c)).
+// K5: degree scan.  One block per 4096-slot tile (slot = tile*4096 + j*256 +
+// tid, coalesced 16-byte loads); members are counted, block-scanned and placed
+// with one global atomic per tile, then written by a second sweep that
+// re-reads only member slots.  Marks rdBG membership in the slot for the walks.
+constexpr int RJ = 16;
+constexpr uint64_t RTILE = 256 * RJ;
+
 __global__ void __launch_bounds__(256)
 k_reduce(Slot* __restrict__ table, uint64_t cap, int k, unsigned long long* __restrict__ out,
          unsigned long long* __restrict__ counters) {
+  __shared__ uint32_t lds[4];
+  __shared__ unsigned long long tile_base;
   __shared__ unsigned long long red[4];
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
+  const uint64_t ntile = cap / RTILE;
   unsigned long long ndbg = 0;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint4 v = *reinterpret_cast<const uint4*>(table + i);
-    const unsigned long long key1 = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
-    const uint32_t m = v.z;
-    const bool occ = key1 != 0ull;
-    const bool pa = occ && (m & PRES_A), pb = occ && (m & PRES_B);
-    const bool ma = pa && rdbg_member(m & MASK12);
-    const bool mb = pb && rdbg_member((m >> 16) & MASK12);
-    ndbg += (unsigned long long)pa + (unsigned long long)pb;
-    if (ma || mb) table[i].mask = m | (ma ? RDBG_A : 0u) | (mb ? RDBG_B : 0u);
-    const unsigned long long ba = __ballot(ma), bb = __ballot(mb);
-    const unsigned na = __builtin_popcountll(ba), nbb = __builtin_popcountll(bb);
-    if (na + nbb == 0) continue;
-    unsigned long long base = 0;
-    if (lane == __builtin_ctzll(ba | bb)) base = atomicAdd(counters, (unsigned long long)(na + nbb));
-    base = __shfl(base, __builtin_ctzll(ba | bb), 64);
-    const uint64_t c = key1 - 1ull;
-    if (ma) out[base + __builtin_popcountll(ba & lt)] = c;
-    if (mb) out[base + na + __builtin_popcountll(bb & lt)] = rc_key(c, k);
+  for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
+    const uint64_t base = t * RTILE + threadIdx.x;
+    uint32_t cnt = 0, bits = 0;
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+      Slot* s = table + base + (uint64_t)j * 256;
+      const uint4 v = *reinterpret_cast<const uint4*>(s);
+      const bool occ = (v.x | v.y) != 0u;
+      const uint32_t m = v.z;
+      const bool pa = occ && (m & PRES_A), pb = occ && (m & PRES_B);
+      const bool ma = pa && rdbg_member(m & MASK12);
+      const bool mb = pb && rdbg_member((m >> 16) & MASK12);
+      ndbg += (unsigned long long)pa + (unsigned long long)pb;
+      cnt += (uint32_t)ma + (uint32_t)mb;
+      bits |= ((uint32_t)ma | ((uint32_t)mb << 1)) << (2 * j);
+      if (ma || mb) s->mask = m | (ma ? RDBG_A : 0u) | (mb ? RDBG_B : 0u);
+    }
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<256>(cnt, lds, tot);
+    if (threadIdx.x == 0) tile_base = tot ? atomicAdd(counters, (unsigned long long)tot) : 0ull;
+    __syncthreads();
+    unsigned long long o = tile_base + pre;
+    while (bits) {
+      const int b = __builtin_ctz(bits);
+      const uint64_t c = table[base + (uint64_t)(b >> 1) * 256].key1 - 1ull;
+      out[o++] = (b & 1) ? rc_key(c, k) : c;
+      bits &= bits - 1u;
+    }
+    __syncthreads();                               // tile_base is reused next tile
   }
   for (int o = 32; o > 0; o >>= 1) ndbg += __shfl_down(ndbg, o, 64);
-  if (lane == 0) red[threadIdx.x >> 6] = ndbg;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ndbg;
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long t = red[0] + red[1] + red[2] + red[3];
@@ -295,8 +304,9 @@ __global__ void k_part_scatter(const Slot* __restrict__ table, uint64_t cap, int
   }
 }
 
-__global__ void k_merge(const Slot* __restrict__ pairs, uint64_t n, Slot* __restrict__ table,
-                        uint64_t capmask, unsigned* __restrict__ flags) {
+__global__ void __launch_bounds__(IBLOCK)
+k_merge(const Slot* __restrict__ pairs, uint64_t n, Slot* __restrict__ table, uint64_t capmask,
+        unsigned* __restrict__ flags) {
   unsigned created = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
@@ -304,22 +314,10 @@ __global__ void k_merge(const Slot* __restrict__ pairs, uint64_t n, Slot* __rest
     if (!s.key1) continue;
     created += (unsigned)table_or(table, capmask, s.key1 - 1ull, s.mask & ~(RDBG_A | RDBG_B), flags);
   }
-  for (int o = 32; o > 0; o >>= 1) created += __shfl_down(created, o, 64);
-  if ((threadIdx.x & 63) == 0 && created) atomicAdd(counter(flags, blockIdx.x % N_CNT), created);
+  block_count(created, flags);
 }
 
 // ------------------------------------------------------------------ host
-static unsigned insert_grid() {
-  static unsigned g = 0;
-  if (!g) {
-    int dev = 0, cus = 256;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) cus = 256;
-    g = (unsigned)cus * 8u;
-  }
-  return g;
-}
-
 static void alloc_table(Ctx& c, uint64_t cap) {
   c.cap = cap;
   c.table.reserve(cap * sizeof(Slot));
@@ -342,6 +340,40 @@ static void read_flags(Ctx& c, unsigned& sentinel, unsigned& overflow, uint64_t&
   for (int i = 0; i < N_CNT; ++i) created += f[16 * (1 + i)];
 }
 
+// Tiles of records with n >= k+2, stripe-major: stripe 0 of every record, then
+// stripe 1, ...  (records with more stripes first within a stripe).  Packed as
+// record << 32 | stripe.  Cached while the record table and flags repeat.
+static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
+  const uint64_t R = c.n_records;
+  if (c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k) return c.n_tiles;
+  std::vector<std::pair<uint64_t, int>> nt;           // (stripes, record)
+  uint64_t total = 0, maxs = 0;
+  for (uint64_t r = 0; r < R; ++r) {
+    const int64_t n = c.h_rec_len[r];
+    if (!flag[r] || n < c.k + 2) continue;
+    const uint64_t s = (uint64_t)((n - c.k + 1 + TILE - 1) / TILE);
+    nt.push_back({s, (int)r});
+    total += s;
+    maxs = std::max(maxs, s);
+  }
+  std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  std::vector<unsigned long long> tiles;
+  tiles.reserve(total);
+  size_t live = nt.size();
+  for (uint64_t j = 0; j < maxs; ++j) {
+    while (live && nt[live - 1].first <= j) --live;
+    for (size_t i = 0; i < live; ++i) tiles.push_back(((unsigned long long)nt[i].second << 32) | j);
+  }
+  c.tiles.reserve(8 * (total + 1));
+  if (total) PG_HIP(hipMemcpyAsync(c.tiles.p, tiles.data(), 8 * total, hipMemcpyHostToDevice, c.stream));
+  c.sync();
+  c.tile_sig_len = c.h_rec_len;
+  c.tile_sig_flag = flag;
+  c.tile_k = c.k;
+  c.n_tiles = total;
+  return total;
+}
+
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   if (!c.parsed) throw Error(-22, "build_dbg: no parsed FASTA (call pg_parse first)");
   const uint64_t R = c.n_records;
@@ -349,18 +381,17 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   c.built = c.reduced = false;
   c.n_dbg = c.n_rdbg = c.n_canon = 0;
   c.windows_fw = 0;
-  if (R) {
-    std::vector<uint8_t> flag(R, 1);
-    if (h_rec_flag)
-      for (uint64_t r = 0; r < R; ++r) flag[r] = h_rec_flag[r] & 1;
-    PG_HIP(hipMemcpyAsync(c.rec_flag.p, flag.data(), R, hipMemcpyHostToDevice, c.stream));
-    for (uint64_t r = 0; r < R; ++r)
-      if (flag[r]) {
-        const int64_t n = c.h_rec_len[r];
-        c.windows_fw += n > c.k ? (uint64_t)(n - c.k + 1) : 1;
-      }
-  }
+  std::vector<uint8_t> flag(R, 1);
+  if (h_rec_flag)
+    for (uint64_t r = 0; r < R; ++r) flag[r] = h_rec_flag[r] & 1;
+  if (R) PG_HIP(hipMemcpyAsync(c.rec_flag.p, flag.data(), R, hipMemcpyHostToDevice, c.stream));
+  for (uint64_t r = 0; r < R; ++r)
+    if (flag[r]) {
+      const int64_t n = c.h_rec_len[r];
+      c.windows_fw += n > c.k ? (uint64_t)(n - c.k + 1) : 1;
+    }
   c.windows_total = c.windows_fw * (rc0 ? 2 : 1);
+  const uint64_t ntiles = make_tiles(c, flag);
   // table size: learned capacity, else a conservative guess; rebuilt on overflow
   uint64_t cap = c.cap_hint ? c.cap_hint : next_pow2(std::max<uint64_t>(1ull << 20, c.windows_fw));
   const uint64_t shift = pow5(c.k - 1);
@@ -373,22 +404,20 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     Slot* tab = c.table.as<Slot>();
     unsigned* flags = c.flags.as<unsigned>();
     c.t1.start(c.stream);
-    if (c.n_bases) {
+    if (ntiles) {
       if (rc0)
-        hipLaunchKernelGGL((k_insert<16, true>), dim3(insert_grid()), dim3(IBLOCK), 0, c.stream,
-                           c.cls.as<uint8_t>(), c.n_bases + (uint64_t)c.h_rec_start[0],
-                           c.rec_start.as<long long>(), c.rec_len.as<long long>(), c.rec_flag.as<uint8_t>(),
-                           R, c.k, shift, tab, cap - 1, flags);
+        hipLaunchKernelGGL(k_insert<true>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
+                           c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
+                           c.k, shift, tab, cap - 1, flags);
       else
-        hipLaunchKernelGGL((k_insert<16, false>), dim3(insert_grid()), dim3(IBLOCK), 0, c.stream,
-                           c.cls.as<uint8_t>(), c.n_bases + (uint64_t)c.h_rec_start[0],
-                           c.rec_start.as<long long>(), c.rec_len.as<long long>(), c.rec_flag.as<uint8_t>(),
-                           R, c.k, shift, tab, cap - 1, flags);
+        hipLaunchKernelGGL(k_insert<false>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
+                           c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
+                           c.k, shift, tab, cap - 1, flags);
       PG_HIP(hipGetLastError());
     }
     c.t1.stop(c.stream);
     if (R) {
-      hipLaunchKernelGGL(k_short, dim3(grid_for(R, 256, 1024)), dim3(256), 0, c.stream,
+      hipLaunchKernelGGL(k_short, dim3(grid_for(R, IBLOCK, 1024)), dim3(IBLOCK), 0, c.stream,
                          c.cls.as<uint8_t>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
                          c.rec_flag.as<uint8_t>(), R, c.k, shift, rc0, tab, cap - 1, flags);
       PG_HIP(hipGetLastError());
@@ -413,15 +442,12 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
 
 void build_rdbg(Ctx& c) {
   if (!c.built) throw Error(-22, "build_rdbg: no dBG (call pg_build_dbg first)");
-  unsigned sentinel = 0, overflow = 0;
-  uint64_t created = 0;
-  read_flags(c, sentinel, overflow, created);
   c.rdbg_keys.reserve(8 * (2 * c.n_canon + 2));
   DevBuf& cnt = c.n_sel;
   cnt.reserve(128);
   PG_HIP(hipMemsetAsync(cnt.p, 0, 128, c.stream));
   c.t0.start(c.stream);
-  hipLaunchKernelGGL(k_reduce, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, c.stream,
+  hipLaunchKernelGGL(k_reduce, dim3(grid_for(c.cap / RTILE, 1, 8192)), dim3(256), 0, c.stream,
                      c.table.as<Slot>(), c.cap, c.k, c.rdbg_keys.as<unsigned long long>(),
                      cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
@@ -432,7 +458,7 @@ void build_rdbg(Ctx& c) {
   c.ms_scan = c.t0.ms();
   c.n_rdbg = res[0];
   c.n_dbg = res[8];
-  if (sentinel) {           // key 2^64-1, mask 32: always an rdBG member
+  if (c.sentinel) {         // key 2^64-1, mask 32: always an rdBG member
     unsigned long long s = SENTINEL;
     PG_HIP(hipMemcpyAsync(c.rdbg_keys.as<unsigned long long>() + c.n_rdbg, &s, 8, hipMemcpyHostToDevice,
                           c.stream));
@@ -445,9 +471,6 @@ void build_rdbg(Ctx& c) {
 
 uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {
   if (!c.built) throw Error(-22, "export_dbg: no dBG");
-  unsigned sentinel = 0, overflow = 0;
-  uint64_t created = 0;
-  read_flags(c, sentinel, overflow, created);
   const uint64_t nmax = 2 * c.n_canon + 1;
   DevBuf keys, masks, cnt;
   keys.reserve(8 * nmax);
@@ -461,11 +484,11 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {
   unsigned long long n = 0;
   PG_HIP(hipMemcpyAsync(&n, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  const uint64_t total = n + (sentinel ? 1 : 0);
+  const uint64_t total = n + (c.sentinel ? 1 : 0);
   if (h_keys && cap >= total) {
     PG_HIP(hipMemcpy(h_keys, keys.p, 8 * n, hipMemcpyDeviceToHost));
     PG_HIP(hipMemcpy(h_masks, masks.p, 2 * n, hipMemcpyDeviceToHost));
-    if (sentinel) { h_keys[n] = SENTINEL; h_masks[n] = 32; }
+    if (c.sentinel) { h_keys[n] = SENTINEL; h_masks[n] = 32; }
   }
   keys.release(); masks.release(); cnt.release();
   return total;
@@ -506,14 +529,14 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
 
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel) {
   uint64_t cap = cap_hint ? next_pow2(cap_hint) : next_pow2(std::max<uint64_t>(1ull << 16, 2 * n));
+  c.t1.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
     alloc_table(c, cap);
     clear_table(c);
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
-    c.t1.init();
     c.t1.start(c.stream);
     if (n)
-      hipLaunchKernelGGL(k_merge, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c.stream,
+      hipLaunchKernelGGL(k_merge, dim3(grid_for(n, IBLOCK, 8192)), dim3(IBLOCK), 0, c.stream,
                          reinterpret_cast<const Slot*>(d_pairs), n, c.table.as<Slot>(), cap - 1,
                          c.flags.as<unsigned>());
     PG_HIP(hipGetLastError());

@@ -105,7 +105,11 @@ struct Ctx {
   uint64_t windows_fw = 0, windows_total = 0;
 
   // ---- walk passes (edges / labels)
-  DevBuf tiles;                   // per-record tiles for ordered compaction
+  DevBuf tiles;                   // K3 tile list (record << 32 | stripe), stripe-major
+  uint64_t n_tiles = 0;
+  int tile_k = 0;
+  std::vector<int64_t> tile_sig_len;   // record lengths / flags the tile list was built for
+  std::vector<uint8_t> tile_sig_flag;
   DevBuf tile_cnt, tile_off;      // per tile x strand counts / offsets
   DevBuf occ;                     // member / hit occurrences, walk ordered
   DevBuf edge_tab, pair_tab;      // edge table and (edge, walk) dedup set

@@ -52,29 +52,6 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
   return (w >> (8 * (j & 3))) & 0xFFu;
 }
 
-// exclusive block scan (256 threads = 4 waves of 64)
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, uint32_t& total) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    uint32_t y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) lds[wid] = x;
-  __syncthreads();
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < PBLOCK / 64; ++w) {
-    uint32_t s = lds[w];
-    pre += (w < wid) ? s : 0u;
-    tot += s;
-  }
-  __syncthreads();
-  total = tot;
-  return pre + x - v;
-}
-
 __global__ void __launch_bounds__(PBLOCK) k_nl_count(const uint8_t* __restrict__ buf, uint64_t n,
                                                      unsigned long long* __restrict__ blk_nl) {
   __shared__ uint32_t lds[PBLOCK / 64];
@@ -86,7 +63,7 @@ __global__ void __launch_bounds__(PBLOCK) k_nl_count(const uint8_t* __restrict__
     if (p < n) cnt += count_nl16(load16(buf, p, n));
   }
   uint32_t tot;
-  (void)block_excl_scan(cnt, lds, tot);
+  (void)block_excl_scan<PBLOCK>(cnt, lds, tot);
   if (threadIdx.x == 0) blk_nl[blockIdx.x] = tot;
 }
 
@@ -102,7 +79,7 @@ __global__ void __launch_bounds__(PBLOCK) k_nl_write(const uint8_t* __restrict__
     uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
     uint32_t c = p < n ? count_nl16(v) : 0u;
     uint32_t tot;
-    uint32_t pre = block_excl_scan(c, lds, tot);
+    uint32_t pre = block_excl_scan<PBLOCK>(c, lds, tot);
     if (c) {
       uint64_t o = run + pre;
       for (int j = 0; j < 16; ++j)
@@ -168,7 +145,7 @@ __global__ void __launch_bounds__(PBLOCK) k_copy(const uint8_t* __restrict__ buf
     uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
     uint32_t c = p < n ? count_nl16(v) : 0u;
     uint32_t tot;
-    uint32_t pre = block_excl_scan(c, lds, tot);
+    uint32_t pre = block_excl_scan<PBLOCK>(c, lds, tot);
     if (p < n) {
       uint64_t li = run + pre;
       uint64_t cur = ~0ull;
