@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpangenome_hip.so")
+LIB_PATH = os.path.join(HERE, os.environ.get("PG_LIB_NAME", "libpangenome_hip.so"))   # diag builds only
 
 PG_OK = 0
 

@@ -48,26 +48,97 @@ constexpr uint32_t LAM_HASH = 0;      // '#' start marker
 constexpr uint64_t SENTINEL = ~0ull;  // the n<k key (-1 stored in a uint64 array, :1038)
 
 // ------------------------------------------------------------------ table
-// One canonical k-mer per 16-byte slot.  A key X and its reverse complement
-// rc(X) share the slot of c = min(X, rc(X)); the slot keeps the reference's
-// 12-bit OR-mask of each orientation separately (A for c, B for rc(c)), so the
-// dBG exported from it is exactly the reference's non-canonical dBG
-// (kmer_numba.py:1036-1047, :1215-1221).  key1 = c + 1, so an all-zero slot is
-// empty and the table is cleared by one memset (c < 5^27 < 2^63).
-struct alignas(16) Slot {
-  unsigned long long key1;
-  unsigned int mask;   // [0,12) A | 1<<12 presA | 1<<13 rdbgA | [16,28) B | 1<<28 presB | 1<<29 rdbgB
-  unsigned int aux;
-};
-constexpr uint32_t PRES_A = 1u << 12, RDBG_A = 1u << 13;
-constexpr uint32_t PRES_B = 1u << 28, RDBG_B = 1u << 29;
+// One canonical k-mer per entry.  A key X and its reverse complement rc(X)
+// share the entry of c = min(X, rc(X)); the entry keeps the reference's 12-bit
+// OR-mask of each orientation separately (A for c, B for rc(c)), so the dBG
+// exported from it is exactly the reference's non-canonical dBG
+// (kmer_numba.py:1036-1047, :1215-1221).
+//
+// Mask word (26 bits): [0,12) A | 1<<12 presA | [13,25) B | 1<<25 presB.
+// A presence bit is needed because a key's mask can be 0 (e.g. '#' before,
+// IUPAC after).
+constexpr uint32_t PRES_A = 1u << 12;
+constexpr int B_SHIFT = 13;
+constexpr uint32_t PRES_B = PRES_A << B_SHIFT;
 constexpr uint32_t MASK12 = 0xFFFu;
+constexpr int MW_BITS = 26;
+constexpr uint64_t MW_MASK = (1ull << MW_BITS) - 1;
 
 __host__ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
   k ^= k >> 33; k *= 0xff51afd7ed558ccdull;
   k ^= k >> 33; k *= 0xc4ceb9fe1a85ec53ull;
   k ^= k >> 33;
   return k;
+}
+
+// 16-byte entry: the overflow table's slots and the multi-GPU exchange record.
+// key1 = c + 1 (0 = empty).
+struct alignas(16) Slot {
+  unsigned long long key1;
+  unsigned int mask;   // 26-bit mask word
+  unsigned int aux;
+};
+
+// The primary table is quotiented: a bijective hash h = perm(c) of the kb-bit
+// key splits into a bucket index (high bits) and a quotient (low qbits <= 38
+// bits), so [quotient | 26-bit mask word] is one 64-bit word and a new key is
+// created, masks included, by a single 64-bit CAS.  A bucket is 2 words (one
+// 16-byte load per probe); a key whose bucket is full goes to the small
+// overflow table of 16-byte slots (linear probing).  Entries only ever go
+// empty -> key and masks only gain bits, which is what lets readers tolerate
+// stale plain loads (device atomics execute beyond the XCD's L2).
+struct TableView {
+  unsigned long long* prim;    // 2 words per bucket
+  uint64_t bmask;              // buckets - 1
+  uint32_t qbits, sh1, sh2, pad;
+  uint64_t kmask, m1, m2, m1i, m2i;
+  Slot* ovf;
+  uint64_t omask;              // overflow slots - 1
+
+  __host__ __device__ __forceinline__ uint64_t perm(uint64_t c) const {
+    uint64_t h = (c * m1) & kmask;
+    h ^= h >> sh1;
+    h = (h * m2) & kmask;
+    h ^= h >> sh2;
+    return h;
+  }
+  __host__ __device__ __forceinline__ static uint64_t unxs(uint64_t y, uint32_t s) {
+    uint64_t x = y;
+    for (uint32_t i = s; i < 64; i += s) x = y ^ (x >> s);
+    return x;
+  }
+  __host__ __device__ __forceinline__ uint64_t unperm(uint64_t h) const {
+    h = unxs(h, sh2);
+    h = (h * m2i) & kmask;
+    h = unxs(h, sh1);
+    return (h * m1i) & kmask;
+  }
+  // key of the primary word w of bucket b
+  __host__ __device__ __forceinline__ uint64_t key_of(uint64_t b, unsigned long long w) const {
+    return unperm((b << qbits) | (uint64_t)(w >> MW_BITS));
+  }
+};
+
+// Read-only lookup (kernels after the build): the 26-bit mask word of c, or 0.
+// A bucket's second word is only ever filled after its first, and the overflow
+// table only after both, so an empty word ends the search.
+__device__ __forceinline__ uint32_t tab_get(const TableView& T, uint64_t c) {
+  const uint64_t h = T.perm(c);
+  const uint64_t b = h >> T.qbits, q = h & ((1ull << T.qbits) - 1ull);
+  const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(T.prim + 2 * b);
+  if (v.x == 0ull) return 0u;
+  if ((v.x >> MW_BITS) == q) return (uint32_t)(v.x & MW_MASK);
+  if (v.y == 0ull) return 0u;
+  if ((v.y >> MW_BITS) == q) return (uint32_t)(v.y & MW_MASK);
+  const unsigned long long key1 = c + 1ull;
+  uint64_t slot = fmix64(c) & T.omask;
+  for (uint64_t probe = 0; probe <= T.omask; ++probe) {
+    const Slot s = T.ovf[slot];
+    if (s.key1 == key1) return s.mask;
+    if (s.key1 == 0ull) return 0u;
+    slot = (slot + 1) & T.omask;
+  }
+  return 0u;
 }
 
 // modular inverse of 5 mod 2^64: (K - d) is a multiple of 5 when d is K's low

@@ -1,4 +1,4 @@
-// pg_dbg.hip — K3: k-mer windows -> open-addressed HBM table (atomic OR of
+// pg_dbg.hip — K3: k-mer windows -> quotiented HBM hash table (atomic OR of
 // neighbour masks); K5: degree scan + rdBG compaction; exports and the
 // owner-partitioned exchange used by the multi-GPU build.
 //
@@ -16,11 +16,12 @@
 // Homology-aware order.  A pangenome repeats each k-mer once per genome at
 // nearly the same offset, so K3 walks tiles of TILE windows stripe-major
 // (stripe j of every record, then stripe j+1, ...) and remaps blocks so one
-// stripe's tiles run on one XCD: the first genome's probe of a slot misses,
+// stripe's tiles run on one XCD: the first genome's probe of a bucket misses,
 // the other genomes' probes of it hit that XCD's L2 / the Infinity Cache.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
-#include <numeric>
 #include <rocprim/rocprim.hpp>
 
 #include "pg_internal.h"
@@ -30,22 +31,19 @@ namespace pg {
 constexpr int IBLOCK = 256;
 constexpr int IW = 16;                        // windows per thread
 constexpr int TILE = IBLOCK * IW;             // windows per tile (one block)
-constexpr int MAX_PROBE = 4096;
+constexpr int IB = 8;                         // windows per probe batch
+constexpr int SPAN = TILE + 64;               // staged bytes (k <= 27: TILE + k + 3 <= SPAN - 16)
 constexpr int N_CNT = 64;                     // spread counters (one 64-byte line each)
 
 // flags layout (uint32 words): [0] sentinel seen, [1] overflow, [16*(1+i)] counter i
 __device__ __forceinline__ unsigned* counter(unsigned* flags, int i) { return flags + 16 * (1 + i); }
 
-// Insert/OR one canonical key.  Returns 1 if this call created the slot.
-// Plain loads may be stale (atomics run beyond the XCD's L2), but a slot only
-// ever goes empty -> key and masks only gain bits: a stale empty is settled
-// by the CAS's return value, a stale mask only costs a redundant atomicOr.
-__device__ __forceinline__ int table_or(Slot* __restrict__ table, uint64_t capmask, uint64_t c,
-                                        uint32_t mw, unsigned* flags) {
+// overflow table: linear probing on 16-byte slots (CAS on key1, then OR)
+__device__ int ovf_or(const TableView& T, uint64_t c, uint32_t mw, unsigned* flags) {
   const unsigned long long key1 = (unsigned long long)c + 1ull;
-  uint64_t slot = fmix64(c) & capmask;
-  for (int probe = 0; probe < MAX_PROBE; ++probe) {
-    Slot* s = table + slot;
+  uint64_t slot = fmix64(c) & T.omask;
+  for (uint64_t probe = 0; probe <= T.omask && probe < 65536; ++probe) {
+    Slot* s = T.ovf + slot;
     const uint4 v = *reinterpret_cast<const uint4*>(s);
     const unsigned long long kk = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
     if (kk == key1) {
@@ -59,10 +57,55 @@ __device__ __forceinline__ int table_or(Slot* __restrict__ table, uint64_t capma
         return old == 0ull;
       }
     }
-    slot = (slot + 1) & capmask;
+    slot = (slot + 1) & T.omask;
   }
   atomicOr(flags + 1, 1u);
   return 0;
+}
+
+#ifdef PG_DIAG
+// diagnostic build only: per-path event counters at flags[16*(2+N_CNT)+i]
+#define DIAG(i) atomicAdd(flags + 16 * (2 + N_CNT) + (i), 1u)
+#else
+#define DIAG(i) ((void)0)
+#endif
+
+// Insert/OR one canonical key given its bucket words v (possibly stale: a
+// stale empty is settled by the CAS result, a stale mask only costs a
+// redundant atomicOr).  Returns 1 if this call created the entry.
+__device__ __forceinline__ int tab_or_at(const TableView& T, uint64_t c, uint64_t b, uint64_t q, uint32_t mw,
+                                         ulonglong2 v, unsigned* flags) {
+  unsigned long long* w = T.prim + 2 * b;
+  unsigned long long x = v.x;
+  DIAG(0);
+  if (x == 0ull) {
+    DIAG(1);
+    x = atomicCAS(w, 0ull, (q << MW_BITS) | mw);
+    if (x == 0ull) { DIAG(2); return 1; }
+  }
+  if ((x >> MW_BITS) == q) {
+    if ((x & mw) != mw) { DIAG(3); atomicOr(w, (unsigned long long)mw); }
+    return 0;
+  }
+  x = v.y;
+  if (x == 0ull) {
+    DIAG(4);
+    x = atomicCAS(w + 1, 0ull, (q << MW_BITS) | mw);
+    if (x == 0ull) { DIAG(5); return 1; }
+  }
+  if ((x >> MW_BITS) == q) {
+    if ((x & mw) != mw) { DIAG(6); atomicOr(w + 1, (unsigned long long)mw); }
+    return 0;
+  }
+  DIAG(7);
+  return ovf_or(T, c, mw, flags);
+}
+
+__device__ __forceinline__ int tab_or(const TableView& T, uint64_t c, uint32_t mw, unsigned* flags) {
+  const uint64_t h = T.perm(c);
+  const uint64_t b = h >> T.qbits, q = h & ((1ull << T.qbits) - 1ull);
+  const ulonglong2 v = *reinterpret_cast<const ulonglong2*>(T.prim + 2 * b);
+  return tab_or_at(T, c, b, q, mw, v, flags);
 }
 
 __device__ __forceinline__ void block_count(unsigned created, unsigned* flags) {
@@ -79,90 +122,129 @@ __device__ __forceinline__ void block_count(unsigned created, unsigned* flags) {
 }
 
 // K3.  One block per tile (record, stripe j): windows [j*TILE, (j+1)*TILE) of
-// a record with n >= k+2; thread t takes IW consecutive windows and rolls the
-// keys of both strands across them.
+// a record with n >= k+2.  The tile's class codes (plus the k+3 bytes of
+// context around it) are staged in LDS with 16-byte loads; thread t takes IW
+// consecutive windows, rolls both strands' keys across them, and probes the
+// table in batches of IB windows: IB independent bucket loads in flight per
+// lane, and only windows whose entry is not already complete take the CAS /
+// atomicOr / overflow path.
 template <bool RC>
 __global__ void __launch_bounds__(IBLOCK)
 k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__ tiles,
          const long long* __restrict__ rec_start, const long long* __restrict__ rec_len, int k, uint64_t shift,
-         Slot* __restrict__ table, uint64_t capmask, unsigned* __restrict__ flags) {
+         TableView T, unsigned* __restrict__ flags) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   const unsigned long long tile = tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
   const int r = (int)(tile >> 32);
   const long long rs = rec_start[r], rn = rec_len[r];
   const long long last = rn - k;                              // last window index
-  const long long q0 = (long long)(tile & 0xFFFFFFFFull) * TILE + (long long)threadIdx.x * IW;
+  const long long qt = (long long)(tile & 0xFFFFFFFFull) * TILE;
+  // stage positions [lo, hi) of the record: windows qt .. qt+TILE-1 read from
+  // q-2 (last-window pred) to q+k+1 (twin pred of window 0)
+  const long long lo = rs + (qt >= 2 ? qt - 2 : 0);
+  const long long hi = rs + (qt + TILE + k + 2 < rn ? qt + TILE + k + 2 : rn);
+  const long long a0 = lo & ~15ll;                            // 16-byte aligned source
+  for (long long off = (long long)threadIdx.x * 16; a0 + off < hi; off += IBLOCK * 16)
+    *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + a0 + off);
+  __syncthreads();
+  const long long base = rs - a0;                             // s_cls index of record position 0
+  auto S = [&](long long q) -> uint32_t { return s_cls[base + q]; };
+
+  const long long q0 = qt + (long long)threadIdx.x * IW;
   const long long q1 = q0 + IW <= last + 1 ? q0 + IW : last + 1;
+  const uint64_t qmask = (1ull << T.qbits) - 1ull;
   unsigned created = 0;
   uint64_t K = 0, Kr = 0;
-  for (long long q = q0; q < q1; ++q) {
-    const uint64_t p = (uint64_t)(rs + q);
-    if (q == q0) {
-      uint64_t pw = 1;
-      for (int j = 0; j < k; ++j) {                // k2n_jit (:975-985), both strands
-        const uint32_t cj = cls[p + j];
-        K += (uint64_t)digit_fw(cj) * pw;
-        Kr = Kr * 5 + digit_rc(cj);
-        pw *= 5;
+  if (q0 < q1) {
+    uint64_t pw = 1;
+    for (int j = 0; j < k; ++j) {                  // k2n_jit (:975-985), both strands
+      const uint32_t cj = S(q0 + j);
+      K += (uint64_t)digit_fw(cj) * pw;
+      Kr = Kr * 5 + digit_rc(cj);
+      pw *= 5;
+    }
+  }
+  for (long long qb = q0; qb < q1; qb += IB) {
+    uint64_t cc[IB], hh[IB];
+    uint32_t mm[IB];
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const long long q = qb + i;
+      cc[i] = 0;
+      mm[i] = 0;
+      if (q < q1) {
+        if (q != q0) {                             // Nu // 5 + alpha * 5^(k-1) (:1072)
+          const uint32_t dout = S(q - 1), din = S(q + k - 1);
+          K = (K - digit_fw(dout)) * INV5 + (uint64_t)digit_fw(din) * shift;
+          Kr = (Kr - (uint64_t)digit_rc(dout) * shift) * 5 + digit_rc(din);
+        }
+        // forward window q: pred '#' at q==0, s[q-2] at the last window (:1080 quirk), else s[q-1]
+        const uint32_t fpred = q == 0 ? LAM_HASH : lam_fw(S(q - (q == last ? 2 : 1)));
+        const uint32_t fsucc = q == last ? LAM_DOLLAR : lam_fw(S(q + k));
+        const uint32_t mf = (fpred << OFFBIT) | fsucc | PRES_A;
+        if (RC) {
+          // its twin: reverse-strand window n-k-q, same boundary rules on that strand
+          const uint32_t rpred = q == last ? LAM_HASH : lam_rc(S(q + k + (q == 0 ? 1 : 0)));
+          const uint32_t rsucc = q == 0 ? LAM_DOLLAR : lam_rc(S(q - 1));
+          const uint32_t mr = (rpred << OFFBIT) | rsucc | PRES_A;
+          if (K < Kr)      { cc[i] = K;  mm[i] = mf | (mr << B_SHIFT); }
+          else if (K > Kr) { cc[i] = Kr; mm[i] = mr | (mf << B_SHIFT); }
+          else             { cc[i] = K;  mm[i] = mf | mr; }
+        } else {
+          if (K <= Kr) { cc[i] = K; mm[i] = mf; } else { cc[i] = Kr; mm[i] = mf << B_SHIFT; }
+        }
       }
-    } else {                                       // Nu // 5 + alpha * 5^(k-1) (:1072)
-      const uint32_t dout = cls[p - 1], din = cls[p + k - 1];
-      K = (K - digit_fw(dout)) * INV5 + (uint64_t)digit_fw(din) * shift;
-      Kr = (Kr - (uint64_t)digit_rc(dout) * shift) * 5 + digit_rc(din);
+      hh[i] = T.perm(cc[i]);
     }
-    // forward window q: pred '#' at q==0, s[q-2] at the last window (:1080 quirk), else s[q-1]
-    const uint32_t fpred = q == 0 ? LAM_HASH : lam_fw(cls[p - (q == last ? 2 : 1)]);
-    const uint32_t fsucc = q == last ? LAM_DOLLAR : lam_fw(cls[p + k]);
-    const uint32_t mf = (fpred << OFFBIT) | fsucc | PRES_A;
-    uint64_t c;
-    uint32_t mw;
-    if (RC) {
-      // its twin: reverse-strand window n-k-q, same boundary rules on that strand
-      const uint32_t rpred = q == last ? LAM_HASH : lam_rc(cls[p + k + (q == 0 ? 1 : 0)]);
-      const uint32_t rsucc = q == 0 ? LAM_DOLLAR : lam_rc(cls[p - 1]);
-      const uint32_t mr = (rpred << OFFBIT) | rsucc | PRES_A;
-      if (K < Kr)      { c = K;  mw = mf | (mr << 16); }
-      else if (K > Kr) { c = Kr; mw = mr | (mf << 16); }
-      else             { c = K;  mw = mf | mr; }
-    } else {
-      if (K <= Kr) { c = K; mw = mf; } else { c = Kr; mw = mf << 16; }
+    ulonglong2 v[IB];
+#pragma unroll
+    for (int i = 0; i < IB; ++i)                   // IB independent probes in flight (unconditional:
+      v[i] = *reinterpret_cast<const ulonglong2*>(T.prim + 2 * (hh[i] >> T.qbits));   // no per-load branch)
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      if (!mm[i]) continue;
+      const uint64_t b = hh[i] >> T.qbits, q = hh[i] & qmask;
+      const bool done0 = v[i].x != 0ull && (v[i].x >> MW_BITS) == q && (v[i].x & mm[i]) == mm[i];
+      const bool done1 = v[i].y != 0ull && (v[i].y >> MW_BITS) == q && (v[i].y & mm[i]) == mm[i];
+      if (done0 || done1) continue;                // complete: nothing to do
+      created += (unsigned)tab_or_at(T, cc[i], b, q, mm[i], v[i], flags);
     }
-    created += (unsigned)table_or(table, capmask, c, mw, flags);
   }
   block_count(created, flags);
 }
 
 // one reference window of an explicit strand (used for records with n <= k+1)
-__device__ __forceinline__ void oriented_or(Slot* table, uint64_t capmask, int k, uint64_t x,
-                                            uint32_t m12, unsigned* flags, unsigned& created) {
+__device__ __forceinline__ void oriented_or(const TableView& T, int k, uint64_t x, uint32_t m12,
+                                            unsigned* flags, unsigned& created) {
   const uint64_t xr = rc_key(x, k);
   const uint32_t m = m12 | PRES_A;
-  if (x <= xr) created += (unsigned)table_or(table, capmask, x, m, flags);
-  else created += (unsigned)table_or(table, capmask, xr, m << 16, flags);
+  if (x <= xr) created += (unsigned)tab_or(T, x, m, flags);
+  else created += (unsigned)tab_or(T, xr, m << B_SHIFT, flags);
 }
 
 // build_dbg for one strand of length n in {k, k+1}.  strand 0: s[i] = cls[rs+i];
 // strand 1: s[i] = comp_class(cls[rs+n-1-i]) (tab_rev(reversed(s)), :1217).
 __device__ void short_strand(const uint8_t* cls, long long rs, long long n, int strand, int k,
-                             uint64_t shift, Slot* table, uint64_t capmask, unsigned* flags, unsigned& created) {
+                             uint64_t shift, const TableView& T, unsigned* flags, unsigned& created) {
   auto S = [&](long long i) -> uint32_t {
     return strand == 0 ? (uint32_t)cls[rs + i] : comp_class(cls[rs + n - 1 - i]);
   };
   uint64_t K0 = 0, pw = 1;
   for (int j = 0; j < k; ++j) { K0 += (uint64_t)digit_fw(S(j)) * pw; pw *= 5; }
   if (n == k) {                                            // :1084-1085
-    oriented_or(table, capmask, k, K0, (LAM_HASH << OFFBIT) | LAM_DOLLAR, flags, created);
+    oriented_or(T, k, K0, (LAM_HASH << OFFBIT) | LAM_DOLLAR, flags, created);
     return;
   }
   // n == k+1 (:1061-1082): the loop never runs and numba reads its variable as 0
-  oriented_or(table, capmask, k, K0, (LAM_HASH << OFFBIT) | lam_fw(S(k)), flags, created);
+  oriented_or(T, k, K0, (LAM_HASH << OFFBIT) | lam_fw(S(k)), flags, created);
   const uint64_t K1 = K0 / 5 + (uint64_t)digit_fw(S(1)) * shift;   // alpha[seq[0+1]]
-  oriented_or(table, capmask, k, K1, (lam_fw(S(1)) << OFFBIT) | LAM_DOLLAR, flags, created);  // seq[0-k] == s[1]
+  oriented_or(T, k, K1, (lam_fw(S(1)) << OFFBIT) | LAM_DOLLAR, flags, created);  // seq[0-k] == s[1]
 }
 
 __global__ void __launch_bounds__(IBLOCK)
 k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start,
         const long long* __restrict__ rec_len, const uint8_t* __restrict__ rec_flag, uint64_t R, int k,
-        uint64_t shift, int rc, Slot* table, uint64_t capmask, unsigned* flags) {
+        uint64_t shift, int rc, TableView T, unsigned* flags) {
   unsigned created = 0;
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R;
        r += (uint64_t)gridDim.x * blockDim.x) {
@@ -170,8 +252,8 @@ k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start
     const long long n = rec_len[r];
     if (n > k + 1) continue;
     if (n < k) { atomicOr(flags, 1u); continue; }          // key -1, mask '$' (:1087-1088)
-    short_strand(cls, rec_start[r], n, 0, k, shift, table, capmask, flags, created);
-    if (rc) short_strand(cls, rec_start[r], n, 1, k, shift, table, capmask, flags, created);
+    short_strand(cls, rec_start[r], n, 0, k, shift, T, flags, created);
+    if (rc) short_strand(cls, rec_start[r], n, 1, k, shift, T, flags, created);
   }
   block_count(created, flags);
 }
@@ -180,37 +262,47 @@ k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start
 // pangenome_amd/host.py): each adds the n<k sentinel.
 __global__ void k_set_flag(unsigned* flags) { atomicOr(flags, 1u); }
 
-// K5: degree scan.  One block per 4096-slot tile (slot = tile*4096 + j*256 +
-// tid, coalesced 16-byte loads); members are counted, block-scanned and placed
-// with one global atomic per tile, then written by a second sweep that
-// re-reads only member slots.  Marks rdBG membership in the slot for the walks.
+// ---- table scans.  Entry index space: [0, 2*buckets) primary words, then
+// [2*buckets, 2*buckets + ovf) overflow slots; both are multiples of RTILE.
 constexpr int RJ = 16;
 constexpr uint64_t RTILE = 256 * RJ;
 
+__device__ __forceinline__ uint32_t entry_mask(const TableView& T, uint64_t nw, uint64_t i) {
+  if (i < nw) {
+    const unsigned long long w = T.prim[i];
+    return w ? (uint32_t)(w & MW_MASK) : 0u;
+  }
+  const Slot s = T.ovf[i - nw];
+  return s.key1 ? s.mask : 0u;
+}
+__device__ __forceinline__ uint64_t entry_key(const TableView& T, uint64_t nw, uint64_t i) {
+  if (i < nw) return T.key_of(i >> 1, T.prim[i]);
+  return T.ovf[i - nw].key1 - 1ull;
+}
+
+// K5: degree scan.  One block per RTILE-entry tile (entry = tile*RTILE + j*256
+// + tid, coalesced); members are counted, block-scanned and placed with one
+// global atomic per tile, then written by a second sweep over member entries.
 __global__ void __launch_bounds__(256)
-k_reduce(Slot* __restrict__ table, uint64_t cap, int k, unsigned long long* __restrict__ out,
+k_reduce(TableView T, uint64_t nw, uint64_t ntot, int k, unsigned long long* __restrict__ out,
          unsigned long long* __restrict__ counters) {
   __shared__ uint32_t lds[4];
   __shared__ unsigned long long tile_base;
   __shared__ unsigned long long red[4];
-  const uint64_t ntile = cap / RTILE;
+  const uint64_t ntile = ntot / RTILE;
   unsigned long long ndbg = 0;
   for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
     const uint64_t base = t * RTILE + threadIdx.x;
     uint32_t cnt = 0, bits = 0;
 #pragma unroll
     for (int j = 0; j < RJ; ++j) {
-      Slot* s = table + base + (uint64_t)j * 256;
-      const uint4 v = *reinterpret_cast<const uint4*>(s);
-      const bool occ = (v.x | v.y) != 0u;
-      const uint32_t m = v.z;
-      const bool pa = occ && (m & PRES_A), pb = occ && (m & PRES_B);
+      const uint32_t m = entry_mask(T, nw, base + (uint64_t)j * 256);
+      const bool pa = m & PRES_A, pb = m & PRES_B;
       const bool ma = pa && rdbg_member(m & MASK12);
-      const bool mb = pb && rdbg_member((m >> 16) & MASK12);
+      const bool mb = pb && rdbg_member((m >> B_SHIFT) & MASK12);
       ndbg += (unsigned long long)pa + (unsigned long long)pb;
       cnt += (uint32_t)ma + (uint32_t)mb;
       bits |= ((uint32_t)ma | ((uint32_t)mb << 1)) << (2 * j);
-      if (ma || mb) s->mask = m | (ma ? RDBG_A : 0u) | (mb ? RDBG_B : 0u);
     }
     uint32_t tot;
     const uint32_t pre = block_excl_scan<256>(cnt, lds, tot);
@@ -219,7 +311,7 @@ k_reduce(Slot* __restrict__ table, uint64_t cap, int k, unsigned long long* __re
     unsigned long long o = tile_base + pre;
     while (bits) {
       const int b = __builtin_ctz(bits);
-      const uint64_t c = table[base + (uint64_t)(b >> 1) * 256].key1 - 1ull;
+      const uint64_t c = entry_key(T, nw, base + (uint64_t)(b >> 1) * 256);
       out[o++] = (b & 1) ? rc_key(c, k) : c;
       bits &= bits - 1u;
     }
@@ -234,16 +326,16 @@ k_reduce(Slot* __restrict__ table, uint64_t cap, int k, unsigned long long* __re
   }
 }
 
-// dBG export: (key, 12-bit mask) of both orientations of every slot
-__global__ void k_export_dbg(const Slot* __restrict__ table, uint64_t cap, int k,
+// dBG export: (key, 12-bit mask) of both orientations of every entry
+__global__ void k_export_dbg(TableView T, uint64_t nw, uint64_t ntot, int k,
                              unsigned long long* __restrict__ keys, unsigned short* __restrict__ masks,
                              unsigned long long* __restrict__ counter) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntot;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    const Slot s = table[i];
-    const bool pa = s.key1 && (s.mask & PRES_A), pb = s.key1 && (s.mask & PRES_B);
+    const uint32_t m = entry_mask(T, nw, i);
+    const bool pa = m & PRES_A, pb = m & PRES_B;
     const unsigned long long ba = __ballot(pa), bb = __ballot(pb);
     const unsigned na = __builtin_popcountll(ba), nbb = __builtin_popcountll(bb);
     if (na + nbb == 0) continue;
@@ -251,43 +343,43 @@ __global__ void k_export_dbg(const Slot* __restrict__ table, uint64_t cap, int k
     unsigned long long base = 0;
     if (lane == leader) base = atomicAdd(counter, (unsigned long long)(na + nbb));
     base = __shfl(base, leader, 64);
-    const uint64_t c = s.key1 - 1ull;
-    if (pa) { uint64_t o = base + __builtin_popcountll(ba & lt); keys[o] = c; masks[o] = s.mask & MASK12; }
+    if (!(pa || pb)) continue;
+    const uint64_t c = entry_key(T, nw, i);
+    if (pa) { uint64_t o = base + __builtin_popcountll(ba & lt); keys[o] = c; masks[o] = m & MASK12; }
     if (pb) {
       uint64_t o = base + na + __builtin_popcountll(bb & lt);
-      keys[o] = rc_key(c, k); masks[o] = (s.mask >> 16) & MASK12;
+      keys[o] = rc_key(c, k); masks[o] = (m >> B_SHIFT) & MASK12;
     }
   }
 }
 
-// ---- multi-GPU exchange: owner = high bits of the slot hash mod nparts
+// ---- multi-GPU exchange: owner = high bits of a key hash mod nparts
 __device__ __forceinline__ int owner_of(uint64_t c, int nparts) {
   return (int)((fmix64(c) >> 40) % (uint64_t)nparts);
 }
 
-__global__ void k_part_count(const Slot* __restrict__ table, uint64_t cap, int nparts,
+__global__ void k_part_count(TableView T, uint64_t nw, uint64_t ntot, int nparts,
                              unsigned long long* __restrict__ counts) {
   __shared__ unsigned long long hist[64];
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) hist[i] = 0;
   __syncthreads();
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const unsigned long long key1 = table[i].key1;
-    if (key1) atomicAdd(&hist[owner_of(key1 - 1ull, nparts)], 1ull);
-  }
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntot;
+       i += (uint64_t)gridDim.x * blockDim.x)
+    if (entry_mask(T, nw, i)) atomicAdd(&hist[owner_of(entry_key(T, nw, i), nparts)], 1ull);
   __syncthreads();
   for (int i = threadIdx.x; i < nparts; i += blockDim.x)
     if (hist[i]) atomicAdd(&counts[i], hist[i]);
 }
 
-__global__ void k_part_scatter(const Slot* __restrict__ table, uint64_t cap, int nparts,
+__global__ void k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts,
                                unsigned long long* __restrict__ cursor, Slot* __restrict__ out) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt = (1ull << lane) - 1ull;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntot;
        i += (uint64_t)gridDim.x * blockDim.x) {
-    Slot s = table[i];
-    const int own = s.key1 ? owner_of(s.key1 - 1ull, nparts) : -1;
+    const uint32_t m = entry_mask(T, nw, i);
+    const uint64_t c = m ? entry_key(T, nw, i) : 0ull;
+    const int own = m ? owner_of(c, nparts) : -1;
     for (int o = 0; o < nparts; ++o) {
       const unsigned long long b = __ballot(own == o);
       if (!b) continue;
@@ -295,54 +387,73 @@ __global__ void k_part_scatter(const Slot* __restrict__ table, uint64_t cap, int
       unsigned long long base = 0;
       if (lane == leader) base = atomicAdd(&cursor[o], (unsigned long long)__builtin_popcountll(b));
       base = __shfl(base, leader, 64);
-      if (own == o) {
-        s.mask &= ~(RDBG_A | RDBG_B);
-        s.aux = 0;
-        out[base + __builtin_popcountll(b & lt)] = s;
-      }
+      if (own == o) out[base + __builtin_popcountll(b & lt)] = Slot{c + 1ull, m, 0u};
     }
   }
 }
 
 __global__ void __launch_bounds__(IBLOCK)
-k_merge(const Slot* __restrict__ pairs, uint64_t n, Slot* __restrict__ table, uint64_t capmask,
-        unsigned* __restrict__ flags) {
+k_merge(const Slot* __restrict__ pairs, uint64_t n, TableView T, unsigned* __restrict__ flags) {
   unsigned created = 0;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const Slot s = pairs[i];
     if (!s.key1) continue;
-    created += (unsigned)table_or(table, capmask, s.key1 - 1ull, s.mask & ~(RDBG_A | RDBG_B), flags);
+    created += (unsigned)tab_or(T, s.key1 - 1ull, s.mask & (uint32_t)MW_MASK, flags);
   }
   block_count(created, flags);
 }
 
 // ------------------------------------------------------------------ host
-static void alloc_table(Ctx& c, uint64_t cap) {
-  c.cap = cap;
-  c.table.reserve(cap * sizeof(Slot));
-  c.flags.reserve(4 * 16 * (N_CNT + 2));
+constexpr int N_FLAGS = 16 * (N_CNT + 2) + 16;       // + diagnostic counters
+
+static void alloc_table(Ctx& c, uint64_t keys) {
+  uint64_t buckets = 0, ovf = 0;
+  TableView t = make_geometry(c.k, keys, buckets, ovf);
+  c.table.reserve(16 * buckets);
+  c.ovf.reserve(sizeof(Slot) * ovf);
+  t.prim = c.table.as<unsigned long long>();
+  t.ovf = c.ovf.as<Slot>();
+  c.tv = t;
+  c.cap = buckets;
+  c.ovf_cap = ovf;
+  c.flags.reserve(4 * N_FLAGS);
 }
 
 static void clear_table(Ctx& c) {
-  PG_HIP(hipMemsetAsync(c.table.p, 0, c.cap * sizeof(Slot), c.stream));
-  PG_HIP(hipMemsetAsync(c.flags.p, 0, 4 * 16 * (N_CNT + 2), c.stream));
+  PG_HIP(hipMemsetAsync(c.table.p, 0, 16 * c.cap, c.stream));
+  PG_HIP(hipMemsetAsync(c.ovf.p, 0, sizeof(Slot) * c.ovf_cap, c.stream));
+  PG_HIP(hipMemsetAsync(c.flags.p, 0, 4 * N_FLAGS, c.stream));
 }
+
+static uint64_t n_entries(const Ctx& c) { return 2 * c.cap + c.ovf_cap; }
 
 // read back [sentinel, overflow, sum of spread counters]
 static void read_flags(Ctx& c, unsigned& sentinel, unsigned& overflow, uint64_t& created) {
-  std::vector<unsigned> f(16 * (N_CNT + 2));
+  std::vector<unsigned> f(N_FLAGS);
   PG_HIP(hipMemcpyAsync(f.data(), c.flags.p, 4 * f.size(), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   sentinel = f[0];
   overflow = f[1];
   created = 0;
   for (int i = 0; i < N_CNT; ++i) created += f[16 * (1 + i)];
+#ifdef PG_DIAG
+  fprintf(stderr, "PG_DIAG calls=%u casA=%u okA=%u orA=%u casB=%u okB=%u orB=%u ovf=%u created=%llu\n",
+          f[16 * (2 + N_CNT)], f[16 * (2 + N_CNT) + 1], f[16 * (2 + N_CNT) + 2], f[16 * (2 + N_CNT) + 3],
+          f[16 * (2 + N_CNT) + 4], f[16 * (2 + N_CNT) + 5], f[16 * (2 + N_CNT) + 6], f[16 * (2 + N_CNT) + 7],
+          (unsigned long long)created);
+#endif
 }
 
 // Tiles of records with n >= k+2, stripe-major: stripe 0 of every record, then
-// stripe 1, ...  (records with more stripes first within a stripe).  Packed as
-// record << 32 | stripe.  Cached while the record table and flags repeat.
+// stripe 1, ...  (records with more stripes first within a stripe).  One lead
+// record runs LEAD stripes ahead of the others: it creates the k-mers the
+// genomes share before its followers probe them, instead of every genome
+// reading the same empty bucket at once and racing to CAS it (a stale empty
+// costs a failed memory-side CAS).  Packed as record << 32 | stripe.  Cached
+// while the record table and flags repeat.
+constexpr uint64_t LEAD = 4;
+
 static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   const uint64_t R = c.n_records;
   if (c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k) return c.n_tiles;
@@ -360,9 +471,13 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   std::vector<unsigned long long> tiles;
   tiles.reserve(total);
   size_t live = nt.size();
-  for (uint64_t j = 0; j < maxs; ++j) {
-    while (live && nt[live - 1].first <= j) --live;
-    for (size_t i = 0; i < live; ++i) tiles.push_back(((unsigned long long)nt[i].second << 32) | j);
+  for (uint64_t j = 0; j < maxs + LEAD; ++j) {
+    if (!nt.empty() && j < nt[0].first)                        // the lead, LEAD stripes ahead
+      tiles.push_back(((unsigned long long)nt[0].second << 32) | j);
+    if (j < LEAD) continue;
+    const uint64_t jf = j - LEAD;                              // the followers' stripe
+    while (live && nt[live - 1].first <= jf) --live;
+    for (size_t i = 1; i < live; ++i) tiles.push_back(((unsigned long long)nt[i].second << 32) | jf);
   }
   c.tiles.reserve(8 * (total + 1));
   if (total) PG_HIP(hipMemcpyAsync(c.tiles.p, tiles.data(), 8 * total, hipMemcpyHostToDevice, c.stream));
@@ -392,34 +507,34 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     }
   c.windows_total = c.windows_fw * (rc0 ? 2 : 1);
   const uint64_t ntiles = make_tiles(c, flag);
-  // table size: learned capacity, else a conservative guess; rebuilt on overflow
-  uint64_t cap = c.cap_hint ? c.cap_hint : next_pow2(std::max<uint64_t>(1ull << 20, c.windows_fw));
+  // expected canonical keys: learned from the previous build, else an upper
+  // bound (every forward window distinct); an overflow rebuilds larger
+  uint64_t keys = c.cap_hint ? c.cap_hint : std::max<uint64_t>(1024, c.windows_fw);
   const uint64_t shift = pow5(c.k - 1);
   c.t0.init(); c.t1.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
-    alloc_table(c, cap);
+    alloc_table(c, keys);
     c.t0.start(c.stream);
     clear_table(c);
     c.t0.stop(c.stream);
-    Slot* tab = c.table.as<Slot>();
     unsigned* flags = c.flags.as<unsigned>();
     c.t1.start(c.stream);
     if (ntiles) {
       if (rc0)
         hipLaunchKernelGGL(k_insert<true>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
                            c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                           c.k, shift, tab, cap - 1, flags);
+                           c.k, shift, c.tv, flags);
       else
         hipLaunchKernelGGL(k_insert<false>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
                            c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                           c.k, shift, tab, cap - 1, flags);
+                           c.k, shift, c.tv, flags);
       PG_HIP(hipGetLastError());
     }
     c.t1.stop(c.stream);
     if (R) {
       hipLaunchKernelGGL(k_short, dim3(grid_for(R, IBLOCK, 1024)), dim3(IBLOCK), 0, c.stream,
                          c.cls.as<uint8_t>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                         c.rec_flag.as<uint8_t>(), R, c.k, shift, rc0, tab, cap - 1, flags);
+                         c.rec_flag.as<uint8_t>(), R, c.k, shift, rc0, c.tv, flags);
       PG_HIP(hipGetLastError());
     }
     if (extra_empty) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, flags);
@@ -428,14 +543,22 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     read_flags(c, sentinel, overflow, created);
     c.ms_clear = c.t0.ms();
     c.ms_insert = c.t1.ms();
-    if (!overflow && created * 10 <= cap * 7) {
+    if (!overflow) {
       c.n_canon = created;
       c.sentinel = sentinel ? 1 : 0;
-      c.cap_hint = next_pow2(std::max<uint64_t>(1ull << 16, created * 2));
+      c.cap_hint = std::max<uint64_t>(1024, created + created / 4);
       c.built = true;
+      if (getenv("PG_DEBUG_REINSERT") && ntiles && rc0) {   // diagnostic: probe cost without atomics
+        c.t1.start(c.stream);
+        hipLaunchKernelGGL(k_insert<true>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
+                           c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
+                           c.k, shift, c.tv, flags);
+        c.t1.stop(c.stream);
+        fprintf(stderr, "PG_DEBUG_REINSERT first=%.3f ms re-insert=%.3f ms\n", c.ms_insert, c.t1.ms());
+      }
       return;
     }
-    cap = next_pow2(std::max<uint64_t>(cap * 2, created * 3));
+    keys = std::max<uint64_t>(keys * 4, created * 2);
   }
   throw Error(-12, "build_dbg: hash table overflow after resizing");
 }
@@ -447,8 +570,8 @@ void build_rdbg(Ctx& c) {
   cnt.reserve(128);
   PG_HIP(hipMemsetAsync(cnt.p, 0, 128, c.stream));
   c.t0.start(c.stream);
-  hipLaunchKernelGGL(k_reduce, dim3(grid_for(c.cap / RTILE, 1, 8192)), dim3(256), 0, c.stream,
-                     c.table.as<Slot>(), c.cap, c.k, c.rdbg_keys.as<unsigned long long>(),
+  hipLaunchKernelGGL(k_reduce, dim3(grid_for(n_entries(c) / RTILE, 1, 8192)), dim3(256), 0, c.stream, c.tv,
+                     2 * c.cap, n_entries(c), c.k, c.rdbg_keys.as<unsigned long long>(),
                      cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
   c.t0.stop(c.stream);
@@ -477,9 +600,9 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {
   masks.reserve(2 * nmax);
   cnt.reserve(8);
   PG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
-  hipLaunchKernelGGL(k_export_dbg, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, c.stream,
-                     c.table.as<Slot>(), c.cap, c.k, keys.as<unsigned long long>(),
-                     masks.as<unsigned short>(), cnt.as<unsigned long long>());
+  hipLaunchKernelGGL(k_export_dbg, dim3(grid_for(n_entries(c), 256, 8192)), dim3(256), 0, c.stream, c.tv,
+                     2 * c.cap, n_entries(c), c.k, keys.as<unsigned long long>(), masks.as<unsigned short>(),
+                     cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
   unsigned long long n = 0;
   PG_HIP(hipMemcpyAsync(&n, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
@@ -508,8 +631,8 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
   cnt.reserve(16 * 64);
   PG_HIP(hipMemsetAsync(cnt.p, 0, 16 * 64, c.stream));
   auto* counts = cnt.as<unsigned long long>();
-  hipLaunchKernelGGL(k_part_count, dim3(grid_for(c.cap, 256, 4096)), dim3(256), 0, c.stream,
-                     c.table.as<Slot>(), c.cap, nparts, counts);
+  hipLaunchKernelGGL(k_part_count, dim3(grid_for(n_entries(c), 256, 4096)), dim3(256), 0, c.stream, c.tv,
+                     2 * c.cap, n_entries(c), nparts, counts);
   PG_HIP(hipGetLastError());
   std::vector<unsigned long long> h(nparts), off(nparts);
   PG_HIP(hipMemcpyAsync(h.data(), counts, 8 * nparts, hipMemcpyDeviceToHost, c.stream));
@@ -518,8 +641,8 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
   for (int i = 0; i < nparts; ++i) { off[i] = total; total += h[i]; h_counts[i] = h[i]; }
   if (d_out && out_cap >= total && total) {
     PG_HIP(hipMemcpyAsync(counts + 64, off.data(), 8 * nparts, hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_part_scatter, dim3(grid_for(c.cap, 256, 4096)), dim3(256), 0, c.stream,
-                       c.table.as<Slot>(), c.cap, nparts, counts + 64, reinterpret_cast<Slot*>(d_out));
+    hipLaunchKernelGGL(k_part_scatter, dim3(grid_for(n_entries(c), 256, 4096)), dim3(256), 0, c.stream, c.tv,
+                       2 * c.cap, n_entries(c), nparts, counts + 64, reinterpret_cast<Slot*>(d_out));
     PG_HIP(hipGetLastError());
     c.sync();
   }
@@ -528,31 +651,30 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
 }
 
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel) {
-  uint64_t cap = cap_hint ? next_pow2(cap_hint) : next_pow2(std::max<uint64_t>(1ull << 16, 2 * n));
+  uint64_t keys = cap_hint ? cap_hint : std::max<uint64_t>(1024, n);
   c.t1.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
-    alloc_table(c, cap);
+    alloc_table(c, keys);
     clear_table(c);
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
     c.t1.start(c.stream);
     if (n)
       hipLaunchKernelGGL(k_merge, dim3(grid_for(n, IBLOCK, 8192)), dim3(IBLOCK), 0, c.stream,
-                         reinterpret_cast<const Slot*>(d_pairs), n, c.table.as<Slot>(), cap - 1,
-                         c.flags.as<unsigned>());
+                         reinterpret_cast<const Slot*>(d_pairs), n, c.tv, c.flags.as<unsigned>());
     PG_HIP(hipGetLastError());
     c.t1.stop(c.stream);
     unsigned s = 0, overflow = 0;
     uint64_t created = 0;
     read_flags(c, s, overflow, created);
     c.ms_insert = c.t1.ms();
-    if (!overflow && created * 10 <= cap * 7) {
+    if (!overflow) {
       c.n_canon = created;
       c.sentinel = s ? 1 : 0;
       c.built = true;
       c.reduced = false;
       return;
     }
-    cap = next_pow2(std::max<uint64_t>(cap * 2, created * 3));
+    keys *= 4;
   }
   throw Error(-12, "merge_dbg: hash table overflow after resizing");
 }

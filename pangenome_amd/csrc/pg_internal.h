@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -94,9 +95,12 @@ struct Ctx {
   bool parsed = false;
 
   // ---- dBG table (K3) and rdBG (K5)
-  DevBuf table;
-  uint64_t cap = 0;               // slots (power of two)
-  uint64_t cap_hint = 0;          // learned from the previous build
+  DevBuf table;                   // primary buckets (2 x 64-bit words each)
+  DevBuf ovf;                     // overflow slots (16 B)
+  TableView tv{};                 // current geometry (pg_common.h)
+  uint64_t cap = 0;               // primary buckets (power of two)
+  uint64_t ovf_cap = 0;           // overflow slots (power of two)
+  uint64_t cap_hint = 0;          // canonical keys seen by the previous build
   DevBuf flags;                   // [0] sentinel seen, [1] overflow, [2..] counters
   DevBuf rdbg_keys;
   uint64_t n_dbg = 0, n_rdbg = 0, n_canon = 0, sentinel = 0;
@@ -149,6 +153,40 @@ inline uint64_t next_pow2(uint64_t x) {
   uint64_t p = 1;
   while (p < x) p <<= 1;
   return p;
+}
+inline int log2u(uint64_t p) {
+  int b = 0;
+  while ((1ull << b) < p) ++b;
+  return b;
+}
+
+// Table geometry for k-mers of length k holding about `keys` canonical keys:
+// load <= 0.5 keys per 2-word bucket, quotient <= 38 bits (so that quotient +
+// 26 mask bits fit 64), overflow table ~1/16 of the keys.
+inline TableView make_geometry(int k, uint64_t keys, uint64_t& buckets, uint64_t& ovf_slots) {
+  uint64_t maxkey = 1;
+  for (int i = 0; i < k; ++i) maxkey *= 5;
+  const int kb = std::max(1, log2u(maxkey));                 // keys < 5^k <= 2^kb
+  const int bb = std::max({kb - 38, log2u(std::max<uint64_t>(keys * 2, 1)), 11});   // >= 2048 buckets
+  buckets = 1ull << bb;
+  ovf_slots = next_pow2(std::max<uint64_t>(4096, keys / 16));
+  TableView t{};
+  t.bmask = buckets - 1;
+  t.qbits = kb > bb ? (uint32_t)(kb - bb) : 0u;
+  t.kmask = kb >= 64 ? ~0ull : ((1ull << kb) - 1ull);
+  t.sh1 = std::max(1, kb / 2);
+  t.sh2 = std::max(1, kb / 3);
+  auto inv = [](uint64_t m) {                                 // inverse of odd m mod 2^64
+    uint64_t x = m;
+    for (int i = 0; i < 6; ++i) x *= 2 - m * x;
+    return x;
+  };
+  t.m1 = (0x9E3779B97F4A7C15ull & t.kmask) | 1ull;
+  t.m2 = (0xC2B2AE3D27D4EB4Full & t.kmask) | 1ull;
+  t.m1i = inv(t.m1) & t.kmask;
+  t.m2i = inv(t.m2) & t.kmask;
+  t.omask = ovf_slots - 1;
+  return t;
 }
 inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536u) {
   uint64_t g = (n + block - 1) / block;

@@ -96,20 +96,13 @@ __device__ __forceinline__ void for_windows(const uint8_t* __restrict__ cls, lon
 }
 
 // rdbg_dict.has_key (:1465): rdBG member, or key 0 (has_key never checks counts, :599-603)
-__device__ __forceinline__ bool edge_member(const Slot* __restrict__ table, uint64_t capmask,
-                                            uint64_t x, uint64_t xrc) {
+__device__ __forceinline__ bool edge_member(const TableView& T, uint64_t x, uint64_t xrc) {
   if (x == SENTINEL) return false;             // skipped before the lookup (:1461-1462)
   if (x == 0) return true;
   const uint64_t c = x < xrc ? x : xrc;
-  const unsigned long long key1 = c + 1ull;
-  uint64_t slot = fmix64(c) & capmask;
-  for (uint64_t probe = 0; probe <= capmask; ++probe) {
-    const Slot s = table[slot];
-    if (s.key1 == key1) return (s.mask & (x == c ? RDBG_A : RDBG_B)) != 0;
-    if (s.key1 == 0) return false;
-    slot = (slot + 1) & capmask;
-  }
-  return false;
+  const uint32_t m = tab_get(T, c);
+  if (x == c) return (m & PRES_A) && rdbg_member(m & MASK12);
+  return (m & PRES_B) && rdbg_member((m >> B_SHIFT) & MASK12);
 }
 
 __device__ __forceinline__ uint64_t lab_hash(long long a, long long b) {
@@ -136,7 +129,7 @@ struct WalkArgs {
   const int* run_rec;                  // walked record -> record index
   uint64_t nrec;                       // walked records
   int k; uint64_t shift; int rc;
-  const Slot* table; uint64_t capmask; // edges
+  TableView T;                         // edges: the dBG table
   const LabSlot* lab; uint64_t lab_capmask;   // rows
 };
 
@@ -167,8 +160,8 @@ __global__ void __launch_bounds__(WBLOCK) k_walk_count(WalkArgs a, uint64_t nrun
     for_windows(a.cls, rs, n, a.k, a.shift, q0, q1, [&](long long q, const Win& w) {
       bool hf, hr = false;
       if (MODE == 0) {
-        hf = edge_member(a.table, a.capmask, w.xf, w.xf_rc);
-        if (a.rc) hr = edge_member(a.table, a.capmask, w.xr, w.xr_rc);
+        hf = edge_member(a.T, w.xf, w.xf_rc);
+        if (a.rc) hr = edge_member(a.T, w.xr, w.xr_rc);
       } else {
         long long id;
         hf = label_get(a.lab, a.lab_capmask, (long long)w.xf, (long long)((w.fp << OFFBIT) | w.fs), id);
@@ -451,8 +444,7 @@ static WalkArgs make_args(Ctx& c, WalkPlan& P, int rc) {
   a.k = c.k;
   a.shift = pow5(c.k - 1);
   a.rc = rc;
-  a.table = c.table.as<Slot>();
-  a.capmask = c.cap ? c.cap - 1 : 0;
+  a.T = c.tv;
   a.lab = c.lab_tab.as<LabSlot>();
   a.lab_capmask = c.lab_cap ? c.lab_cap - 1 : 0;
   return a;
