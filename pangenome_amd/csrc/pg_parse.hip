@@ -133,10 +133,16 @@ __global__ void __launch_bounds__(PBLOCK) k_copy(const uint8_t* __restrict__ buf
                                                  const unsigned long long* __restrict__ line_off,
                                                  const uint8_t* __restrict__ hdr,
                                                  uint8_t* __restrict__ out) {
+  // Compaction keeps byte order, so one 4 KiB input step's content bytes form
+  // one contiguous output range: stage their class codes in LDS at their
+  // offset in that range, then write the range with aligned 16-byte stores.
   __shared__ uint32_t lds[PBLOCK / 64];
   __shared__ uint8_t cls[256];
+  __shared__ unsigned long long s_lo[PBLOCK / 64], s_hi[PBLOCK / 64];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[PSTEP];
   cls[threadIdx.x] = c_byte_class[threadIdx.x];
   __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
   uint64_t run = blk_off[blockIdx.x];
   for (int s = 0; s < PSTEPS; ++s) {
@@ -146,21 +152,71 @@ __global__ void __launch_bounds__(PBLOCK) k_copy(const uint8_t* __restrict__ buf
     uint32_t c = p < n ? count_nl16(v) : 0u;
     uint32_t tot;
     uint32_t pre = block_excl_scan<PBLOCK>(c, lds, tot);
-    if (p < n) {
+    // output offset of each content byte (~0 for none)
+    unsigned long long off[16];
+    uint8_t code[16];
+    unsigned long long mylo = ~0ull, myhi = 0;
+    {
       uint64_t li = run + pre;
       uint64_t cur = ~0ull;
       long long ls = 0; unsigned long long lo = 0; bool lh = true;
-      for (int j = 0; j < 16 && p + j < n; ++j) {
-        uint32_t b = byte_of(v, j);
-        uint64_t pos = p + j;
-        bool term = (b == 10u) || (has_tail && pos == n - 1);
-        if (li < L && !term) {
-          if (li != cur) { cur = li; ls = line_start[li]; lo = line_off[li]; lh = hdr[li] != 0; }
-          if (!lh) out[lo + (pos - (uint64_t)ls)] = cls[b];
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        off[j] = ~0ull;
+        code[j] = 0;
+        const uint32_t b = byte_of(v, j);
+        const uint64_t pos = p + j;
+        if (pos < n) {
+          const bool term = (b == 10u) || (has_tail && pos == n - 1);
+          if (li < L && !term) {
+            if (li != cur) { cur = li; ls = line_start[li]; lo = line_off[li]; lh = hdr[li] != 0; }
+            if (!lh) {
+              off[j] = lo + (pos - (uint64_t)ls);
+              code[j] = cls[b];
+              mylo = off[j] < mylo ? off[j] : mylo;
+              myhi = off[j] + 1 > myhi ? off[j] + 1 : myhi;
+            }
+          }
+          if (b == 10u) ++li;
         }
-        if (b == 10u) ++li;
       }
     }
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long a = __shfl_xor(mylo, o, 64), b2 = __shfl_xor(myhi, o, 64);
+      mylo = a < mylo ? a : mylo;
+      myhi = b2 > myhi ? b2 : myhi;
+    }
+    if (lane == 0) { s_lo[wid] = mylo; s_hi[wid] = myhi; }
+    __syncthreads();
+    unsigned long long olo = ~0ull, ohi = 0;
+    for (int w = 0; w < PBLOCK / 64; ++w) {
+      olo = s_lo[w] < olo ? s_lo[w] : olo;
+      ohi = s_hi[w] > ohi ? s_hi[w] : ohi;
+    }
+    if (olo < ohi) {                                   // block-uniform
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (off[j] != ~0ull) stage[off[j] - olo] = code[j];
+      __syncthreads();
+      // 16-byte aligned global chunks covering [olo, ohi)
+      const unsigned long long g0 = olo & ~15ull;
+      for (unsigned long long g = g0 + 16ull * threadIdx.x; g < ohi; g += 16ull * PBLOCK) {
+        if (g >= olo && g + 16 <= ohi) {
+          uint32_t w[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const uint64_t i0 = g + 4 * q - olo;
+            w[q] = (uint32_t)stage[i0] | ((uint32_t)stage[i0 + 1] << 8) | ((uint32_t)stage[i0 + 2] << 16) |
+                   ((uint32_t)stage[i0 + 3] << 24);
+          }
+          *reinterpret_cast<uint4*>(out + g) = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+          for (int j = 0; j < 16; ++j)
+            if (g + j >= olo && g + j < ohi) out[g + j] = stage[g + j - olo];
+        }
+      }
+    }
+    __syncthreads();                                   // stage / s_lo reused next step
     run += tot;
   }
 }
