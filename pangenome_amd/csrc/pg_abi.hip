@@ -70,9 +70,9 @@ void pg_destroy(pg_ctx* x) {
   pg::Ctx& c = x->c;
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
-  pg::DevBuf* bufs[] = {&c.fasta_own, &c.blk_nl, &c.blk_nl_off, &c.nl_pos, &c.line_start, &c.line_off,
-                        &c.line_contrib, &c.line_hdr, &c.hdr_lines, &c.n_sel, &c.rec_start, &c.rec_len,
-                        &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.flags,
+  pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.n_sel, &c.rec_start,
+                        &c.rec_len, &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.ovf,
+                        &c.flags,
                         &c.rdbg_keys, &c.tiles, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
                         &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt};
   for (auto* b : bufs) b->release();

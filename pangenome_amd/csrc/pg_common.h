@@ -94,6 +94,7 @@ struct TableView {
   uint64_t kmask, m1, m2, m1i, m2i;
   Slot* ovf;
   uint64_t omask;              // overflow slots - 1
+  uint64_t rc_pad, rc_inv;     // rc(): 3(5^(27-k)-1)/4 and 5^-(27-k) mod 2^64 (see rc_key27)
 
   __host__ __device__ __forceinline__ uint64_t perm(uint64_t c) const {
     uint64_t h = (c * m1) & kmask;
@@ -113,6 +114,9 @@ struct TableView {
     h = unxs(h, sh1);
     return (h * m1i) & kmask;
   }
+  // reverse complement of a k-digit key (== rc_key(x, k)), ~10x fewer
+  // instructions than the digit loop
+  __host__ __device__ __forceinline__ uint64_t rc(uint64_t x) const;
   // key of the primary word w of bucket b
   __host__ __device__ __forceinline__ uint64_t key_of(uint64_t b, unsigned long long w) const {
     return unperm((b << qbits) | (uint64_t)(w >> MW_BITS));
@@ -162,6 +166,38 @@ __host__ __device__ __forceinline__ uint64_t rc_key(uint64_t x, int k) {
     r = r * 5 + rd;
   }
   return r;
+}
+
+// Reverse complement through 27 digits, three 9-digit chunks at a time in
+// 32-bit arithmetic (v * 0xCCCCCCCD >> 34 == v / 5 for every 32-bit v).
+// Reversing a k-digit key as 27 digits puts 27-k complemented zero digits
+// (3 = 'T') below it: rc_key(x, k) == (R27 - 3(5^(27-k)-1)/4) / 5^(27-k),
+// an exact division, done as a multiply by 5's inverse mod 2^64.
+__host__ __device__ __forceinline__ uint32_t rc_digits9(uint32_t v) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const uint32_t q = (uint32_t)(((uint64_t)v * 0xCCCCCCCDull) >> 34);
+    const uint32_t d = v - 5u * q;
+    r = r * 5u + (d < 4u ? 3u - d : 4u);
+    v = q;
+  }
+  return r;
+}
+__host__ __device__ __forceinline__ uint64_t rc_key27(uint64_t x) {
+  constexpr uint64_t P9 = 1953125ull, P18 = P9 * P9;
+  const uint64_t a = x / P18, r = x - a * P18;
+  const uint32_t b = (uint32_t)(r / P9), c = (uint32_t)(r - (uint64_t)b * P9);
+  return (uint64_t)rc_digits9(c) * P18 + (uint64_t)rc_digits9(b) * P9 + rc_digits9((uint32_t)a);
+}
+__host__ __device__ __forceinline__ uint64_t TableView::rc(uint64_t x) const {
+  return (rc_key27(x) - rc_pad) * rc_inv;
+}
+inline void rc_constants(int k, uint64_t& pad, uint64_t& inv) {
+  uint64_t p = 1, iv = 1;
+  for (int i = k; i < 27; ++i) { p *= 5; iv *= INV5; }
+  pad = 3 * ((p - 1) / 4);
+  inv = iv;
 }
 
 // rdBG rule (build_rdbg_jit_ :1300-1305): drop iff exactly one predecessor

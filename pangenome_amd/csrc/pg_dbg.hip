@@ -216,7 +216,7 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
 // one reference window of an explicit strand (used for records with n <= k+1)
 __device__ __forceinline__ void oriented_or(const TableView& T, int k, uint64_t x, uint32_t m12,
                                             unsigned* flags, unsigned& created) {
-  const uint64_t xr = rc_key(x, k);
+  const uint64_t xr = T.rc(x);
   const uint32_t m = m12 | PRES_A;
   if (x <= xr) created += (unsigned)tab_or(T, x, m, flags);
   else created += (unsigned)tab_or(T, xr, m << B_SHIFT, flags);
@@ -263,9 +263,7 @@ k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start
 __global__ void k_set_flag(unsigned* flags) { atomicOr(flags, 1u); }
 
 // ---- table scans.  Entry index space: [0, 2*buckets) primary words, then
-// [2*buckets, 2*buckets + ovf) overflow slots; both are multiples of RTILE.
-constexpr int RJ = 16;
-constexpr uint64_t RTILE = 256 * RJ;
+// [2*buckets, 2*buckets + ovf) overflow slots.
 
 __device__ __forceinline__ uint32_t entry_mask(const TableView& T, uint64_t nw, uint64_t i) {
   if (i < nw) {
@@ -280,48 +278,120 @@ __device__ __forceinline__ uint64_t entry_key(const TableView& T, uint64_t nw, u
   return T.ovf[i - nw].key1 - 1ull;
 }
 
-// K5: degree scan.  One block per RTILE-entry tile (entry = tile*RTILE + j*256
-// + tid, coalesced); members are counted, block-scanned and placed with one
-// global atomic per tile, then written by a second sweep over member entries.
-__global__ void __launch_bounds__(256)
-k_reduce(TableView T, uint64_t nw, uint64_t ntot, int k, unsigned long long* __restrict__ out,
-         unsigned long long* __restrict__ counters) {
-  __shared__ uint32_t lds[4];
-  __shared__ unsigned long long tile_base;
-  __shared__ unsigned long long red[4];
-  const uint64_t ntile = ntot / RTILE;
-  unsigned long long ndbg = 0;
-  for (uint64_t t = blockIdx.x; t < ntile; t += gridDim.x) {
-    const uint64_t base = t * RTILE + threadIdx.x;
-    uint32_t cnt = 0, bits = 0;
+// K5: degree scan.  The table is swept as 16-byte elements (a primary bucket
+// = two words, or one overflow slot), RU per thread per 16 KiB unit, with
+// 16-byte loads.  A unit's members (at most 4 per element) are block-scanned
+// into an LDS stage of RCAP keys; the stage goes out with ONE global atomic
+// per flush — a single device counter takes ~90 returning atomics per us, so
+// per-tile atomics would cost more than the sweep itself.
+constexpr int RT = 256, RU = 2;
+constexpr uint64_t RUNIT = (uint64_t)RT * RU;
+constexpr int RCAP = 4 * (int)RUNIT;               // a whole unit always fits an empty stage
+
+// Stage entries are the bucket-hash value h = perm(c) with bit 63 = "B
+// orientation"; keys are rebuilt here, one entry per lane (dense), rather than
+// by the few member lanes of every wave during the sweep.
+__device__ __forceinline__ void reduce_flush(const TableView& T, unsigned long long* stage, uint32_t n,
+                                             unsigned long long* s_base, unsigned long long* __restrict__ out,
+                                             unsigned long long* __restrict__ counter) {
+  if (threadIdx.x == 0) *s_base = atomicAdd(counter, (unsigned long long)n);
+  __syncthreads();
+  const unsigned long long b = *s_base;
+  for (uint32_t x = threadIdx.x; x < n; x += RT) {
+    const unsigned long long v = stage[x];
+    const uint64_t c = T.unperm(v & ~(1ull << 63));
+    out[b + x] = (v >> 63) ? T.rc(c) : c;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void reduce_load(const TableView& T, uint64_t nb, uint64_t nel, uint64_t u,
+                                            uint4 (&e)[RU]) {
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-      const uint32_t m = entry_mask(T, nw, base + (uint64_t)j * 256);
-      const bool pa = m & PRES_A, pb = m & PRES_B;
-      const bool ma = pa && rdbg_member(m & MASK12);
-      const bool mb = pb && rdbg_member((m >> B_SHIFT) & MASK12);
-      ndbg += (unsigned long long)pa + (unsigned long long)pb;
-      cnt += (uint32_t)ma + (uint32_t)mb;
-      bits |= ((uint32_t)ma | ((uint32_t)mb << 1)) << (2 * j);
+  for (int j = 0; j < RU; ++j) {
+    const uint64_t i = u * RUNIT + (uint64_t)j * RT + threadIdx.x;
+    e[j] = i >= nel ? make_uint4(0, 0, 0, 0)
+                    : i < nb ? *reinterpret_cast<const uint4*>(T.prim + 2 * i)
+                             : *reinterpret_cast<const uint4*>(T.ovf + (i - nb));
+  }
+}
+
+__global__ void __launch_bounds__(RT)
+k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __restrict__ out,
+         unsigned long long* __restrict__ counters) {
+  __shared__ unsigned long long stage[RCAP];
+  __shared__ uint32_t lds[RT / 64];
+  __shared__ unsigned long long s_base;
+  __shared__ unsigned long long red[RT / 64];
+  uint32_t staged = 0;                             // block-uniform
+  unsigned long long ndbg = 0;
+  const uint64_t nunit = (nel + RUNIT - 1) / RUNIT;
+  uint4 e[RU];
+  if (blockIdx.x < nunit) reduce_load(T, nb, nel, blockIdx.x, e);
+  for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
+    uint4 nx[RU];                                  // next unit in flight while this one is reduced
+    if (u + gridDim.x < nunit) reduce_load(T, nb, nel, u + gridDim.x, nx);
+    uint32_t m[RU][2];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < RU; ++j) {
+      const uint64_t i = u * RUNIT + (uint64_t)j * RT + threadIdx.x;
+      const bool w0 = e[j].x | e[j].y, w1 = e[j].z | e[j].w;
+      if (i < nb) {
+        m[j][0] = w0 ? (e[j].x & MW_MASK) : 0u;
+        m[j][1] = w1 ? (e[j].z & MW_MASK) : 0u;
+      } else {                                     // Slot {key1, mask, aux}
+        m[j][0] = w0 ? e[j].z : 0u;
+        m[j][1] = 0u;
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const uint32_t mm = m[j][h];
+        const bool pa = mm & PRES_A, pb = mm & PRES_B;
+        ndbg += (unsigned long long)pa + (unsigned long long)pb;
+        cnt += (uint32_t)(pa && rdbg_member(mm & MASK12)) + (uint32_t)(pb && rdbg_member((mm >> B_SHIFT) & MASK12));
+      }
     }
     uint32_t tot;
-    const uint32_t pre = block_excl_scan<256>(cnt, lds, tot);
-    if (threadIdx.x == 0) tile_base = tot ? atomicAdd(counters, (unsigned long long)tot) : 0ull;
-    __syncthreads();
-    unsigned long long o = tile_base + pre;
-    while (bits) {
-      const int b = __builtin_ctz(bits);
-      const uint64_t c = entry_key(T, nw, base + (uint64_t)(b >> 1) * 256);
-      out[o++] = (b & 1) ? rc_key(c, k) : c;
-      bits &= bits - 1u;
+    const uint32_t pre = block_excl_scan<RT>(cnt, lds, tot);
+    if (staged + tot > (uint32_t)RCAP) {           // block-uniform
+      reduce_flush(T, stage, staged, &s_base, out, counters);
+      staged = 0;
     }
-    __syncthreads();                               // tile_base is reused next tile
+    if (cnt) {
+      uint32_t o = staged + pre;
+#pragma unroll
+      for (int j = 0; j < RU; ++j) {
+        const uint64_t i = u * RUNIT + (uint64_t)j * RT + threadIdx.x;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const uint32_t mm = m[j][h];
+          const bool ma = (mm & PRES_A) && rdbg_member(mm & MASK12);
+          const bool mb = (mm & PRES_B) && rdbg_member((mm >> B_SHIFT) & MASK12);
+          if (ma || mb) {
+            const unsigned long long w = h ? ((unsigned long long)e[j].z | (unsigned long long)e[j].w << 32)
+                                           : ((unsigned long long)e[j].x | (unsigned long long)e[j].y << 32);
+            // perm(c): the bucket / quotient split of a primary word; overflow
+            // slots hold c + 1 (rare: hash it here)
+            const uint64_t hv = i < nb ? ((i << T.qbits) | (uint64_t)(w >> MW_BITS)) : T.perm(w - 1ull);
+            if (ma) stage[o++] = hv;
+            if (mb) stage[o++] = hv | (1ull << 63);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    staged += tot;
+#pragma unroll
+    for (int j = 0; j < RU; ++j) e[j] = nx[j];
   }
+  if (staged) reduce_flush(T, stage, staged, &s_base, out, counters);
   for (int o = 32; o > 0; o >>= 1) ndbg += __shfl_down(ndbg, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ndbg;
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long t = red[0] + red[1] + red[2] + red[3];
+    unsigned long long t = 0;
+    for (int w = 0; w < RT / 64; ++w) t += red[w];
     if (t) atomicAdd(counters + 8, t);
   }
 }
@@ -348,7 +418,7 @@ __global__ void k_export_dbg(TableView T, uint64_t nw, uint64_t ntot, int k,
     if (pa) { uint64_t o = base + __builtin_popcountll(ba & lt); keys[o] = c; masks[o] = m & MASK12; }
     if (pb) {
       uint64_t o = base + na + __builtin_popcountll(bb & lt);
-      keys[o] = rc_key(c, k); masks[o] = (m >> B_SHIFT) & MASK12;
+      keys[o] = T.rc(c); masks[o] = (m >> B_SHIFT) & MASK12;
     }
   }
 }
@@ -570,9 +640,9 @@ void build_rdbg(Ctx& c) {
   cnt.reserve(128);
   PG_HIP(hipMemsetAsync(cnt.p, 0, 128, c.stream));
   c.t0.start(c.stream);
-  hipLaunchKernelGGL(k_reduce, dim3(grid_for(n_entries(c) / RTILE, 1, 8192)), dim3(256), 0, c.stream, c.tv,
-                     2 * c.cap, n_entries(c), c.k, c.rdbg_keys.as<unsigned long long>(),
-                     cnt.as<unsigned long long>());
+  const uint64_t nel = c.cap + c.ovf_cap;               // 16-byte elements: buckets, then overflow slots
+  hipLaunchKernelGGL(k_reduce, dim3(grid_for(nel / RUNIT, 1, 4096)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
+                     c.k, c.rdbg_keys.as<unsigned long long>(), cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
   c.t0.stop(c.stream);
   unsigned long long res[9];

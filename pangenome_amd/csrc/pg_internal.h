@@ -79,11 +79,7 @@ struct Ctx {
   uint64_t n_bytes = 0;
 
   // ---- parse products (K1)
-  DevBuf blk_nl, blk_nl_off;      // per-chunk newline counts / offsets
-  DevBuf nl_pos;                  // newline (line terminator) positions, int64
-  DevBuf line_start, line_off, line_contrib;   // per line
-  DevBuf line_hdr;                // uint8 per line: header flag
-  DevBuf hdr_lines;               // int64 line index of each record header
+  DevBuf span_sum, span_start;    // per 16 KiB wave span: function / inclusive prefix (K1)
   DevBuf n_sel;                   // device counters
   DevBuf rec_start, rec_len;      // int64 per record: compacted offset / length
   DevBuf rec_hdr, rec_ptr;        // int64 per record: header byte span packed, `ptr` emulation
@@ -186,6 +182,7 @@ inline TableView make_geometry(int k, uint64_t keys, uint64_t& buckets, uint64_t
   t.m1i = inv(t.m1) & t.kmask;
   t.m2i = inv(t.m2) & t.kmask;
   t.omask = ovf_slots - 1;
+  rc_constants(k, t.rc_pad, t.rc_inv);
   return t;
 }
 inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536u) {

@@ -1,20 +1,28 @@
 // pg_parse.hip — K1: FASTA bytes in HBM -> record table + one class code per base.
 //
-// Restates readline_jit_ (kmer_numba.py:122-132) and seqio_jit_ (:135-172)
-// as data-parallel passes over the byte stream:
-//   k_nl_count  newlines per 64 KiB chunk (16-byte vector loads, SWAR compare)
-//   scan        chunk offsets (rocPRIM)
-//   k_nl_write  newline positions, in order (block-wide scan per 4 KiB step)
-//   k_lines     per line: start, header flag, content length (= len - 1: every
-//               line loses its last byte, :160/:167)
-//   scan        line -> offset in the compacted base stream
-//   select      header lines -> records
-//   k_records   per record: offset, length, header span, resume pointer
-//   k_copy      every content byte -> its class code at its compacted offset
-// A final line without '\n' counts when `end > start > 0` (:131-132); its last
-// byte then plays the terminator's role, so it is appended as a virtual
-// newline at n-1.  Lines before the first header land in front of record 0
-// in the compacted stream and belong to no record (:156-161).
+// Restates readline_jit_ (kmer_numba.py:122-132) and seqio_jit_ (:135-172).
+// The byte stream is read twice, streaming, 16 bytes per lane:
+//
+//   k_span_sum   one wave per 16 KiB span.  Newline / header counts, the last
+//                two newline positions, and the span's content-byte count as a
+//                function of its in-state (is the line open at the span start
+//                a header line?) with the out-state it leaves behind.
+//   scan         rocPRIM inclusive scan composing those 2-state functions:
+//                every span's output offset, in-state and first record index.
+//   k_emit       one wave per span again: each content byte -> its class code at
+//                its compacted offset (staged per step in the wave's own LDS
+//                slice, written with aligned 16-byte stores); each header's
+//                byte span and record start.  No block-wide barrier.
+//   k_records    record lengths and seqio's `ptr` value.
+//
+// Line semantics (kmer_numba.py:126-132): a line starts at 0 and after every
+// '\n'; it ends at its '\n', or, for a final unterminated line, at byte n-1
+// when `end > start > 0` — its last byte then plays the terminator's role
+// (line[:-1], :160/:167).  So byte n-1 is never a base, a line starting at n-1
+// without '\n' is no line, and a base is any byte < n-1 that is not '\n' and
+// whose line does not start with '>' (:155).  Lines before the first header
+// land in front of record 0 in the compacted stream and belong to no record
+// (:156-161, qid[0] != 62).  A file without any '\n' has no lines at all.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -22,18 +30,11 @@
 
 namespace pg {
 
-constexpr int PBLOCK = 256;                       // threads per block
-constexpr int PVEC = 16;                          // bytes per thread per step
-constexpr int PSTEP = PBLOCK * PVEC;              // 4 KiB per block step
-constexpr int PSTEPS = 16;
-constexpr uint64_t PCHUNK = (uint64_t)PSTEP * PSTEPS;   // 64 KiB per block
-
-__device__ __forceinline__ uint32_t count_nl_word(uint32_t w) {
-  uint32_t x = w ^ 0x0A0A0A0Au;
-  uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;
-  return __builtin_popcount(~t & 0x80808080u);
-}
-
+constexpr int PBLOCK = 256;                       // threads per block (4 waves)
+constexpr int WAVES = PBLOCK / 64;
+constexpr int WSTEP = 64 * 16;                    // 1 KiB per wave step (16 B per lane)
+constexpr int WSTEPS = 16;
+constexpr uint64_t WSPAN = (uint64_t)WSTEP * WSTEPS;   // 16 KiB per wave
 // load the 16 bytes at p (16-byte aligned); bytes at or past n read as 0
 __device__ __forceinline__ uint4 load16(const uint8_t* buf, uint64_t p, uint64_t n) {
   if (p + 16 <= n) return *reinterpret_cast<const uint4*>(buf + p);
@@ -43,181 +44,286 @@ __device__ __forceinline__ uint4 load16(const uint8_t* buf, uint64_t p, uint64_t
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-__device__ __forceinline__ uint32_t count_nl16(uint4 v) {
-  return count_nl_word(v.x) + count_nl_word(v.y) + count_nl_word(v.z) + count_nl_word(v.w);
+// bit j (0..3) set iff byte j of w equals the replicated byte in pat (exact SWAR)
+__device__ __forceinline__ uint32_t eq4(uint32_t w, uint32_t pat) {
+  const uint32_t x = w ^ pat;
+  const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+  return ((z >> 7) | (z >> 14) | (z >> 21) | (z >> 28)) & 0xFu;
+}
+__device__ __forceinline__ uint32_t eq16(const uint4& v, uint32_t pat) {
+  return eq4(v.x, pat) | eq4(v.y, pat) << 4 | eq4(v.z, pat) << 8 | eq4(v.w, pat) << 12;
 }
 
-__device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
-  uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
-  return (w >> (8 * (j & 3))) & 0xFFu;
+// bits of the lane's 16 positions below `lim`
+__device__ __forceinline__ uint32_t below_mask(uint64_t p, uint64_t lim) {
+  return p + 16 <= lim ? 0xFFFFu : (p < lim ? (1u << (uint32_t)(lim - p)) - 1u : 0u);
 }
 
-__global__ void __launch_bounds__(PBLOCK) k_nl_count(const uint8_t* __restrict__ buf, uint64_t n,
-                                                     unsigned long long* __restrict__ blk_nl) {
-  __shared__ uint32_t lds[PBLOCK / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
-  uint32_t cnt = 0;
-#pragma unroll 4
-  for (int s = 0; s < PSTEPS; ++s) {
-    uint64_t p = base + (uint64_t)s * PSTEP + (uint64_t)threadIdx.x * PVEC;
-    if (p < n) cnt += count_nl16(load16(buf, p, n));
+// Header-line bytes of a lane: from each header start (or bit 0 when the lane
+// continues a header line) through the first '\n' at or after it.  Header
+// starts always follow a '\n', so the borrow chains of E - hs never overlap.
+__device__ __forceinline__ uint32_t header_region(uint32_t nlm, uint32_t hs) {
+  const uint32_t E = nlm | 0x10000u;
+  return ((E - hs) ^ E) & 0xFFFFu;
+}
+
+// DPP inclusive prefix sum over the 64 lanes (all lanes active)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);   // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);   // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ int wave_max_i32(int x) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const int y = __shfl_xor(x, o, 64);
+    x = y > x ? y : x;
   }
-  uint32_t tot;
-  (void)block_excl_scan<PBLOCK>(cnt, lds, tot);
-  if (threadIdx.x == 0) blk_nl[blockIdx.x] = tot;
+  return x;
 }
 
-__global__ void __launch_bounds__(PBLOCK) k_nl_write(const uint8_t* __restrict__ buf, uint64_t n,
-                                                     const unsigned long long* __restrict__ blk_off,
-                                                     long long* __restrict__ nl_pos) {
-  __shared__ uint32_t lds[PBLOCK / 64];
-  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
-  uint64_t run = blk_off[blockIdx.x];
-  for (int s = 0; s < PSTEPS; ++s) {
-    uint64_t p = base + (uint64_t)s * PSTEP + (uint64_t)threadIdx.x * PVEC;
-    if (base + (uint64_t)s * PSTEP >= n) break;          // block-uniform
-    uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
-    uint32_t c = p < n ? count_nl16(v) : 0u;
-    uint32_t tot;
-    uint32_t pre = block_excl_scan<PBLOCK>(c, lds, tot);
-    if (c) {
-      uint64_t o = run + pre;
-      for (int j = 0; j < 16; ++j)
-        if (byte_of(v, j) == 10u) nl_pos[o++] = (long long)(p + j);
+// Per-lane view of one 16-byte step; `carry_nl` is the byte before the step
+// (or BOF) being '\n', updated for the next step.
+struct LaneStep {
+  uint32_t nlm, lsm, hs, vn1;
+  uint64_t B, H;          // lanes holding a line start / whose last line start is a header
+  uint64_t lt;            // lanes below this one
+};
+__device__ __forceinline__ LaneStep lane_step(const uint4& v, uint64_t p, uint64_t n, int lane,
+                                              uint32_t& carry_nl) {
+  LaneStep s;
+  s.nlm = eq16(v, 0x0A0A0A0Au);
+  const uint32_t gtm = eq16(v, 0x3E3E3E3Eu);
+  const uint64_t Bnl = __ballot((s.nlm >> 15) & 1u);
+  const uint32_t prev = lane ? (uint32_t)(Bnl >> (lane - 1)) & 1u : carry_nl;
+  carry_nl = (uint32_t)(Bnl >> 63) & 1u;
+  s.vn1 = below_mask(p, n - 1);
+  s.lsm = ((s.nlm << 1) | prev) & below_mask(p, n);
+  s.hs = s.lsm & gtm & s.vn1;
+  const bool has = s.lsm != 0;
+  const bool lh = has && ((s.hs >> (31 - __builtin_clz(s.lsm | 1u))) & 1u);
+  s.B = __ballot(has);
+  s.H = __ballot(lh);
+  s.lt = (1ull << lane) - 1ull;
+  return s;
+}
+// in-state of the lane given the step's in-state
+__device__ __forceinline__ uint32_t lane_in(const LaneStep& s, uint32_t step_in) {
+  const uint64_t below = s.B & s.lt;
+  return below ? (uint32_t)(s.H >> (63 - __builtin_clzll(below))) & 1u : step_in;
+}
+__device__ __forceinline__ uint32_t step_out(const LaneStep& s, uint32_t step_in) {
+  return s.B ? (uint32_t)(s.H >> (63 - __builtin_clzll(s.B))) & 1u : step_in;
+}
+__device__ __forceinline__ uint32_t lane_region(const LaneStep& s, uint32_t in) {
+  return header_region(s.nlm, s.hs | ((in && !(s.lsm & 1u)) ? 1u : 0u));
+}
+__device__ __forceinline__ uint32_t lane_content(const LaneStep& s, uint32_t region) {
+  return ~s.nlm & ~region & s.vn1 & 0xFFFFu;
+}
+
+// A span sequence as a function of its in-state (is the line open before it
+// a header line?): bases emitted and out-state for in-state 0 / 1, plus
+// newline / header counts and the last two newline positions.
+struct Fn {
+  unsigned long long c0, c1, nl, hdr;
+  long long last, last2;
+  uint32_t o;                                       // bit s: out-state for in-state s
+};
+__host__ __device__ __forceinline__ Fn fn_identity() { return Fn{0, 0, 0, 0, -1, -1, 2u}; }
+struct FnThen {                                     // a, then b (associative, not commutative)
+  __host__ __device__ __forceinline__ Fn operator()(const Fn& a, const Fn& b) const {
+    const uint32_t a0 = a.o & 1u, a1 = (a.o >> 1) & 1u;
+    Fn r;
+    r.c0 = a.c0 + (a0 ? b.c1 : b.c0);
+    r.c1 = a.c1 + (a1 ? b.c1 : b.c0);
+    r.o = ((b.o >> a0) & 1u) | ((b.o >> a1) & 1u) << 1;
+    r.nl = a.nl + b.nl;
+    r.hdr = a.hdr + b.hdr;
+    if (b.last2 >= 0) { r.last = b.last; r.last2 = b.last2; }
+    else if (b.last >= 0) { r.last = b.last; r.last2 = a.last; }
+    else { r.last = a.last; r.last2 = a.last2; }
+    return r;
+  }
+};
+
+// all of a wave's span loads are issued before the first step is processed
+__device__ __forceinline__ void load_span(const uint8_t* buf, uint64_t p0, uint64_t n, int lane,
+                                          uint4 (&v)[WSTEPS]) {
+#pragma unroll
+  for (int s = 0; s < WSTEPS; ++s) {
+    const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
+    v[s] = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+__global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__ buf, uint64_t n,
+                                                     uint64_t nspan, Fn* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t span = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (span >= nspan) return;                                  // wave-uniform
+  const uint64_t p0 = span * WSPAN;
+  uint4 v[WSTEPS];
+  load_span(buf, p0, n, lane, v);
+  uint32_t carry = p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u);
+  uint32_t c0 = 0, c1 = 0, fo = 2u;                           // identity: out(s) = s
+  uint32_t nl = 0, hdr = 0;
+  int top = -1, second = -1;
+#pragma unroll
+  for (int s = 0; s < WSTEPS; ++s) {
+    if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
+    const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
+    const LaneStep ls = lane_step(v[s], p, n, lane, carry);
+    // lane-local counts for span in-state 0 / 1: a lane's in-state is fixed by
+    // a line start in a lower lane, else it is the step's in-state fo(s)
+    const uint32_t m0 = lane_content(ls, lane_region(ls, 0)), m1 = lane_content(ls, lane_region(ls, 1));
+    const uint32_t f0 = fo & 1u, f1 = (fo >> 1) & 1u;         // span-so-far out-states
+    const bool det = (ls.B & ls.lt) != 0;
+    const uint32_t d = lane_in(ls, 0);
+    c0 += __builtin_popcount((det ? d : f0) ? m1 : m0);
+    c1 += __builtin_popcount((det ? d : f1) ? m1 : m0);
+    fo = step_out(ls, f0) | step_out(ls, f1) << 1;
+    nl += __builtin_popcount(ls.nlm);
+    hdr += __builtin_popcount(ls.hs);
+    if (ls.nlm) {
+      const int rel = (int)(p - p0);
+      const int t = 31 - __builtin_clz(ls.nlm);
+      const uint32_t rest = ls.nlm & ~(1u << t);
+      second = rest ? rel + 31 - __builtin_clz(rest) : top;
+      top = rel + t;
     }
-    run += tot;
   }
-}
-
-__global__ void k_lines(const uint8_t* __restrict__ buf, const long long* __restrict__ nl_pos,
-                        uint64_t L, long long* __restrict__ line_start,
-                        unsigned long long* __restrict__ contrib, uint8_t* __restrict__ hdr) {
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < L;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    long long st = i == 0 ? 0 : nl_pos[i - 1] + 1;
-    long long term = nl_pos[i];
-    bool h = buf[st] == 62;                                  // line[0] == 62 (:155)
-    line_start[i] = st;
-    hdr[i] = h;
-    contrib[i] = h ? 0ull : (unsigned long long)(term - st);   // line[:-1]
-  }
-}
-
-__global__ void k_records(const long long* __restrict__ hdr_lines, uint64_t R,
-                          const unsigned long long* __restrict__ line_off,
-                          const long long* __restrict__ line_start,
-                          const long long* __restrict__ nl_pos, uint64_t L, uint64_t total,
-                          long long* __restrict__ rec_start, long long* __restrict__ rec_len,
-                          long long* __restrict__ rec_hdr, long long* __restrict__ rec_ptr) {
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R;
-       r += (uint64_t)gridDim.x * blockDim.x) {
-    long long h = hdr_lines[r];
-    long long s = (long long)line_off[h];
-    long long e = r + 1 < R ? (long long)line_off[hdr_lines[r + 1]] : (long long)total;
-    rec_start[r] = s;
-    rec_len[r] = e - s;
-    rec_hdr[2 * r] = line_start[h];                          // qid = line[:-1] (:160)
-    rec_hdr[2 * r + 1] = nl_pos[h] - line_start[h];
-    // seqio's ptr[0] when this record is yielded: the next header line's
-    // start, or the last line's start at EOF (:153, :170-172)
-    rec_ptr[r] = r + 1 < R ? line_start[hdr_lines[r + 1]] : line_start[L - 1];
+  // per lane: c0, c1 <= 256 and nl, hdr <= 256, so the packed sums stay in 16 bits
+  const uint32_t cs = __builtin_amdgcn_readlane(wave_incl_sum(c0 | c1 << 16), 63);
+  const uint32_t cnts = __builtin_amdgcn_readlane(wave_incl_sum(nl | hdr << 16), 63);
+  const int last = wave_max_i32(top);
+  const int last2 = wave_max_i32(top != last ? top : second);
+  if (lane == 0) {
+    const long long b = (long long)p0;
+    out[span] = Fn{cs & 0xFFFFu, cs >> 16, cnts & 0xFFFFu, cnts >> 16, last >= 0 ? b + last : -1,
+                   last2 >= 0 ? b + last2 : -1, fo};
   }
 }
 
 __constant__ uint8_t c_byte_class[256];
 
-__global__ void __launch_bounds__(PBLOCK) k_copy(const uint8_t* __restrict__ buf, uint64_t n,
-                                                 const unsigned long long* __restrict__ blk_off,
-                                                 uint64_t L, int has_tail,
-                                                 const long long* __restrict__ line_start,
-                                                 const unsigned long long* __restrict__ line_off,
-                                                 const uint8_t* __restrict__ hdr,
-                                                 uint8_t* __restrict__ out) {
-  // Compaction keeps byte order, so one 4 KiB input step's content bytes form
-  // one contiguous output range: stage their class codes in LDS at their
-  // offset in that range, then write the range with aligned 16-byte stores.
-  __shared__ uint32_t lds[PBLOCK / 64];
-  __shared__ uint8_t cls[256];
-  __shared__ unsigned long long s_lo[PBLOCK / 64], s_hi[PBLOCK / 64];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[PSTEP];
-  cls[threadIdx.x] = c_byte_class[threadIdx.x];
+__global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf, uint64_t n, uint64_t nspan,
+                                                 const Fn* __restrict__ incl,
+                                                 uint8_t* __restrict__ out, long long* __restrict__ rec_start,
+                                                 long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
+  constexpr int STAGE = WSTEP + 32;
+  __shared__ uint8_t lut[256];
+  __shared__ __attribute__((aligned(16))) uint8_t stage_all[WAVES][STAGE];
+  lut[threadIdx.x] = c_byte_class[threadIdx.x];
   __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint64_t base = (uint64_t)blockIdx.x * PCHUNK;
-  uint64_t run = blk_off[blockIdx.x];
-  for (int s = 0; s < PSTEPS; ++s) {
-    uint64_t p = base + (uint64_t)s * PSTEP + (uint64_t)threadIdx.x * PVEC;
-    if (base + (uint64_t)s * PSTEP >= n) break;
-    uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
-    uint32_t c = p < n ? count_nl16(v) : 0u;
-    uint32_t tot;
-    uint32_t pre = block_excl_scan<PBLOCK>(c, lds, tot);
-    // output offset of each content byte (~0 for none)
-    unsigned long long off[16];
-    uint8_t code[16];
-    unsigned long long mylo = ~0ull, myhi = 0;
-    {
-      uint64_t li = run + pre;
-      uint64_t cur = ~0ull;
-      long long ls = 0; unsigned long long lo = 0; bool lh = true;
-#pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        off[j] = ~0ull;
-        code[j] = 0;
-        const uint32_t b = byte_of(v, j);
-        const uint64_t pos = p + j;
-        if (pos < n) {
-          const bool term = (b == 10u) || (has_tail && pos == n - 1);
-          if (li < L && !term) {
-            if (li != cur) { cur = li; ls = line_start[li]; lo = line_off[li]; lh = hdr[li] != 0; }
-            if (!lh) {
-              off[j] = lo + (pos - (uint64_t)ls);
-              code[j] = cls[b];
-              mylo = off[j] < mylo ? off[j] : mylo;
-              myhi = off[j] + 1 > myhi ? off[j] + 1 : myhi;
-            }
-          }
-          if (b == 10u) ++li;
-        }
+  const int lane = threadIdx.x & 63;
+  const uint64_t span = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (span >= nspan) return;                                  // wave-uniform, after the only barrier
+  uint8_t* stage = stage_all[threadIdx.x >> 6];
+  const uint64_t p0 = span * WSPAN;
+  // the prefix function evaluated at the file's in-state (0; byte 0 starts a line)
+  const Fn pre = span ? incl[span - 1] : fn_identity();
+  unsigned long long off = pre.c0, rec = pre.hdr;
+  // stage[0] holds output position cb (16-aligned); bytes below `own` belong
+  // to the previous span
+  unsigned long long cb = off & ~15ull;
+  const unsigned long long own = off;
+  uint32_t state = pre.o & 1u;
+  uint32_t carry = p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u);
+  // one step of prefetch: occupancy (LDS round trip per step) beats depth here
+  uint64_t p = p0 + (uint64_t)lane * 16;
+  uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+  for (int s = 0; s < WSTEPS; ++s) {
+    if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
+    const uint64_t pn = p + WSTEP;
+    const uint4 vn = (s + 1 < WSTEPS && pn < n) ? load16(buf, pn, n) : make_uint4(0, 0, 0, 0);
+    const LaneStep ls = lane_step(v, p, n, lane, carry);
+    const uint32_t region = lane_region(ls, lane_in(ls, state));
+    const uint32_t cm = lane_content(ls, region);
+    const uint32_t mine = (uint32_t)__builtin_popcount(cm) | (uint32_t)__builtin_popcount(ls.hs) << 16;
+    const uint32_t incl = wave_incl_sum(mine);
+    const uint32_t excl = incl - mine;
+    const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+    const unsigned long long lane_off = off + (excl & 0xFFFFu);
+    const unsigned long long lane_rec = rec + (excl >> 16);
+    // header lines: start (record begins at the next base) and terminator
+    const uint32_t term = region & (ls.nlm | (~ls.vn1 & below_mask(p, n) & (ls.vn1 + 1u)));
+    if (ls.hs | term) {
+      for (uint32_t m = ls.hs; m; m &= m - 1) {
+        const int j = __builtin_ctz(m);
+        const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((1u << j) - 1u));
+        hdr_start[r] = (long long)(p + j);
+        rec_start[r] = (long long)(lane_off + __builtin_popcount(cm & ((1u << j) - 1u)));
+      }
+      for (uint32_t m = term; m; m &= m - 1) {
+        const int j = __builtin_ctz(m);
+        const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((2u << j) - 1u)) - 1;
+        hdr_end[r] = (long long)(p + j);
       }
     }
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long a = __shfl_xor(mylo, o, 64), b2 = __shfl_xor(myhi, o, 64);
-      mylo = a < mylo ? a : mylo;
-      myhi = b2 > myhi ? b2 : myhi;
-    }
-    if (lane == 0) { s_lo[wid] = mylo; s_hi[wid] = myhi; }
-    __syncthreads();
-    unsigned long long olo = ~0ull, ohi = 0;
-    for (int w = 0; w < PBLOCK / 64; ++w) {
-      olo = s_lo[w] < olo ? s_lo[w] : olo;
-      ohi = s_hi[w] > ohi ? s_hi[w] : ohi;
-    }
-    if (olo < ohi) {                                   // block-uniform
+    // stage this step's bases after the pending bytes of chunk `cb`
+    {
+      uint32_t w = (uint32_t)(off - cb) + (excl & 0xFFFFu);
+      const uint32_t words[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int j = 0; j < 16; ++j)
-        if (off[j] != ~0ull) stage[off[j] - olo] = code[j];
-      __syncthreads();
-      // 16-byte aligned global chunks covering [olo, ohi)
-      const unsigned long long g0 = olo & ~15ull;
-      for (unsigned long long g = g0 + 16ull * threadIdx.x; g < ohi; g += 16ull * PBLOCK) {
-        if (g >= olo && g + 16 <= ohi) {
-          uint32_t w[4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const uint64_t i0 = g + 4 * q - olo;
-            w[q] = (uint32_t)stage[i0] | ((uint32_t)stage[i0 + 1] << 8) | ((uint32_t)stage[i0 + 2] << 16) |
-                   ((uint32_t)stage[i0 + 3] << 24);
-          }
-          *reinterpret_cast<uint4*>(out + g) = make_uint4(w[0], w[1], w[2], w[3]);
+        if ((cm >> j) & 1u) stage[w++] = lut[(words[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t ctot = tot & 0xFFFFu;
+    // write every completed 16-byte chunk; the partial one stays staged.  Only
+    // the span's first chunk can hold bytes of the previous span (< own).
+    const unsigned long long full = (off + ctot) & ~15ull;
+    if (full > cb) {
+      for (unsigned long long g = cb + 16ull * lane; g < full; g += 16ull * 64) {
+        const uint8_t* src = stage + (g - cb);
+        if (g >= own) {
+          *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(src);
         } else {
           for (int j = 0; j < 16; ++j)
-            if (g + j >= olo && g + j < ohi) out[g + j] = stage[g + j - olo];
+            if (g + j >= own) out[g + j] = src[j];
         }
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (lane == 0)
+        *reinterpret_cast<uint4*>(stage) = *reinterpret_cast<const uint4*>(stage + (full - cb));
+      cb = full;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    __syncthreads();                                   // stage / s_lo reused next step
-    run += tot;
+    off += ctot;
+    rec += tot >> 16;
+    state = step_out(ls, state);
+    v = vn;
+    p = pn;
+  }
+  // the span's last, partial chunk: byte stores of the bytes this span owns
+  if (lane < 16) {
+    const unsigned long long q = cb + lane;
+    if (q >= own && q < off) out[q] = stage[lane];
+  }
+}
+
+__global__ void k_records(uint64_t R, unsigned long long total, long long last_line_start,
+                          long long* __restrict__ rec_start, long long* __restrict__ rec_len,
+                          long long* __restrict__ hdr, long long* __restrict__ rec_ptr) {
+  // hdr: [0, R) header start, [R, 2R) header terminator -> header length
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const long long s = rec_start[r];
+    rec_len[r] = (r + 1 < R ? rec_start[r + 1] : (long long)total) - s;
+    hdr[R + r] -= hdr[r];                                     // qid = line[:-1] (:160)
+    // seqio's ptr[0] when this record is yielded: the next header line's
+    // start, or the last line's start at EOF (:153, :170-172)
+    rec_ptr[r] = r + 1 < R ? hdr[r + 1] : last_line_start;
   }
 }
 
@@ -234,15 +340,6 @@ static void upload_byte_class() {
   done = true;
 }
 
-template <class F>
-static void with_temp(Ctx& c, F&& f) {
-  size_t bytes = 0;
-  PG_HIP(f((void*)nullptr, bytes));
-  c.scratch.reserve(bytes + 16);
-  bytes = c.scratch.cap;
-  PG_HIP(f(c.scratch.p, bytes));
-}
-
 void parse_fasta(Ctx& c) {
   upload_byte_class();
   hipStream_t st = c.stream;
@@ -253,110 +350,56 @@ void parse_fasta(Ctx& c) {
   c.h_rec_hdr_len.clear(); c.h_rec_ptr.clear();
   if (n == 0) { c.parsed = true; return; }
 
-  const uint64_t nblk = (n + PCHUNK - 1) / PCHUNK;
-  c.blk_nl.reserve(8 * (nblk + 1));
-  c.blk_nl_off.reserve(8 * (nblk + 1));
-  c.n_sel.reserve(64);
-  hipLaunchKernelGGL(k_nl_count, dim3((unsigned)nblk), dim3(PBLOCK), 0, st, c.d_fasta, n,
-                     c.blk_nl.as<unsigned long long>());
+  const uint64_t nspan = (n + WSPAN - 1) / WSPAN;
+  const unsigned nblk = (unsigned)((nspan + WAVES - 1) / WAVES);
+  c.span_sum.reserve(sizeof(Fn) * nspan);
+  c.span_start.reserve(sizeof(Fn) * nspan);
+  auto* fns = c.span_sum.as<Fn>();
+  auto* incl = c.span_start.as<Fn>();
+  hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, nspan, fns);
   PG_HIP(hipGetLastError());
-  auto* bn = c.blk_nl.as<unsigned long long>();
-  auto* bo = c.blk_nl_off.as<unsigned long long>();
-  with_temp(c, [&](void* tmp, size_t& bytes) {
-    return rocprim::exclusive_scan(tmp, bytes, bn, bo, 0ull, (size_t)nblk,
-                                   rocprim::plus<unsigned long long>(), st);
-  });
-  unsigned long long last[2];
-  PG_HIP(hipMemcpyAsync(&last[0], bo + nblk - 1, 8, hipMemcpyDeviceToHost, st));
-  PG_HIP(hipMemcpyAsync(&last[1], bn + nblk - 1, 8, hipMemcpyDeviceToHost, st));
+  size_t bytes = 0;
+  PG_HIP(rocprim::inclusive_scan(nullptr, bytes, fns, incl, (size_t)nspan, FnThen{}, st));
+  c.scratch.reserve(bytes + 16);
+  bytes = c.scratch.cap;
+  PG_HIP(rocprim::inclusive_scan(c.scratch.p, bytes, fns, incl, (size_t)nspan, FnThen{}, st));
+  Fn tot;
+  PG_HIP(hipMemcpyAsync(&tot, incl + nspan - 1, sizeof tot, hipMemcpyDeviceToHost, st));
   c.sync();
-  const uint64_t n_nl = last[0] + last[1];
-  c.n_nl = n_nl;
-  c.nl_pos.reserve(8 * (n_nl + 2));
-  auto* nl = c.nl_pos.as<long long>();
-  if (n_nl) {
-    hipLaunchKernelGGL(k_nl_write, dim3((unsigned)nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, bo, nl);
-    PG_HIP(hipGetLastError());
-  }
-  // tail line (:131-132): `end > start > 0` with end = n-1, start = last '\n' + 1
-  int has_tail = 0;
-  if (n_nl) {
-    long long lastnl = 0;
-    PG_HIP(hipMemcpyAsync(&lastnl, nl + n_nl - 1, 8, hipMemcpyDeviceToHost, st));
-    c.sync();
-    long long start = lastnl + 1;
-    if ((long long)n - 1 > start) {
-      has_tail = 1;
-      long long v = (long long)n - 1;
-      PG_HIP(hipMemcpyAsync(nl + n_nl, &v, 8, hipMemcpyHostToDevice, st));
-    }
-  }
-  const uint64_t L = n_nl + has_tail;
-  c.n_lines = L;
-  if (L == 0) { c.sync(); c.parsed = true; return; }
-
-  c.line_start.reserve(8 * L);
-  c.line_off.reserve(8 * L);
-  c.line_contrib.reserve(8 * L);
-  c.line_hdr.reserve(L);
-  auto* ls = c.line_start.as<long long>();
-  auto* lo = c.line_off.as<unsigned long long>();
-  auto* lc = c.line_contrib.as<unsigned long long>();
-  auto* lh = c.line_hdr.as<uint8_t>();
-  hipLaunchKernelGGL(k_lines, dim3(grid_for(L, 256)), dim3(256), 0, st, c.d_fasta, nl, L, ls, lc, lh);
-  PG_HIP(hipGetLastError());
-  with_temp(c, [&](void* tmp, size_t& bytes) {
-    return rocprim::exclusive_scan(tmp, bytes, lc, lo, 0ull, (size_t)L,
-                                   rocprim::plus<unsigned long long>(), st);
-  });
-  c.hdr_lines.reserve(8 * L);
-  auto* hl = c.hdr_lines.as<long long>();
-  auto* nsel = c.n_sel.as<unsigned long long>();
-  rocprim::counting_iterator<long long> idx(0);
-  with_temp(c, [&](void* tmp, size_t& bytes) {
-    return rocprim::select(tmp, bytes, idx, lh, hl, nsel, (size_t)L, st);
-  });
-  unsigned long long meta[3];
-  PG_HIP(hipMemcpyAsync(&meta[0], nsel, 8, hipMemcpyDeviceToHost, st));
-  PG_HIP(hipMemcpyAsync(&meta[1], lo + L - 1, 8, hipMemcpyDeviceToHost, st));
-  PG_HIP(hipMemcpyAsync(&meta[2], lc + L - 1, 8, hipMemcpyDeviceToHost, st));
-  c.sync();
-  const uint64_t R = meta[0];
-  const uint64_t total = meta[1] + meta[2];
+  c.n_nl = tot.nl;
+  if (tot.nl == 0) { c.parsed = true; return; }             // no line at all (:126-132)
+  // the unterminated last line counts when end > start > 0 (:131)
+  const bool has_tail = (long long)n - 1 > tot.last + 1;
+  c.n_lines = tot.nl + (has_tail ? 1 : 0);
+  const long long last_line_start = has_tail ? tot.last + 1 : (tot.last2 >= 0 ? tot.last2 + 1 : 0);
+  const uint64_t R = tot.hdr;
   c.n_records = R;
-  c.cls.reserve(total + 64);
-  if (total) {
-    hipLaunchKernelGGL(k_copy, dim3((unsigned)nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, bo, L, has_tail,
-                       ls, lo, lh, c.cls.as<uint8_t>());
-    PG_HIP(hipGetLastError());
-  }
+  c.cls.reserve(tot.c0 + 64);
+  c.rec_start.reserve(8 * (R + 1));
+  c.rec_len.reserve(8 * (R + 1));
+  c.rec_hdr.reserve(16 * (R + 1));
+  c.rec_ptr.reserve(8 * (R + 1));
+  c.rec_flag.reserve(R + 1);
+  auto* hdr = c.rec_hdr.as<long long>();
+  hipLaunchKernelGGL(k_emit, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, nspan, incl, c.cls.as<uint8_t>(),
+                     c.rec_start.as<long long>(), hdr, hdr + R);
+  PG_HIP(hipGetLastError());
   if (R) {
-    c.rec_start.reserve(8 * R);
-    c.rec_len.reserve(8 * R);
-    c.rec_hdr.reserve(16 * R);
-    c.rec_ptr.reserve(8 * R);
-    c.rec_flag.reserve(R);
-    hipLaunchKernelGGL(k_records, dim3(grid_for(R, 256)), dim3(256), 0, st, hl, R, lo, ls, nl, L, total,
-                       c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                       c.rec_hdr.as<long long>(), c.rec_ptr.as<long long>());
+    hipLaunchKernelGGL(k_records, dim3(grid_for(R, 256)), dim3(256), 0, st, R, tot.c0, last_line_start,
+                       c.rec_start.as<long long>(), c.rec_len.as<long long>(), hdr, c.rec_ptr.as<long long>());
     PG_HIP(hipGetLastError());
     c.h_rec_start.resize(R); c.h_rec_len.resize(R); c.h_rec_ptr.resize(R);
-    std::vector<int64_t> hdr(2 * R);
+    c.h_rec_hdr_start.resize(R); c.h_rec_hdr_len.resize(R);
     PG_HIP(hipMemcpyAsync(c.h_rec_start.data(), c.rec_start.p, 8 * R, hipMemcpyDeviceToHost, st));
     PG_HIP(hipMemcpyAsync(c.h_rec_len.data(), c.rec_len.p, 8 * R, hipMemcpyDeviceToHost, st));
     PG_HIP(hipMemcpyAsync(c.h_rec_ptr.data(), c.rec_ptr.p, 8 * R, hipMemcpyDeviceToHost, st));
-    PG_HIP(hipMemcpyAsync(hdr.data(), c.rec_hdr.p, 16 * R, hipMemcpyDeviceToHost, st));
-    c.sync();
-    c.h_rec_hdr_start.resize(R); c.h_rec_hdr_len.resize(R);
-    uint64_t nb = 0;
-    for (uint64_t r = 0; r < R; ++r) {
-      c.h_rec_hdr_start[r] = hdr[2 * r];
-      c.h_rec_hdr_len[r] = hdr[2 * r + 1];
-      nb += (uint64_t)c.h_rec_len[r];
-    }
-    c.n_bases = nb;
+    PG_HIP(hipMemcpyAsync(c.h_rec_hdr_start.data(), hdr, 8 * R, hipMemcpyDeviceToHost, st));
+    PG_HIP(hipMemcpyAsync(c.h_rec_hdr_len.data(), hdr + R, 8 * R, hipMemcpyDeviceToHost, st));
   }
   c.sync();
+  uint64_t nb = 0;
+  for (uint64_t r = 0; r < R; ++r) nb += (uint64_t)c.h_rec_len[r];
+  c.n_bases = nb;
   c.parsed = true;
 }
 

@@ -1,0 +1,137 @@
+"""K1 (FASTA parse) parity on adversarial byte streams.
+
+The record table (sequence length, header span, seqio's `ptr`) is checked
+against a numpy restatement of readline_jit_ / seqio_jit_
+(kmer_numba.py:122-172); the bases themselves through the k=1 and k=5 dBG
+against the C oracle (every base's class and both neighbours are in a k=1
+mask).  Inputs cover unterminated last lines of every length, '>' at the end,
+CRLF, empty lines and records, bases before the first header, lines and
+headers longer than the kernel's 16 KiB wave span, and random byte soup.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def seqio_records(buf: bytes):
+    """readline_jit_ (:122-132) + seqio_jit_ (:135-172), isfasta, offset 0."""
+    a = np.frombuffer(buf, dtype=np.uint8)
+    n = a.shape[0]
+    nl = np.flatnonzero(a == 10)
+    starts = np.concatenate([[0], nl + 1])[: nl.shape[0]]
+    ends = nl + 1
+    if n and nl.shape[0]:
+        st = int(nl[-1]) + 1
+        if n - 1 > st > 0:                                   # end > start > 0
+            starts = np.append(starts, st)
+            ends = np.append(ends, n)
+    recs = []                                                # (seq_len, hdr_start, hdr_len, ptr)
+    cur = None
+    for st, ed in zip(starts.tolist(), ends.tolist()):
+        if a[st] == 62:
+            if cur is not None:
+                recs.append((cur[0], cur[1], cur[2], st))
+            cur = [0, st, ed - 1 - st]
+        elif cur is not None:
+            cur[0] += ed - st - 1
+    if cur is not None:
+        recs.append((cur[0], cur[1], cur[2], int(starts[-1])))
+    return recs
+
+
+CASES = {
+    "plain": b">a\nACGT\nACG\n>b\nTTTT\n",
+    "tail2": b">a\nACGT\nAC",
+    "tail1": b">a\nACGT\nA",
+    "tail_hdr": b">a\nACGT\n>b",
+    "tail_gt": b">a\nACGT\n>",
+    "tail_hdr_only": b">a\nAC\n>bb",
+    "no_newline": b">a ACGT",
+    "only_newlines": b"\n\n\n",
+    "single_nl": b"\n",
+    "crlf": b">a\r\nACGT\r\nGG\r\n>b\r\nTT\r\n",
+    "empty_lines": b"\n\n>a\n\nAC\n\n\n>b\n\n",
+    "empty_records": b">a\n>b\n>c\nACG\n>d\n",
+    "before_header": b"ACGTACGT\nGG\n>a\nCCCC\n",
+    "headers_only": b">a\n>b\n>c\n",
+    "gt_in_seq": b">a\nAC>GT\n>b\nG>\n",
+    "dollar_n": b">a\nAC$GTNNnnacgtRYK\n",
+}
+
+
+def _long_cases():
+    rng = np.random.default_rng(5)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    one_line = acgt[rng.integers(0, 4, 70_000)].tobytes()
+    long_hdr = b">" + b"h" * 40_000
+    return {
+        "one_line_70k": b">x\n" + one_line + b"\n>y\n" + one_line[:33_333] + b"\n",
+        "long_header": long_hdr + b"\nACGTTGCA\n" + long_hdr + b"\nGG\n",
+        "long_tail": b">x\n" + one_line,
+        "long_tail_hdr": b">x\nACGT\n" + long_hdr,
+    }
+
+
+def _soup(seed, n, alphabet):
+    rng = np.random.default_rng(seed)
+    a = np.frombuffer(alphabet, dtype=np.uint8)
+    return a[rng.integers(0, a.shape[0], n)].tobytes()
+
+
+SOUPS = [(s, n, alpha) for s, (n, alpha) in enumerate([
+    (1, b">\nA"), (2, b">\nA"), (3, b">\nAC"), (17, b">\nACGTN"), (1000, b">\nACGT\r"),
+    (16_383, b"ACGT\n>"), (16_385, b"ACGTACGTACGT\n>"), (50_000, b"ACGTACGTACGTACGTACGT\n>x"),
+    (120_000, b"A" * 60 + b"\n>"), (33_000, b"\n>"),
+])]
+
+
+def _check(buf, oracle_mod):
+    from pangenome_amd._lib import Context
+    ctx = Context(5)
+    ctx.set_fasta(buf)
+    R, B = ctx.parse()
+    exp = seqio_records(buf)
+    assert R == len(exp)
+    if R:
+        got = ctx.records()
+        assert got["seq_len"].tolist() == [e[0] for e in exp]
+        assert got["hdr_start"].tolist() == [e[1] for e in exp]
+        assert got["hdr_len"].tolist() == [e[2] for e in exp]
+        assert got["ptr"].tolist() == [e[3] for e in exp]
+    assert B == sum(e[0] for e in exp)
+    ctx.close()
+    for k in (1, 5):
+        ctx = Context(k)
+        ctx.set_fasta(buf)
+        ctx.parse()
+        ctx.build_dbg(None, 0, True)
+        keys, masks = ctx.dbg()
+        ctx.close()
+        rk, rm = oracle_mod.OracleRun(buf, k, 2).dbg()
+        assert np.array_equal(keys, rk)
+        assert np.array_equal(masks, rm)
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_parse_cases(oracle_mod, name):
+    _check(CASES[name], oracle_mod)
+
+
+@pytest.mark.parametrize("name", ["one_line_70k", "long_header", "long_tail", "long_tail_hdr"])
+def test_parse_long_lines(oracle_mod, name):
+    _check(_long_cases()[name], oracle_mod)
+
+
+@pytest.mark.parametrize("seed,n,alphabet", SOUPS)
+def test_parse_soup(oracle_mod, seed, n, alphabet):
+    _check(_soup(seed, n, alphabet), oracle_mod)
+
+
+def test_parse_span_boundaries(oracle_mod):
+    """Line and header boundaries on every side of the 16 KiB span edge."""
+    span = 16 * 1024
+    for shift in (-2, -1, 0, 1, 2):
+        body = b"A" * (span + shift - 4)
+        _check(b">a\n" + body + b"\n>b\nCC\n", oracle_mod)
+        _check(b">a\nC\n" + b"G" * (span + shift - 6) + b">c\nAC\n", oracle_mod)
