@@ -101,6 +101,74 @@ __device__ __forceinline__ int tab_or_at(const TableView& T, uint64_t c, uint64_
   return ovf_or(T, c, mw, flags);
 }
 
+// tab_or_at for a batch of N windows with their (possibly stale) bucket words,
+// in rounds: every CAS of a round is issued before any result is used, so a
+// lane waits for about two memory-side round trips per batch instead of one
+// per window.  mm[i] == 0 skips entry i.
+template <int N>
+__device__ __forceinline__ void tab_or_batch(const TableView& T, const uint64_t (&cc)[N], const uint64_t (&hh)[N],
+                                             const uint32_t (&mm)[N], const ulonglong2 (&v)[N], unsigned* flags,
+                                             unsigned& created, int dbg = 0) {
+  const uint64_t qmask = (1ull << T.qbits) - 1ull;
+  unsigned long long res[N];
+  uint32_t need = 0, on1 = 0;                    // CAS in flight; on word 1
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    res[i] = 0ull;
+    if (!mm[i]) continue;
+    const uint64_t b = hh[i] >> T.qbits, q = hh[i] & qmask;
+    unsigned long long* w = T.prim + 2 * b;
+    const unsigned long long x = v[i].x, y = v[i].y;
+    const unsigned long long mine = (q << MW_BITS) | mm[i];
+    if (x != 0ull && (x >> MW_BITS) == q) {
+      if ((x & mm[i]) != mm[i] && !(dbg & 16)) atomicOr(w, (unsigned long long)mm[i]);
+    } else if (x == 0ull) {
+      if (dbg & 8) { *w = mine; ++created; continue; }   // dev knob: create by plain store (racy)
+      res[i] = atomicCAS(w, 0ull, mine);
+      need |= 1u << i;
+    } else if (y != 0ull && (y >> MW_BITS) == q) {
+      if ((y & mm[i]) != mm[i]) atomicOr(w + 1, (unsigned long long)mm[i]);
+    } else if (y == 0ull) {
+      res[i] = atomicCAS(w + 1, 0ull, mine);
+      need |= 1u << i;
+      on1 |= 1u << i;
+    } else {
+      created += (unsigned)ovf_or(T, cc[i], mm[i], flags);
+    }
+  }
+  for (int round = 0; round < 2 && need; ++round) {
+    uint32_t next = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      if (!((need >> i) & 1u)) continue;
+      const uint64_t b = hh[i] >> T.qbits, q = hh[i] & qmask;
+      unsigned long long* w = T.prim + 2 * b;
+      const unsigned long long old = res[i];
+      const bool w1 = (on1 >> i) & 1u;
+      if (old == 0ull) { ++created; continue; }
+      if ((old >> MW_BITS) == q) {               // another lane created it first
+        if ((old & mm[i]) != mm[i]) atomicOr(w1 ? w + 1 : w, (unsigned long long)mm[i]);
+        continue;
+      }
+      if (!w1) {                                 // word 0 holds another key: word 1
+        const unsigned long long y = v[i].y;     // non-zero words are final
+        if (y != 0ull && (y >> MW_BITS) == q) {
+          if ((y & mm[i]) != mm[i]) atomicOr(w + 1, (unsigned long long)mm[i]);
+        } else if (y == 0ull) {
+          res[i] = atomicCAS(w + 1, 0ull, (q << MW_BITS) | mm[i]);
+          next |= 1u << i;
+          on1 |= 1u << i;
+        } else {
+          created += (unsigned)ovf_or(T, cc[i], mm[i], flags);
+        }
+      } else {
+        created += (unsigned)ovf_or(T, cc[i], mm[i], flags);
+      }
+    }
+    need = next;
+  }
+}
+
 __device__ __forceinline__ int tab_or(const TableView& T, uint64_t c, uint32_t mw, unsigned* flags) {
   const uint64_t h = T.perm(c);
   const uint64_t b = h >> T.qbits, q = h & ((1ull << T.qbits) - 1ull);
@@ -121,6 +189,38 @@ __device__ __forceinline__ void block_count(unsigned created, unsigned* flags) {
   }
 }
 
+// 4*ND bytes of LDS starting at byte index idx, realigned into dwords
+template <int ND>
+__device__ __forceinline__ void lds_bytes(const uint8_t* s, uint32_t idx, uint32_t (&out)[ND]) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (idx & ~3u));
+  const uint32_t sh = (idx & 3u) * 8u;
+  uint32_t raw[ND + 1];
+#pragma unroll
+  for (int i = 0; i <= ND; ++i) raw[i] = w[i];
+#pragma unroll
+  for (int i = 0; i < ND; ++i)
+    out[i] = sh ? (raw[i] >> sh) | (raw[i + 1] << (32u - sh)) : raw[i];
+}
+template <int ND>
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[ND], int j) {
+  return (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+}
+
+// k2n_jit (:975-985) for both strands of the window whose first base is LDS
+// byte o: K = sum alpha(s[j]) 5^j, Kr = sum alpha'(s[j]) 5^(k-1-j).  The low
+// 13 digits accumulate in 32 bits (5^13 < 2^32), the rest (<= 14) in 64.
+__device__ __forceinline__ void init_keys(const uint8_t* sc, uint32_t o, int k, uint64_t& K, uint64_t& Kr) {
+  uint32_t lo = 0, rlo = 0;
+  uint64_t hi = 0, rhi = 0;
+  const int kl = k < 13 ? k : 13, kh = k - kl;
+  for (int j = kl - 1; j >= 0; --j) lo = lo * 5u + digit_fw(sc[o + j]);
+  for (int j = k - 1; j >= kl; --j) hi = hi * 5u + digit_fw(sc[o + j]);
+  for (int j = 0; j < kh; ++j) rhi = rhi * 5u + digit_rc(sc[o + j]);
+  for (int j = kh; j < k; ++j) rlo = rlo * 5u + digit_rc(sc[o + j]);
+  K = (uint64_t)lo + hi * 1220703125ull;         // 5^13
+  Kr = (uint64_t)rlo + rhi * 1220703125ull;
+}
+
 // K3.  One block per tile (record, stripe j): windows [j*TILE, (j+1)*TILE) of
 // a record with n >= k+2.  The tile's class codes (plus the k+3 bytes of
 // context around it) are staged in LDS with 16-byte loads; thread t takes IW
@@ -132,7 +232,7 @@ template <bool RC>
 __global__ void __launch_bounds__(IBLOCK)
 k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__ tiles,
          const long long* __restrict__ rec_start, const long long* __restrict__ rec_len, int k, uint64_t shift,
-         TableView T, unsigned* __restrict__ flags) {
+         TableView T, unsigned* __restrict__ flags, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   const unsigned long long tile = tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
   const int r = (int)(tile >> 32);
@@ -152,18 +252,63 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
 
   const long long q0 = qt + (long long)threadIdx.x * IW;
   const long long q1 = q0 + IW <= last + 1 ? q0 + IW : last + 1;
-  const uint64_t qmask = (1ull << T.qbits) - 1ull;
   unsigned created = 0;
   uint64_t K = 0, Kr = 0;
-  if (q0 < q1) {
-    uint64_t pw = 1;
-    for (int j = 0; j < k; ++j) {                  // k2n_jit (:975-985), both strands
-      const uint32_t cj = S(q0 + j);
-      K += (uint64_t)digit_fw(cj) * pw;
-      Kr = Kr * 5 + digit_rc(cj);
-      pw *= 5;
+  if (q0 < q1) init_keys(s_cls, (uint32_t)(base + q0), k, K, Kr);
+  auto probe = [&](const uint64_t (&cc)[IB], const uint64_t (&hh)[IB], const uint32_t (&mm)[IB]) {
+    if (dbg & 1) {                                 // dev knob: windows only
+#pragma unroll
+      for (int i = 0; i < IB; ++i) created += (unsigned)(hh[i] ^ mm[i]) & 1u;
+      return;
     }
-  }
+    ulonglong2 v[IB];
+#pragma unroll
+    for (int i = 0; i < IB; ++i)                   // IB independent probes in flight (unconditional:
+      v[i] = *reinterpret_cast<const ulonglong2*>(T.prim + 2 * (hh[i] >> T.qbits));   // no per-load branch)
+    if (dbg & 2) {                                 // dev knob: loads only
+#pragma unroll
+      for (int i = 0; i < IB; ++i) created += (unsigned)(v[i].x ^ v[i].y) & 1u;
+      return;
+    }
+    tab_or_batch(T, cc, hh, mm, v, flags, created, dbg);
+  };
+  if (q0 > 0 && q0 + IW <= last) {
+    // interior thread (no window 0, no last window, all IW live): the context
+    // bytes come from LDS once, into registers; P(i) = S(q-1), D(i) = S(q+k-1)
+    // for window q = q0 + i, and D(i+1) = S(q+k)
+    const uint32_t o = (uint32_t)(base + q0);
+    uint32_t P[IW / 4], D[IW / 4 + 1];
+    lds_bytes(s_cls, o - 1, P);
+    lds_bytes(s_cls, o + (uint32_t)k - 1, D);
+#pragma unroll
+    for (int h = 0; h < IW / IB; ++h) {
+      uint64_t cc[IB], hh[IB];
+      uint32_t mm[IB];
+#pragma unroll
+      for (int i = 0; i < IB; ++i) {
+        const int x = h * IB + i;
+        const uint32_t p = byte_at(P, x), s = byte_at(D, x + 1);
+        if (x) {                                   // Nu // 5 + alpha * 5^(k-1) (:1072)
+          const uint32_t din = byte_at(D, x);
+          K = (K - digit_fw(p)) * INV5 + (uint64_t)digit_fw(din) * shift;
+          Kr = (Kr - (uint64_t)digit_rc(p) * shift) * 5 + digit_rc(din);
+        }
+        const uint32_t mf = (lam_fw(p) << OFFBIT) | lam_fw(s) | PRES_A;
+        if (RC) {
+          const uint32_t mr = (lam_rc(s) << OFFBIT) | lam_rc(p) | PRES_A;
+          const bool lt = K < Kr, eq = K == Kr;
+          cc[i] = lt ? K : Kr;
+          mm[i] = eq ? (mf | mr) : lt ? (mf | (mr << B_SHIFT)) : (mr | (mf << B_SHIFT));
+        } else {
+          const bool le = K <= Kr;
+          cc[i] = le ? K : Kr;
+          mm[i] = le ? mf : (mf << B_SHIFT);
+        }
+        hh[i] = T.perm(cc[i]);
+      }
+      probe(cc, hh, mm);
+    }
+  } else {
   for (long long qb = q0; qb < q1; qb += IB) {
     uint64_t cc[IB], hh[IB];
     uint32_t mm[IB];
@@ -196,19 +341,197 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
       }
       hh[i] = T.perm(cc[i]);
     }
-    ulonglong2 v[IB];
+    probe(cc, hh, mm);
+  }
+  }
+  block_count(created, flags);                     // both paths: one barrier per wave
+}
+
+// K3, group form (pangenome inputs).  One block takes stripe j (GW windows) of
+// GG records at once.  Every genome of a pangenome repeats most k-mers of its
+// neighbours at nearly the same offset, so the block first merges its
+// windows' (canonical key, mask) pairs in an LDS hash table (OR is idempotent
+// and commutative: the table ends the same), then probes / updates the HBM
+// table once per distinct key instead of once per window (C3: ~18% of the
+// windows of 8 genomes' stripe are distinct).  A window that finds no LDS slot
+// within a few probes goes straight to the HBM table.
+constexpr int GG = 8;                         // records per group
+constexpr int GNW = 16;                       // consecutive windows per thread
+constexpr int GTPR = IBLOCK / GG;             // threads per record (32)
+constexpr int GW = GTPR * GNW;                // stripe length (512 windows)
+constexpr int GPAD = 16;                      // staging front pad (window q0-2 of q0 < 2)
+constexpr int GSPAN = GPAD + GW + 64;         // staged bytes per record (+ k + 3 context)
+constexpr int HBITS = 11;
+constexpr int HCAP = 1 << HBITS;              // LDS hash slots
+constexpr int LB = 8;                         // LDS lookups in flight per thread
+static_assert(HCAP * 2 <= GG * GSPAN, "slot list reuses the staging bytes");
+
+__device__ __forceinline__ uint32_t lds_hash(uint64_t c) {
+  return (uint32_t)((c * 0x9E3779B97F4A7C15ull) >> (64 - HBITS));
+}
+
+template <bool RC>
+__global__ void __launch_bounds__(IBLOCK)
+k_insert_grp(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__ tiles,
+             const int* __restrict__ groups, const long long* __restrict__ rec_start,
+             const long long* __restrict__ rec_len, int k, uint64_t shift, TableView T, unsigned* __restrict__ flags,
+             int dbg) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_cls[GG][GSPAN];
+  __shared__ unsigned long long hkey[HCAP];
+  __shared__ uint32_t hmask[HCAP];
+  __shared__ uint32_t s_scan[IBLOCK / 64];
+  const unsigned long long tile = tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
+  const int* grp = groups + (size_t)(tile >> 32) * GG;
+  const long long qt = (long long)(tile & 0xFFFFFFFFull) * GW;
+  for (int s = threadIdx.x; s < HCAP; s += IBLOCK) { hkey[s] = 0ull; hmask[s] = 0u; }
+  // stage record positions [qt-2, qt+GW+k+2) of each record at s_cls[g][GPAD-2 ..]
+  constexpr int CPR = (GSPAN - GPAD + 15) / 16;  // 16-byte chunks per record
+  for (int i = threadIdx.x; i < GG * CPR; i += IBLOCK) {
+    const int g = i / CPR, ch = i % CPR;
+    const int r = grp[g];
+    if (r < 0) continue;
+    const long long rs = rec_start[r], rn = rec_len[r];
+    if (qt > rn - k) continue;
+    const long long lo = rs + (qt >= 2 ? qt - 2 : 0);
+    const long long hi = rs + (qt + GW + k + 2 < rn ? qt + GW + k + 2 : rn);
+    const long long a0 = lo & ~15ll;
+    if (a0 + 16 * ch < hi)
+      *reinterpret_cast<uint4*>(&s_cls[g][GPAD + 16 * ch]) = *reinterpret_cast<const uint4*>(cls + a0 + 16 * ch);
+  }
+  __syncthreads();
+  unsigned created = 0;
+  {
+    const int g = threadIdx.x / GTPR;
+    const int r = grp[g];
+    const long long rs = r >= 0 ? rec_start[r] : 0, rn = r >= 0 ? rec_len[r] : 0;
+    const long long last = rn - k;
+    const long long q0 = qt + (long long)(threadIdx.x % GTPR) * GNW;
+    const long long q1 = q0 + GNW <= last + 1 ? q0 + GNW : last + 1;
+    if (r >= 0 && q0 < q1) {
+      const uint8_t* sc = s_cls[g];
+      // s_cls index of record position q: GPAD + q - a0 + rs
+      const long long base = GPAD + rs - ((rs + (qt >= 2 ? qt - 2 : 0)) & ~15ll);
+      uint32_t A[(GNW + 1 + 3) / 4], B[(GNW + 2 + 3) / 4];
+      lds_bytes(sc, (uint32_t)(base + q0 - 2), A);           // A(j) = S(q0 - 2 + j)
+      lds_bytes(sc, (uint32_t)(base + q0 + k - 1), B);       // B(j) = S(q0 + k - 1 + j)
+      uint64_t K = 0, Kr = 0;
+      init_keys(sc, (uint32_t)(base + q0), k, K, Kr);
+      uint64_t cb[LB];
+      uint32_t mb[LB];
+      int nb = 0;
 #pragma unroll
-    for (int i = 0; i < IB; ++i)                   // IB independent probes in flight (unconditional:
-      v[i] = *reinterpret_cast<const ulonglong2*>(T.prim + 2 * (hh[i] >> T.qbits));   // no per-load branch)
+      for (int i = 0; i < GNW; ++i) {
+        const long long q = q0 + i;
+        const bool live = q < q1;
+        if (i) {                                              // Nu // 5 + alpha * 5^(k-1) (:1072)
+          const uint32_t dout = byte_at(A, i + 1), din = byte_at(B, i);
+          K = (K - digit_fw(dout)) * INV5 + (uint64_t)digit_fw(din) * shift;
+          Kr = (Kr - (uint64_t)digit_rc(dout) * shift) * 5 + digit_rc(din);
+        }
+        // forward window q: pred '#' at q==0, s[q-2] at the last window (:1080 quirk), else s[q-1]
+        const uint32_t fpred = q == 0 ? LAM_HASH : lam_fw(q == last ? byte_at(A, i) : byte_at(A, i + 1));
+        const uint32_t fsucc = q == last ? LAM_DOLLAR : lam_fw(byte_at(B, i + 1));
+        const uint32_t mf = (fpred << OFFBIT) | fsucc | PRES_A;
+        uint64_t c;
+        uint32_t m;
+        if (RC) {
+          // its twin: reverse-strand window n-k-q, same boundary rules on that strand
+          const uint32_t rpred = q == last ? LAM_HASH : lam_rc(q == 0 ? byte_at(B, i + 2) : byte_at(B, i + 1));
+          const uint32_t rsucc = q == 0 ? LAM_DOLLAR : lam_rc(byte_at(A, i + 1));
+          const uint32_t mr = (rpred << OFFBIT) | rsucc | PRES_A;
+          if (K < Kr)      { c = K;  m = mf | (mr << B_SHIFT); }
+          else if (K > Kr) { c = Kr; m = mr | (mf << B_SHIFT); }
+          else             { c = K;  m = mf | mr; }
+        } else {
+          if (K <= Kr) { c = K; m = mf; } else { c = Kr; m = mf << B_SHIFT; }
+        }
+        cb[i % LB] = c;
+        mb[i % LB] = live ? m : 0u;
+        if (i % LB == LB - 1) {                              // merge a batch: LB lookups in flight
+          if (dbg & 1) {
+#pragma unroll
+            for (int x = 0; x < LB; ++x) created += (unsigned)(cb[x] ^ mb[x]) & 1u;
+          } else {
+            // all LB entries advance together: a round issues every pending
+            // entry's CAS (empty slot) or next-slot read, then resolves them
+            uint32_t hb[LB];
+            unsigned long long cur[LB];
+            uint32_t pend = 0;
+#pragma unroll
+            for (int x = 0; x < LB; ++x) {
+              hb[x] = lds_hash(cb[x]);
+              cur[x] = hkey[hb[x]];
+              pend |= (mb[x] != 0u) << x;
+            }
+            for (int round = 0; pend && round < 16; ++round) {
+              bool empty[LB];
+#pragma unroll
+              for (int x = 0; x < LB; ++x) {
+                empty[x] = false;
+                if (((pend >> x) & 1u) && cur[x] == 0ull) {
+                  empty[x] = true;
+                  cur[x] = atomicCAS(&hkey[hb[x]], 0ull, (unsigned long long)cb[x] + 1ull);
+                }
+              }
+#pragma unroll
+              for (int x = 0; x < LB; ++x) {
+                if (!((pend >> x) & 1u)) continue;
+                const unsigned long long k1 = (unsigned long long)cb[x] + 1ull;
+                if ((empty[x] && cur[x] == 0ull) || cur[x] == k1) {
+                  atomicOr(&hmask[hb[x]], mb[x]);
+                  pend &= ~(1u << x);
+                } else {                                      // another key: next slot
+                  hb[x] = (hb[x] + 1u) & (HCAP - 1);
+                  cur[x] = hkey[hb[x]];
+                }
+              }
+            }
+#pragma unroll
+            for (int x = 0; x < LB; ++x)                      // no LDS slot: straight to HBM
+              if ((pend >> x) & 1u) created += (unsigned)tab_or(T, cb[x], mb[x], flags);
+          }
+        }
+        (void)nb;
+      }
+    }
+  }
+  __syncthreads();
+  // compact the occupied slots (their indices reuse the staging bytes)
+  constexpr int HPT = HCAP / IBLOCK;
+  uint16_t* list = reinterpret_cast<uint16_t*>(&s_cls[0][0]);
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int i = 0; i < HPT; ++i) cnt += hkey[threadIdx.x * HPT + i] != 0ull;
+  uint32_t U;
+  uint32_t o = block_excl_scan<IBLOCK>(cnt, s_scan, U);
+#pragma unroll
+  for (int i = 0; i < HPT; ++i)
+    if (hkey[threadIdx.x * HPT + i] != 0ull) list[o++] = (uint16_t)(threadIdx.x * HPT + i);
+  __syncthreads();
+  for (uint32_t b0 = 0; b0 < ((dbg & 4) ? 0u : U); b0 += IBLOCK * IB) {   // dev knob 4: no HBM phase
+    uint64_t cc[IB], hh[IB];
+    uint32_t mm[IB];
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
-      if (!mm[i]) continue;
-      const uint64_t b = hh[i] >> T.qbits, q = hh[i] & qmask;
-      const bool done0 = v[i].x != 0ull && (v[i].x >> MW_BITS) == q && (v[i].x & mm[i]) == mm[i];
-      const bool done1 = v[i].y != 0ull && (v[i].y >> MW_BITS) == q && (v[i].y & mm[i]) == mm[i];
-      if (done0 || done1) continue;                // complete: nothing to do
-      created += (unsigned)tab_or_at(T, cc[i], b, q, mm[i], v[i], flags);
+      const uint32_t idx = b0 + (uint32_t)i * IBLOCK + threadIdx.x;
+      mm[i] = 0;
+      cc[i] = 0;
+      if (idx < U) {
+        const uint32_t s = list[idx];
+        cc[i] = hkey[s] - 1ull;
+        mm[i] = hmask[s];
+      }
+      hh[i] = T.perm(cc[i]);
     }
+    ulonglong2 v[IB];
+#pragma unroll
+    for (int i = 0; i < IB; ++i) v[i] = *reinterpret_cast<const ulonglong2*>(T.prim + 2 * (hh[i] >> T.qbits));
+    if (dbg & 2) {                                 // dev knob: loads only
+#pragma unroll
+      for (int i = 0; i < IB; ++i) created += (unsigned)(v[i].x ^ v[i].y) & 1u;
+      continue;
+    }
+    tab_or_batch(T, cc, hh, mm, v, flags, created);
   }
   block_count(created, flags);
 }
@@ -293,14 +616,14 @@ constexpr int RCAP = 4 * (int)RUNIT;               // a whole unit always fits a
 // by the few member lanes of every wave during the sweep.
 __device__ __forceinline__ void reduce_flush(const TableView& T, unsigned long long* stage, uint32_t n,
                                              unsigned long long* s_base, unsigned long long* __restrict__ out,
-                                             unsigned long long* __restrict__ counter) {
+                                             uint64_t cap, unsigned long long* __restrict__ counter) {
   if (threadIdx.x == 0) *s_base = atomicAdd(counter, (unsigned long long)n);
   __syncthreads();
   const unsigned long long b = *s_base;
   for (uint32_t x = threadIdx.x; x < n; x += RT) {
     const unsigned long long v = stage[x];
     const uint64_t c = T.unperm(v & ~(1ull << 63));
-    out[b + x] = (v >> 63) ? T.rc(c) : c;
+    if (b + x < cap) out[b + x] = (v >> 63) ? T.rc(c) : c;   // the host rejects a count above cap
   }
   __syncthreads();
 }
@@ -317,7 +640,7 @@ __device__ __forceinline__ void reduce_load(const TableView& T, uint64_t nb, uin
 }
 
 __global__ void __launch_bounds__(RT)
-k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __restrict__ out,
+k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __restrict__ out, uint64_t cap,
          unsigned long long* __restrict__ counters) {
   __shared__ unsigned long long stage[RCAP];
   __shared__ uint32_t lds[RT / 64];
@@ -355,7 +678,7 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
     uint32_t tot;
     const uint32_t pre = block_excl_scan<RT>(cnt, lds, tot);
     if (staged + tot > (uint32_t)RCAP) {           // block-uniform
-      reduce_flush(T, stage, staged, &s_base, out, counters);
+      reduce_flush(T, stage, staged, &s_base, out, cap, counters);
       staged = 0;
     }
     if (cnt) {
@@ -385,7 +708,7 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
 #pragma unroll
     for (int j = 0; j < RU; ++j) e[j] = nx[j];
   }
-  if (staged) reduce_flush(T, stage, staged, &s_base, out, counters);
+  if (staged) reduce_flush(T, stage, staged, &s_base, out, cap, counters);
   for (int o = 32; o > 0; o >>= 1) ndbg += __shfl_down(ndbg, o, 64);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ndbg;
   __syncthreads();
@@ -399,7 +722,7 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
 // dBG export: (key, 12-bit mask) of both orientations of every entry
 __global__ void k_export_dbg(TableView T, uint64_t nw, uint64_t ntot, int k,
                              unsigned long long* __restrict__ keys, unsigned short* __restrict__ masks,
-                             unsigned long long* __restrict__ counter) {
+                             uint64_t cap, unsigned long long* __restrict__ counter) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt = (1ull << lane) - 1ull;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntot;
@@ -415,11 +738,10 @@ __global__ void k_export_dbg(TableView T, uint64_t nw, uint64_t ntot, int k,
     base = __shfl(base, leader, 64);
     if (!(pa || pb)) continue;
     const uint64_t c = entry_key(T, nw, i);
-    if (pa) { uint64_t o = base + __builtin_popcountll(ba & lt); keys[o] = c; masks[o] = m & MASK12; }
-    if (pb) {
-      uint64_t o = base + na + __builtin_popcountll(bb & lt);
-      keys[o] = T.rc(c); masks[o] = (m >> B_SHIFT) & MASK12;
-    }
+    // writes past cap are dropped; the host rejects a count above cap
+    const uint64_t oa = base + __builtin_popcountll(ba & lt), ob = base + na + __builtin_popcountll(bb & lt);
+    if (pa && oa < cap) { keys[oa] = c; masks[oa] = m & MASK12; }
+    if (pb && ob < cap) { keys[ob] = T.rc(c); masks[ob] = (m >> B_SHIFT) & MASK12; }
   }
 }
 
@@ -526,7 +848,8 @@ constexpr uint64_t LEAD = 4;
 
 static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   const uint64_t R = c.n_records;
-  if (c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k) return c.n_tiles;
+  if (c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k && c.tile_mode == 0)
+    return c.n_tiles;
   std::vector<std::pair<uint64_t, int>> nt;           // (stripes, record)
   uint64_t total = 0, maxs = 0;
   for (uint64_t r = 0; r < R; ++r) {
@@ -555,8 +878,84 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   c.tile_sig_len = c.h_rec_len;
   c.tile_sig_flag = flag;
   c.tile_k = c.k;
+  c.tile_mode = 0;
   c.n_tiles = total;
   return total;
+}
+
+// Group tiles for k_insert_grp: records (n >= k+2) sorted by length, in groups
+// of GG; tile = group << 32 | stripe (GW windows), stripe-major, the first
+// group LEAD stripes ahead of the rest (see make_tiles).
+static uint64_t make_group_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
+  const uint64_t R = c.n_records;
+  if (c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k && c.tile_mode == 1)
+    return c.n_tiles;
+  std::vector<std::pair<uint64_t, int>> nt;           // (stripes, record)
+  for (uint64_t r = 0; r < R; ++r) {
+    const int64_t n = c.h_rec_len[r];
+    if (!flag[r] || n < c.k + 2) continue;
+    nt.push_back({(uint64_t)((n - c.k + 1 + GW - 1) / GW), (int)r});
+  }
+  std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  const size_t ng = (nt.size() + GG - 1) / GG;
+  std::vector<int> grp(ng * GG, -1);
+  std::vector<uint64_t> gs(ng, 0);
+  for (size_t i = 0; i < nt.size(); ++i) {
+    grp[i] = nt[i].second;
+    gs[i / GG] = std::max(gs[i / GG], nt[i].first);
+  }
+  std::vector<unsigned long long> tiles;
+  const uint64_t maxs = ng ? gs[0] : 0;
+  for (uint64_t j = 0; j < maxs + LEAD; ++j) {
+    if (ng && j < gs[0]) tiles.push_back(j);                   // group 0 leads
+    if (j < LEAD) continue;
+    const uint64_t jf = j - LEAD;
+    for (size_t g = 1; g < ng; ++g)
+      if (jf < gs[g]) tiles.push_back(((unsigned long long)g << 32) | jf);
+  }
+  const uint64_t total = tiles.size();
+  c.tiles.reserve(8 * (total + 1));
+  c.groups.reserve(4 * (grp.size() + 1));
+  if (total) PG_HIP(hipMemcpyAsync(c.tiles.p, tiles.data(), 8 * total, hipMemcpyHostToDevice, c.stream));
+  if (!grp.empty()) PG_HIP(hipMemcpyAsync(c.groups.p, grp.data(), 4 * grp.size(), hipMemcpyHostToDevice, c.stream));
+  c.sync();
+  c.tile_sig_len = c.h_rec_len;
+  c.tile_sig_flag = flag;
+  c.tile_k = c.k;
+  c.tile_mode = 1;
+  c.n_tiles = total;
+  return total;
+}
+
+// K3 form: per-record tiles (k_insert) by default; PG_K3=group selects the
+// group kernel (needs at least GG long records to pay off).  On C3 the tile
+// form is ahead today (6.3 vs 7.8 ms: the group form's LDS merge is
+// latency-bound at its occupancy); both are parity-tested.
+static int k3_mode(const Ctx& c, const std::vector<uint8_t>& flag) {
+  const char* e = getenv("PG_K3");
+  if (!e || strcmp(e, "group")) return 0;
+  uint64_t n = 0;
+  for (uint64_t r = 0; r < c.n_records; ++r) n += flag[r] && c.h_rec_len[r] >= c.k + 2;
+  return n >= (uint64_t)GG ? 1 : 0;
+}
+
+static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t shift, unsigned* flags, int dbg) {
+  const dim3 g((unsigned)ntiles), b(IBLOCK);
+  const uint8_t* cls = c.cls.as<uint8_t>();
+  const auto* tiles = c.tiles.as<unsigned long long>();
+  const auto* rs = c.rec_start.as<long long>();
+  const auto* rl = c.rec_len.as<long long>();
+  if (mode && rc0)
+    hipLaunchKernelGGL(k_insert_grp<true>, g, b, 0, c.stream, cls, tiles, c.groups.as<int>(), rs, rl, c.k, shift, c.tv,
+                       flags, dbg);
+  else if (mode)
+    hipLaunchKernelGGL(k_insert_grp<false>, g, b, 0, c.stream, cls, tiles, c.groups.as<int>(), rs, rl, c.k, shift, c.tv,
+                       flags, dbg);
+  else if (rc0)
+    hipLaunchKernelGGL(k_insert<true>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, dbg);
+  else
+    hipLaunchKernelGGL(k_insert<false>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, dbg);
+  PG_HIP(hipGetLastError());
 }
 
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
@@ -576,11 +975,17 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
       c.windows_fw += n > c.k ? (uint64_t)(n - c.k + 1) : 1;
     }
   c.windows_total = c.windows_fw * (rc0 ? 2 : 1);
-  const uint64_t ntiles = make_tiles(c, flag);
+  const int mode = k3_mode(c, flag);
+  const uint64_t ntiles = mode ? make_group_tiles(c, flag) : make_tiles(c, flag);
   // expected canonical keys: learned from the previous build, else an upper
   // bound (every forward window distinct); an overflow rebuilds larger
   uint64_t keys = c.cap_hint ? c.cap_hint : std::max<uint64_t>(1024, c.windows_fw);
   const uint64_t shift = pow5(c.k - 1);
+  // PG_K3_DBG (development only): 1 = windows only, 2 = HBM loads without
+  // updates, 4 = group form without its HBM phase; PG_K3_KEYS fixes the table
+  // size for such runs.  The product path never sets them.
+  const int dbg = getenv("PG_K3_DBG") ? atoi(getenv("PG_K3_DBG")) : 0;
+  if (dbg && getenv("PG_K3_KEYS")) keys = strtoull(getenv("PG_K3_KEYS"), nullptr, 10);
   c.t0.init(); c.t1.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
     alloc_table(c, keys);
@@ -589,17 +994,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     c.t0.stop(c.stream);
     unsigned* flags = c.flags.as<unsigned>();
     c.t1.start(c.stream);
-    if (ntiles) {
-      if (rc0)
-        hipLaunchKernelGGL(k_insert<true>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
-                           c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                           c.k, shift, c.tv, flags);
-      else
-        hipLaunchKernelGGL(k_insert<false>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
-                           c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                           c.k, shift, c.tv, flags);
-      PG_HIP(hipGetLastError());
-    }
+    if (ntiles) launch_insert(c, mode, rc0, ntiles, shift, flags, dbg);
     c.t1.stop(c.stream);
     if (R) {
       hipLaunchKernelGGL(k_short, dim3(grid_for(R, IBLOCK, 1024)), dim3(IBLOCK), 0, c.stream,
@@ -613,19 +1008,15 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     read_flags(c, sentinel, overflow, created);
     c.ms_clear = c.t0.ms();
     c.ms_insert = c.t1.ms();
+    if (dbg) {                       // dev knob run: timings only, the table is not a dBG
+      fprintf(stderr, "PG_K3_DBG=%d mode=%d insert=%.3f ms\n", dbg, mode, c.ms_insert);
+      return;
+    }
     if (!overflow) {
       c.n_canon = created;
       c.sentinel = sentinel ? 1 : 0;
       c.cap_hint = std::max<uint64_t>(1024, created + created / 4);
       c.built = true;
-      if (getenv("PG_DEBUG_REINSERT") && ntiles && rc0) {   // diagnostic: probe cost without atomics
-        c.t1.start(c.stream);
-        hipLaunchKernelGGL(k_insert<true>, dim3((unsigned)ntiles), dim3(IBLOCK), 0, c.stream, c.cls.as<uint8_t>(),
-                           c.tiles.as<unsigned long long>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                           c.k, shift, c.tv, flags);
-        c.t1.stop(c.stream);
-        fprintf(stderr, "PG_DEBUG_REINSERT first=%.3f ms re-insert=%.3f ms\n", c.ms_insert, c.t1.ms());
-      }
       return;
     }
     keys = std::max<uint64_t>(keys * 4, created * 2);
@@ -642,13 +1033,14 @@ void build_rdbg(Ctx& c) {
   c.t0.start(c.stream);
   const uint64_t nel = c.cap + c.ovf_cap;               // 16-byte elements: buckets, then overflow slots
   hipLaunchKernelGGL(k_reduce, dim3(grid_for(nel / RUNIT, 1, 4096)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
-                     c.k, c.rdbg_keys.as<unsigned long long>(), cnt.as<unsigned long long>());
+                     c.k, c.rdbg_keys.as<unsigned long long>(), 2 * c.n_canon + 1, cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
   c.t0.stop(c.stream);
   unsigned long long res[9];
   PG_HIP(hipMemcpyAsync(res, cnt.p, sizeof(res), hipMemcpyDeviceToHost, c.stream));
   c.sync();
   c.ms_scan = c.t0.ms();
+  if (res[0] > 2 * c.n_canon + 1) throw Error(-5, "build_rdbg: member count exceeds the table's key count");
   c.n_rdbg = res[0];
   c.n_dbg = res[8];
   if (c.sentinel) {         // key 2^64-1, mask 32: always an rdBG member
@@ -671,12 +1063,16 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {
   cnt.reserve(8);
   PG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
   hipLaunchKernelGGL(k_export_dbg, dim3(grid_for(n_entries(c), 256, 8192)), dim3(256), 0, c.stream, c.tv,
-                     2 * c.cap, n_entries(c), c.k, keys.as<unsigned long long>(), masks.as<unsigned short>(),
+                     2 * c.cap, n_entries(c), c.k, keys.as<unsigned long long>(), masks.as<unsigned short>(), nmax,
                      cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
   unsigned long long n = 0;
   PG_HIP(hipMemcpyAsync(&n, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
   c.sync();
+  if (n > nmax) {
+    keys.release(); masks.release(); cnt.release();
+    throw Error(-5, "export_dbg: entry count exceeds the table's key count");
+  }
   const uint64_t total = n + (c.sentinel ? 1 : 0);
   if (h_keys && cap >= total) {
     PG_HIP(hipMemcpy(h_keys, keys.p, 8 * n, hipMemcpyDeviceToHost));

@@ -108,6 +108,8 @@ struct Ctx {
   DevBuf tiles;                   // K3 tile list (record << 32 | stripe), stripe-major
   uint64_t n_tiles = 0;
   int tile_k = 0;
+  int tile_mode = 0;              // 0: per-record tiles (k_insert), 1: record groups (k_insert_grp)
+  DevBuf groups;                  // int32 [n_groups * GG] record ids, -1 padded
   std::vector<int64_t> tile_sig_len;   // record lengths / flags the tile list was built for
   std::vector<uint8_t> tile_sig_flag;
   DevBuf tile_cnt, tile_off;      // per tile x strand counts / offsets

@@ -102,6 +102,32 @@ def test_pangenome_vs_oracle(km, oracle_mod, tmp_path, c):
     assert got["rows"] == ref["rows"]
 
 
+@pytest.mark.parametrize("form", ["tile", "group"])
+@pytest.mark.parametrize("rc0", [True, False])
+def test_k3_forms_vs_oracle(oracle_mod, monkeypatch, form, rc0):
+    """Both K3 kernels (per-record tiles, record groups with the LDS merge) on
+    a pangenome with ragged record lengths, including records shorter than a
+    stripe and records of n <= k+1."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    monkeypatch.setenv("PG_K3", form)
+    fasta = synth.pangenome(11, 70_000, snp=0.004, indel=6e-4, seed=31)
+    fasta += b">s1\nACGTACGTACGTACGTACGTACGTACGT\n>s2\nACGT\n>s3\n" + b"A" * 700 + b"\n"
+    c = 2 if rc0 else 0
+    ref = oracle_mod.OracleRun(fasta, 27, c)
+    ctx = Context(27)
+    ctx.set_fasta(fasta)
+    ctx.parse()
+    ctx.build_dbg(None, 0, rc0)
+    keys, masks = ctx.dbg()
+    ctx.build_rdbg()
+    rk, rm = ref.dbg()
+    assert np.array_equal(keys, rk)
+    assert np.array_equal(masks, rm)
+    assert np.array_equal(ctx.rdbg(), ref.rdbg())
+    ctx.close()
+
+
 def test_edge_checkpoint_reversal_vs_oracle(km, oracle_mod, tmp_path):
     from pangenome_amd import synth
     fasta = b"junk before header\n" + synth.pangenome(9, 20_000, snp=0.01, indel=1e-3, seed=5)
