@@ -93,6 +93,26 @@ int pg_dbg_export(pg_ctx* ctx, uint64_t* keys, uint16_t* masks, uint64_t cap, ui
 /* rdBG keys, unordered. keys == NULL: only *n is set. */
 int pg_rdbg_export(pg_ctx* ctx, uint64_t* keys, uint64_t cap, uint64_t* n);
 
+/* ---- npz persistence: dump() / load_on_disk() (kmer_numba.py:243-335).
+ * pg_dbg_dump writes the last build's dBG as an oakht slot layout that
+ * load_on_disk (:289-335) and oakht.pointer (:521-538) accept: FNV-1a over the
+ * key's low 4 bytes mod a prime capacity, probes j, j, j+1, j+4, j+9, ...;
+ * keys[capacity] uint64, values[capacity] uint16 (12-bit mask), counts
+ * [capacity] uint8 = occurrences of the oriented key, saturating at 255
+ * (__setitem__ :556; counted by an extra window pass over the build).
+ * *capacity == 0 picks the reference's growth chain (find_prime(2^20), then
+ * find_prime(cap * 1.62) while size > 0.75 * cap, :423-474).  keys == NULL
+ * only sets *capacity and *size (call again with arrays of *capacity). */
+int pg_dbg_dump(pg_ctx* ctx, uint64_t* capacity, uint64_t* keys, uint16_t* values, uint8_t* counts, uint64_t* size);
+/* Stage (oriented key, 12-bit mask, count) pairs — the counts > 0 slots of a
+ * loaded npz — to be OR-merged into every following pg_build_dbg (-d: a dBG
+ * with no records inserted; -D: rdBG keys with mask 0, members by the rdBG
+ * rule; -r: a checkpoint the build resumes onto).  Key 2^64-1 is the n<k
+ * sentinel.  counts may be NULL (1 each); n == 0 clears the stage. */
+int pg_dbg_load(pg_ctx* ctx, const uint64_t* keys, const uint16_t* masks, const uint8_t* counts, uint64_t n);
+/* The reference's final oakht capacity for `size` keys (host only). */
+uint64_t pg_oakht_capacity(uint64_t size);
+
 /* ---- multi-GPU exchange (one process per GPU; the caller moves the bytes
  *      with RCCL).  Replaces nothing in the reference, which is single-core. */
 /* Owner-partition this rank's local dBG into `nparts` contiguous runs of

@@ -45,6 +45,9 @@ def lib():
             getattr(L, f).restype = C.c_double
         L.pgo_get_dbg.argtypes = [P, P, P]
         L.pgo_get_rdbg.argtypes = [P, P]
+        L.pgo_get_dbg_counts.argtypes = [P, P]
+        L.pgo_dbg_capacity.argtypes = [P]
+        L.pgo_dbg_capacity.restype = i64
         L.pgo_get_edges.argtypes = [P, P, P]
         L.pgo_get_rows.argtypes = [P, P]
         L.pgo_free.argtypes = [P]
@@ -93,6 +96,21 @@ class OracleRun:
         lib().pgo_get_dbg(self.h, keys.ctypes.data, masks.ctypes.data)
         o = np.argsort(keys, kind="stable")
         return keys[o], masks[o]
+
+    def dbg_counts(self):
+        """(keys, masks, counts) sorted by key: the oakht's saturating occurrence
+        counts (__setitem__ :556), as `<in>_db.npz` stores them."""
+        n = lib().pgo_n_dbg(self.h)
+        keys = np.empty(n, np.uint64)
+        masks = np.empty(n, np.uint16)
+        counts = np.empty(n, np.uint8)
+        lib().pgo_get_dbg(self.h, keys.ctypes.data, masks.ctypes.data)
+        lib().pgo_get_dbg_counts(self.h, counts.ctypes.data)
+        o = np.argsort(keys, kind="stable")
+        return keys[o], masks[o], counts[o]
+
+    def dbg_capacity(self):
+        return int(lib().pgo_dbg_capacity(self.h))
 
     def rdbg(self):
         n = lib().pgo_n_rdbg(self.h)

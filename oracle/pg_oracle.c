@@ -555,6 +555,12 @@ void pgo_get_dbg(const pgo_result* r, uint64_t* keys, uint16_t* masks) {   /* it
     for (int64_t i = 0; i < r->dbg.cap; i++)
         if (r->dbg.counts[i]) { keys[o] = r->dbg.keys[i]; masks[o] = r->dbg.vals[i]; o++; }
 }
+void pgo_get_dbg_counts(const pgo_result* r, uint8_t* counts) {         /* counts, same order */
+    int64_t o = 0;
+    for (int64_t i = 0; i < r->dbg.cap; i++)
+        if (r->dbg.counts[i]) counts[o++] = r->dbg.counts[i];
+}
+int64_t pgo_dbg_capacity(const pgo_result* r) { return r->dbg.cap; }   /* dump parameters[0] (:253) */
 void pgo_get_rdbg(const pgo_result* r, uint64_t* keys) {
     int64_t o = 0;
     for (int64_t i = 0; i < r->rdbg.cap; i++)

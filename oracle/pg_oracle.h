@@ -59,6 +59,8 @@ double pgo_seconds_rdbg(const pgo_result* r);
 
 /* Copy-outs, in the oakht's slot order (dBG, rdBG) or reference order. */
 void pgo_get_dbg(const pgo_result* r, uint64_t* keys, uint16_t* masks);
+void pgo_get_dbg_counts(const pgo_result* r, uint8_t* counts);   /* saturating occurrence counts */
+int64_t pgo_dbg_capacity(const pgo_result* r);
 void pgo_get_rdbg(const pgo_result* r, uint64_t* keys);
 /* edges: 4 x uint64 per edge (n0, v0, n1, v1) and the walk count */
 void pgo_get_edges(const pgo_result* r, uint64_t* tuples, int64_t* counts);

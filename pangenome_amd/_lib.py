@@ -55,6 +55,9 @@ SIGNATURES = {
     "pg_rows": (C.c_int, [_P, _P, C.c_int, _U64P]),
     "pg_rows_export": (C.c_int, [_P, _P, C.c_uint64]),
     "pg_get_stats": (C.c_int, [_P, _SP]),
+    "pg_dbg_dump": (C.c_int, [_P, _U64P, _P, _P, _P, _U64P]),
+    "pg_dbg_load": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
+    "pg_oakht_capacity": (C.c_uint64, [C.c_uint64]),
 }
 
 _lib = None
@@ -179,6 +182,26 @@ class Context:
         keys = np.empty(n.value, np.uint64)
         check(self.lib.pg_rdbg_export(self.h, ptr(keys), n.value, C.byref(n)), "pg_rdbg_export")
         return np.sort(keys)
+
+    # ----------------------------------------------------- npz persistence
+    def dbg_dump(self, capacity: int = 0):
+        """The last build's dBG as oakht slot arrays (dump(), :243-261):
+        (capacity, size, keys, values, counts)."""
+        cap, size = C.c_uint64(capacity), C.c_uint64()
+        check(self.lib.pg_dbg_dump(self.h, C.byref(cap), None, None, None, C.byref(size)), "pg_dbg_dump")
+        keys = np.empty(cap.value, np.uint64)
+        values = np.empty(cap.value, np.uint16)
+        counts = np.empty(cap.value, np.uint8)
+        check(self.lib.pg_dbg_dump(self.h, C.byref(cap), ptr(keys), ptr(values), ptr(counts), C.byref(size)),
+              "pg_dbg_dump")
+        return cap.value, size.value, keys, values, counts
+
+    def dbg_load(self, keys, masks=None, counts=None):
+        """Stage oriented (key, mask, count) slots for the following builds."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        m = None if masks is None else np.ascontiguousarray(masks, dtype=np.uint16)
+        c = None if counts is None else np.ascontiguousarray(counts, dtype=np.uint8)
+        check(self.lib.pg_dbg_load(self.h, ptr(keys), ptr(m), ptr(c), keys.shape[0]), "pg_dbg_load")
 
     # ------------------------------------------------------ multi-GPU hooks
     def partition(self, nparts: int, d_out: int | None = None, out_cap: int = 0):

@@ -74,7 +74,7 @@ void pg_destroy(pg_ctx* x) {
                         &c.rec_len, &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.ovf,
                         &c.flags,
                         &c.rdbg_keys, &c.tiles, &c.groups, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
-                        &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt};
+                        &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload, &c.dump_cnt};
   for (auto* b : bufs) b->release();
   c.t0.destroy();
   c.t1.destroy();
@@ -192,6 +192,30 @@ int pg_rdbg_export(pg_ctx* x, uint64_t* keys, uint64_t cap, uint64_t* n) {
       pg::export_rdbg(x->c, keys, cap);
     }
   });
+}
+
+int pg_dbg_dump(pg_ctx* x, uint64_t* capacity, uint64_t* keys, uint16_t* values, uint8_t* counts, uint64_t* size) {
+  return guard([&] {
+    if (!x || !capacity || !size) throw pg::Error(PG_EINVAL, "pg_dbg_dump: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    *size = pg::dbg_dump(x->c, *capacity, keys, values, counts);
+  });
+}
+
+int pg_dbg_load(pg_ctx* x, const uint64_t* keys, const uint16_t* masks, const uint8_t* counts, uint64_t n) {
+  return guard([&] {
+    if (!x || (n && !keys)) throw pg::Error(PG_EINVAL, "pg_dbg_load: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::dbg_load(x->c, keys, masks, counts, n);
+  });
+}
+
+uint64_t pg_oakht_capacity(uint64_t size) {
+  try {
+    return pg::oakht_capacity(size);
+  } catch (...) {
+    return 0;
+  }
 }
 
 int pg_dbg_partition(pg_ctx* x, int nparts, void* d_out, uint64_t out_cap, uint64_t* counts) {

@@ -231,6 +231,61 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, u
   return pre + x - v;
 }
 
+// build_dbg for one strand of length n in {k, k+1}: emit(key, 12-bit mask)
+// per window.  strand 0: s[i] = cls[rs+i]; strand 1: s[i] =
+// comp_class(cls[rs+n-1-i]) (tab_rev(reversed(s)), :1217).
+template <class Emit>
+__device__ void short_strand(const uint8_t* cls, long long rs, long long n, int strand, int k, uint64_t shift,
+                             Emit&& emit) {
+  auto S = [&](long long i) -> uint32_t {
+    return strand == 0 ? (uint32_t)cls[rs + i] : comp_class(cls[rs + n - 1 - i]);
+  };
+  uint64_t K0 = 0, pw = 1;
+  for (int j = 0; j < k; ++j) { K0 += (uint64_t)digit_fw(S(j)) * pw; pw *= 5; }
+  if (n == k) {                                            // :1084-1085
+    emit(K0, (LAM_HASH << OFFBIT) | LAM_DOLLAR);
+    return;
+  }
+  // n == k+1 (:1061-1082): the loop never runs and numba reads its variable as 0
+  emit(K0, (LAM_HASH << OFFBIT) | lam_fw(S(k)));
+  const uint64_t K1 = K0 / 5 + (uint64_t)digit_fw(S(1)) * shift;   // alpha[seq[0+1]]
+  emit(K1, (lam_fw(S(1)) << OFFBIT) | LAM_DOLLAR);                 // seq[0-k] == s[1]
+}
+
+// ---- table entries.  Entry index space: [0, nw = 2*buckets) primary words,
+// then [nw, nw + overflow slots) overflow slots.
+__device__ __forceinline__ uint32_t entry_mask(const TableView& T, uint64_t nw, uint64_t i) {
+  if (i < nw) {
+    const unsigned long long w = T.prim[i];
+    return w ? (uint32_t)(w & MW_MASK) : 0u;
+  }
+  const Slot s = T.ovf[i - nw];
+  return s.key1 ? s.mask : 0u;
+}
+__device__ __forceinline__ uint64_t entry_key(const TableView& T, uint64_t nw, uint64_t i) {
+  if (i < nw) return T.key_of(i >> 1, T.prim[i]);
+  return T.ovf[i - nw].key1 - 1ull;
+}
+// entry index of canonical key c (tab_get's search), or ~0 when absent
+__device__ __forceinline__ uint64_t tab_find(const TableView& T, uint64_t c) {
+  const uint64_t h = T.perm(c);
+  const uint64_t b = h >> T.qbits, q = h & ((1ull << T.qbits) - 1ull);
+  const unsigned long long* w = T.prim + 2 * b;
+  if (w[0] == 0ull) return ~0ull;
+  if ((w[0] >> MW_BITS) == q) return 2 * b;
+  if (w[1] == 0ull) return ~0ull;
+  if ((w[1] >> MW_BITS) == q) return 2 * b + 1;
+  const unsigned long long key1 = c + 1ull;
+  uint64_t slot = fmix64(c) & T.omask;
+  for (uint64_t probe = 0; probe <= T.omask; ++probe) {
+    const unsigned long long k1 = T.ovf[slot].key1;
+    if (k1 == key1) return 2 * (T.bmask + 1) + slot;
+    if (k1 == 0ull) return ~0ull;
+    slot = (slot + 1) & T.omask;
+  }
+  return ~0ull;
+}
+
 // bijective XCD-aware remap (cdna_hip_programming.md §5.5 T1): blocks b,
 // b+8, b+16, ... share an XCD under round-robin dispatch; give them
 // consecutive work items so an XCD's L2 sees contiguous work

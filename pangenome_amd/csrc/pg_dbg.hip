@@ -545,25 +545,6 @@ __device__ __forceinline__ void oriented_or(const TableView& T, int k, uint64_t 
   else created += (unsigned)tab_or(T, xr, m << B_SHIFT, flags);
 }
 
-// build_dbg for one strand of length n in {k, k+1}.  strand 0: s[i] = cls[rs+i];
-// strand 1: s[i] = comp_class(cls[rs+n-1-i]) (tab_rev(reversed(s)), :1217).
-__device__ void short_strand(const uint8_t* cls, long long rs, long long n, int strand, int k,
-                             uint64_t shift, const TableView& T, unsigned* flags, unsigned& created) {
-  auto S = [&](long long i) -> uint32_t {
-    return strand == 0 ? (uint32_t)cls[rs + i] : comp_class(cls[rs + n - 1 - i]);
-  };
-  uint64_t K0 = 0, pw = 1;
-  for (int j = 0; j < k; ++j) { K0 += (uint64_t)digit_fw(S(j)) * pw; pw *= 5; }
-  if (n == k) {                                            // :1084-1085
-    oriented_or(T, k, K0, (LAM_HASH << OFFBIT) | LAM_DOLLAR, flags, created);
-    return;
-  }
-  // n == k+1 (:1061-1082): the loop never runs and numba reads its variable as 0
-  oriented_or(T, k, K0, (LAM_HASH << OFFBIT) | lam_fw(S(k)), flags, created);
-  const uint64_t K1 = K0 / 5 + (uint64_t)digit_fw(S(1)) * shift;   // alpha[seq[0+1]]
-  oriented_or(T, k, K1, (lam_fw(S(1)) << OFFBIT) | LAM_DOLLAR, flags, created);  // seq[0-k] == s[1]
-}
-
 __global__ void __launch_bounds__(IBLOCK)
 k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start,
         const long long* __restrict__ rec_len, const uint8_t* __restrict__ rec_flag, uint64_t R, int k,
@@ -575,8 +556,9 @@ k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start
     const long long n = rec_len[r];
     if (n > k + 1) continue;
     if (n < k) { atomicOr(flags, 1u); continue; }          // key -1, mask '$' (:1087-1088)
-    short_strand(cls, rec_start[r], n, 0, k, shift, T, flags, created);
-    if (rc) short_strand(cls, rec_start[r], n, 1, k, shift, T, flags, created);
+    auto emit = [&](uint64_t x, uint32_t m12) { oriented_or(T, k, x, m12, flags, created); };
+    short_strand(cls, rec_start[r], n, 0, k, shift, emit);
+    if (rc) short_strand(cls, rec_start[r], n, 1, k, shift, emit);
   }
   block_count(created, flags);
 }
@@ -585,21 +567,30 @@ k_short(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start
 // pangenome_amd/host.py): each adds the n<k sentinel.
 __global__ void k_set_flag(unsigned* flags) { atomicOr(flags, 1u); }
 
+// Staged slots of a loaded npz (pg_dbg_load): OR each oriented (key, mask)
+// into the table as add_kmer would (the sentinel sets the flag).
+__global__ void __launch_bounds__(IBLOCK)
+k_preload_merge(const PreEnt* __restrict__ e, uint64_t n, TableView T, unsigned* __restrict__ flags) {
+  unsigned created = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t x = e[i].key;
+    if (x == SENTINEL) { atomicOr(flags, 1u); continue; }
+    oriented_or(T, 0, x, e[i].mask & MASK12, flags, created);
+  }
+  block_count(created, flags);
+}
+
+void merge_preload(Ctx& c, unsigned* flags) {
+  if (!c.n_preload) return;
+  hipLaunchKernelGGL(k_preload_merge, dim3(grid_for(c.n_preload, IBLOCK, 4096)), dim3(IBLOCK), 0, c.stream,
+                     c.preload.as<PreEnt>(), c.n_preload, c.tv, flags);
+  PG_HIP(hipGetLastError());
+}
+
 // ---- table scans.  Entry index space: [0, 2*buckets) primary words, then
 // [2*buckets, 2*buckets + ovf) overflow slots.
 
-__device__ __forceinline__ uint32_t entry_mask(const TableView& T, uint64_t nw, uint64_t i) {
-  if (i < nw) {
-    const unsigned long long w = T.prim[i];
-    return w ? (uint32_t)(w & MW_MASK) : 0u;
-  }
-  const Slot s = T.ovf[i - nw];
-  return s.key1 ? s.mask : 0u;
-}
-__device__ __forceinline__ uint64_t entry_key(const TableView& T, uint64_t nw, uint64_t i) {
-  if (i < nw) return T.key_of(i >> 1, T.prim[i]);
-  return T.ovf[i - nw].key1 - 1ull;
-}
 
 // K5: degree scan.  The table is swept as 16-byte elements (a primary bucket
 // = two words, or one overflow slot), RU per thread per 16 KiB unit, with
@@ -975,11 +966,15 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
       c.windows_fw += n > c.k ? (uint64_t)(n - c.k + 1) : 1;
     }
   c.windows_total = c.windows_fw * (rc0 ? 2 : 1);
+  c.last_flag = flag;
+  c.last_extra = extra_empty;
+  c.dump_ready = false;
   const int mode = k3_mode(c, flag);
   const uint64_t ntiles = mode ? make_group_tiles(c, flag) : make_tiles(c, flag);
   // expected canonical keys: learned from the previous build, else an upper
-  // bound (every forward window distinct); an overflow rebuilds larger
-  uint64_t keys = c.cap_hint ? c.cap_hint : std::max<uint64_t>(1024, c.windows_fw);
+  // bound (every forward window distinct, plus the staged npz slots); an
+  // overflow rebuilds larger
+  uint64_t keys = c.cap_hint ? c.cap_hint : std::max<uint64_t>(1024, c.windows_fw + c.n_preload);
   const uint64_t shift = pow5(c.k - 1);
   // PG_K3_DBG (development only): 1 = windows only, 2 = HBM loads without
   // updates, 4 = group form without its HBM phase; PG_K3_KEYS fixes the table
@@ -1003,6 +998,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
       PG_HIP(hipGetLastError());
     }
     if (extra_empty) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, flags);
+    merge_preload(c, flags);
     unsigned sentinel = 0, overflow = 0;
     uint64_t created = 0;
     read_flags(c, sentinel, overflow, created);

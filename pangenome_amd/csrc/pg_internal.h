@@ -123,6 +123,15 @@ struct Ctx {
   uint64_t n_rows = 0;
   std::vector<int64_t> h_rows;    // rec, start, end, strand, label
 
+  // ---- npz persistence (pg_persist.hip)
+  DevBuf preload;                 // staged PreEnt pairs, OR-merged by every build
+  uint64_t n_preload = 0;
+  std::vector<uint8_t> last_flag; // record flags / extra empties / strands of the last build
+  int last_extra = 0;
+  DevBuf dump_cnt;                // uint32 occurrence count per (entry, orientation) of the last build
+  bool dump_ready = false;
+  uint64_t dump_size = 0, dump_sentinel = 0;
+
   // timings of the last calls (ms, HIP events on `stream`)
   Timer t0, t1;
   double ms_parse = 0, ms_clear = 0, ms_insert = 0, ms_short = 0, ms_scan = 0;
@@ -140,6 +149,15 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap);
 uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap);
 uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts);
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel);
+void merge_preload(Ctx& c, unsigned* flags);
+// pg_persist.hip
+struct PreEnt {                   // one staged oakht slot: oriented key, 12-bit mask, count
+  unsigned long long key;
+  uint32_t mask, count;
+};
+void dbg_load(Ctx& c, const uint64_t* keys, const uint16_t* masks, const uint8_t* counts, uint64_t n);
+uint64_t dbg_dump(Ctx& c, uint64_t& capacity, uint64_t* keys, uint16_t* values, uint8_t* counts);
+uint64_t oakht_capacity(uint64_t size);
 // pg_walk.hip
 uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1);
 void export_edges(Ctx& c, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap);

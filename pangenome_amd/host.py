@@ -91,14 +91,16 @@ def _resumed_records(pos: int, R: int, shape: FileShape):
     return []
 
 
-def plan_dbg(seq_len: np.ndarray, shape: FileShape, rc0: bool, Ns: int, chunk: int = CHUNK):
+def plan_dbg(seq_len: np.ndarray, shape: FileShape, rc0: bool, Ns: int, chunk: int = CHUNK,
+             resume: int | None = None):
     """seq2rdbg (:1251-1266) over seq2dbg_jit_ (:1204-1230): which records the
-    dBG pass inserts, and how many extra empty records it meets."""
+    dBG pass inserts, and how many extra empty records it meets.  `resume`
+    is the record a -r checkpoint restarts at (resume_position)."""
     R = seq_len.shape[0]
     flags = np.zeros(R, np.uint8)
     extra = 0
     mult = 2 if rc0 else 1
-    recs = list(range(R))
+    recs = list(range(R)) if not resume else _resumed_records(resume, R, shape)
     N = 0
     while True:
         Nl = chk = 0
@@ -242,3 +244,43 @@ def format_rows(rows: np.ndarray, buf, hdr_start: np.ndarray, hdr_len: np.ndarra
             q = names[r] = bytes(buf[hs:hs + hl]).decode()[1:]
         out.append("%s\t%d\t%d\t%s\t%d" % (q, s, e, "+" if strand == 1 else "-", lab))
     return out
+
+
+# ------------------------------------------------------------ npz side files
+DB_LOAD = 750000000            # int(0.75 * 1e9): oakht's load factor as dump() stores it (:252)
+
+
+def write_db_npz(fn: str, capacity: int, size: int, keys, values, counts, offset: int = 0):
+    """dump() for an oakht (:243-261): parameters [capacity, load * 1e9, size,
+    ksize, vsize, offset] and the keys / values / counts slot arrays."""
+    fn = fn[:-4] if fn.endswith(".npz") else fn
+    params = np.asarray([capacity, DB_LOAD, size, 1, 1, offset], dtype=np.uint64)
+    np.savez_compressed(fn, parameters=params, keys=keys, values=values, counts=counts)
+
+
+def read_db_npz(fn: str):
+    """load_on_disk (:289-335) of an oakht dump: (offset, keys, values, counts)
+    of the occupied (counts > 0) slots, the entries iteritems yields (:623-631).
+    The file is read with numpy's non-pickling loader."""
+    with np.load(fn, allow_pickle=False) as z:
+        params = np.asarray(z["parameters"])
+        if params.shape[0] != 6:
+            raise ValueError("%s: not an oakht dump (parameters %r)" % (fn, params.tolist()))
+        if int(params[3]) != 1 or int(params[4]) != 1:
+            raise ValueError("%s: ksize/vsize %d/%d, the dBG uses 1/1" % (fn, int(params[3]), int(params[4])))
+        counts = np.asarray(z["counts"])
+        sel = counts > 0
+        keys = np.asarray(z["keys"])[sel].astype(np.uint64)
+        values = np.asarray(z["values"])[sel].astype(np.uint16)
+        return int(params[5]), keys, values, np.minimum(counts[sel], 255).astype(np.uint8)
+
+
+def resume_position(offset: int, rec_ptr: np.ndarray) -> int:
+    """The record a checkpoint's `offset` (seqio's ptr when record r was
+    yielded, :1255-1259) restarts at: r + 1.  Offset 0 is a fresh start."""
+    if offset == 0:
+        return 0
+    hit = np.flatnonzero(rec_ptr == offset)
+    if hit.shape[0] == 0:
+        raise ValueError("checkpoint offset %d is not a record boundary of this input" % offset)
+    return int(hit[0]) + 1

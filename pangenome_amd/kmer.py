@@ -8,7 +8,8 @@ runs in libpangenome_hip.so on an MI355X (pangenome_amd/csrc).  Mirrors:
   seq2rdbg     :1234-1268                dBG build (K1 parse + K3 insert)
   dbg2rdbg     :1313-1321                rdBG (K5 degree scan + compaction)
   seq2graph    :1853-1951                edges -> .xyz -> mcl -> labels -> rows
-  entry_point  :1971-2146                CLI (-i -k -n -c -r -d -R -D)
+  dump / load_on_disk  :243-335         `<in>_db.npz` (oakht slot layout)
+  entry_point  :1971-2146                CLI (-i -k -n -c -r -d -D; -R not yet)
 
 Usage:  python -m pangenome_amd -i genomes.fa -k 27 > result.tab
 """
@@ -54,6 +55,7 @@ class DeviceGraph:
         self.ctx.parse()
         rec = self.ctx.records()
         self.seq_len, self.hdr_start, self.hdr_len = rec["seq_len"], rec["hdr_start"], rec["hdr_len"]
+        self.rec_ptr = rec["ptr"]
         self.shape = host.FileShape.from_bytes(self.buf, self.hdr_start, self.hdr_len)
         self.stats = None
         self.reduced = False
@@ -73,15 +75,38 @@ class DeviceGraph:
 # ------------------------------------------------------------------- passes
 def seq2rdbg(qry, kmer=13, bits=5, Ns=1e6, chunk=2 ** 32, brkpt="./breakpoint", saved="dBG_disk",
              hashfunc=None, jit=True, rc=True, device=0):
-    """:1234-1268.  Returns the device dBG."""
-    if brkpt and os.path.isfile(brkpt):
-        raise NotImplementedError("resuming a dBG checkpoint (-r) is not supported by the GPU build")
+    """:1234-1268.  Returns the device dBG.  An existing `brkpt` npz (-r) is
+    the table so far plus the offset to resume at (:1239-1241); the GPU build
+    does not write `<in>_db_brkpt.npz` checkpoints itself (inputs > 2^33 bases)."""
     if seq_chk(qry) != "fasta":
         raise ValueError("%s: only FASTA input is supported (the reference's FASTQ branch is "
                          "broken, kmer_numba.py:174-186)" % qry)
     g = DeviceGraph(qry, kmer, device)
-    flags, extra = host.plan_dbg(g.seq_len, g.shape, bool(rc), int(Ns), int(chunk))
+    resume = None
+    if brkpt and os.path.isfile(brkpt):
+        offset, keys, values, counts = host.read_db_npz(brkpt)
+        g.ctx.dbg_load(keys, values, counts)
+        resume = host.resume_position(offset, g.rec_ptr)
+    flags, extra = host.plan_dbg(g.seq_len, g.shape, bool(rc), int(Ns), int(chunk), resume=resume)
     g.stats = g.ctx.build_dbg(flags, extra, bool(rc))
+    return g
+
+
+def dump(g: DeviceGraph, fn="./tmp"):
+    """:243-261 — `fn`.npz as an oakht the reference's load_on_disk accepts."""
+    cap, size, keys, values, counts = g.ctx.dbg_dump()
+    host.write_db_npz(fn, cap, size, keys, values, counts)
+    return 0
+
+
+def load_graph(qry, kmer, fn, device=0, rdbg=False, rc=True):
+    """load_on_disk (:289-335) into a device graph over `qry`: -d (a dBG,
+    reduced next) or -D (rdBG keys: staged with mask 0, so every key passes
+    the rdBG rule and membership is exactly the file's key set)."""
+    _, keys, values, counts = host.read_db_npz(fn)
+    g = DeviceGraph(qry, kmer, device)
+    g.ctx.dbg_load(keys, None if rdbg else values, counts)
+    g.stats = g.ctx.build_dbg(np.zeros(g.seq_len.shape[0], np.uint8), 0, bool(rc))
     return g
 
 
@@ -165,12 +190,32 @@ def entry_point(argv, out=None, device=0):
         manual_print(out)
         raise SystemExit()
     chunk = 2 ** 33
-    if dbs or rdb:
-        raise NotImplementedError("-d/-D (loading an npz dBG/rdBG) is not supported by the GPU build yet")
+    if rbk and os.path.isfile(rbk):
+        raise NotImplementedError("resuming an edge checkpoint (-R) is not supported by the GPU build")
+    rc0, rc1 = (rc >> 1) == 1, (rc & 1) == 1
+    if dbs or rdb:                                    # :2073-2101
+        if not rdb:
+            print("load dBG from disk", file=out)
+            kmer_dict = load_graph(qry, kmer, dbs, device, rdbg=False, rc=rc0)
+            print("# build the reduced dBG", file=out)
+            rdbg_dict = dbg2rdbg(kmer_dict)
+        else:
+            rdbg_dict = dbg2rdbg(load_graph(qry, kmer, rdb, device, rdbg=True, rc=rc0))
+        print("# find fr", file=out)
+        seq2graph(qry, kmer=kmer, bits=5, Ns=Ns, rdbg_dict=rdbg_dict, chunk=chunk, brkpt=rbk, rc=rc1, out=out)
+        return 0
     print("# build the dBG", file=out)
     st = time()
-    rc0 = (rc >> 1) == 1
     kmer_dict = seq2rdbg(qry, kmer, 5, Ns, brkpt=bkt, chunk=chunk, rc=rc0, device=device)
+    print("# finished in", time() - st, "seconds", file=out)
+    print("# save dBG to disk", file=out)
+    st = time()
+    dump(kmer_dict, qry + "_db")
+    print("# finished in", time() - st, "seconds", file=out)
+    # the reference reloads the file it just wrote (:2120-2126); the device
+    # table is that same dBG, so nothing is read back
+    print("# load dBG from disk", file=out)
+    st = time()
     print("# finished in", time() - st, "seconds", file=out)
     print("# build the reduced dBG", file=out)
     st = time()
@@ -178,7 +223,6 @@ def entry_point(argv, out=None, device=0):
     print("# finished in", time() - st, "seconds", file=out)
     print("# find fr", file=out)
     st = time()
-    rc1 = (rc & 1) == 1
     seq2graph(qry, kmer=kmer, bits=5, Ns=Ns, rdbg_dict=rdbg_dict, chunk=chunk, brkpt=rbk, rc=rc1, out=out)
     print("# finished in", time() - st, "seconds", file=out)
     return 0

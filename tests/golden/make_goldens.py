@@ -187,6 +187,8 @@ def run_fixture(K, name, input_name, fasta: bytes, k, c=2, n=None, mcl=None, chu
     cnt = db["counts"]
     keys = db["keys"][cnt > 0].astype(np.uint64)
     masks = db["values"][cnt > 0].astype(np.uint16)
+    counts = cnt[cnt > 0].astype(np.uint8)          # the reference's own dump (:243-261)
+    params = db["parameters"].astype(np.uint64)
     o = np.argsort(keys, kind="stable")
     rdbg = np.sort(captured["rdbg"])
 
@@ -197,8 +199,10 @@ def run_fixture(K, name, input_name, fasta: bytes, k, c=2, n=None, mcl=None, chu
         g = np.load(gpath)
         assert np.array_equal(g["dbg_keys"], keys[o]) and np.array_equal(g["dbg_masks"], masks[o])
         assert np.array_equal(g["rdbg_keys"], rdbg)
+        assert np.array_equal(g["dbg_counts"], counts[o]) and np.array_equal(g["db_params"], params)
     else:
-        np.savez_compressed(gpath, dbg_keys=keys[o], dbg_masks=masks[o], rdbg_keys=rdbg)
+        np.savez_compressed(gpath, dbg_keys=keys[o], dbg_masks=masks[o], rdbg_keys=rdbg,
+                            dbg_counts=counts[o], db_params=params)
     with open(qry + "_rdbg_weight.xyz", "rb") as f, \
             gzip.GzipFile(os.path.join(out_dir, "rdbg_weight.xyz.gz"), "wb", mtime=0) as g:
         g.write(f.read())

@@ -22,6 +22,9 @@ class Fixture:
         self.fasta = open(self.input_path, "rb").read()
         g = np.load(os.path.join(GOLDEN, "graphs", self.meta["graph"]))
         self.dbg_keys, self.dbg_masks, self.rdbg_keys = g["dbg_keys"], g["dbg_masks"], g["rdbg_keys"]
+        # the reference's own `<in>_db.npz` (:243-261): occurrence counts per key
+        # (sorted like dbg_keys) and its parameters row
+        self.dbg_counts, self.db_params = g["dbg_counts"], g["db_params"]
         self.xyz = gzip.open(os.path.join(self.dir, "rdbg_weight.xyz.gz")).read().decode()
         self.rows = gzip.open(os.path.join(self.dir, "rows.tsv.gz")).read().decode().split("\n")[:-1]
         mp = os.path.join(self.dir, "input.mcl")

@@ -11,7 +11,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_symbols():
     text = open(os.path.join(ROOT, "include", "pangenome.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(pg_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|uint64_t|const char\*)\s+(pg_\w+)\s*\(", text, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
@@ -94,3 +94,43 @@ def test_label_dict_matches_oracle(oracle_mod):
     a = host.label_dict(mcl, xyz.splitlines(keepends=True))
     k, v, i = oracle_mod.label_table(xyz, mcl)
     assert a == {(int(x), int(y)): int(z) for x, y, z in zip(k, v, i)}
+
+
+def test_oakht_capacity_chain_matches_oracle(oracle_mod):
+    """pg_oakht_capacity (host-only) against the oracle's faithful oakht growth
+    (find_prime(2^20), x1.62 at load 0.75, kmer_numba.py:423-474) at sizes on
+    both sides of the first two resizes."""
+    from pangenome_amd import _lib, synth
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.pg_oakht_capacity.restype = ctypes.c_uint64
+    lib.pg_oakht_capacity.argtypes = [ctypes.c_uint64]
+    assert lib.pg_oakht_capacity(0) == 1048583
+    assert lib.pg_oakht_capacity(786437) == 1048583        # 0.75 * 1048583 = 786437.25
+    assert lib.pg_oakht_capacity(786438) > 1048583
+    for n_bases in (380_000, 420_000, 700_000):
+        fa = synth.to_fasta_lines(b"g", synth.base_genome(n_bases, seed=n_bases))
+        run = oracle_mod.OracleRun(fa, 27, 2)
+        keys, _ = run.dbg()
+        assert lib.pg_oakht_capacity(keys.shape[0]) == run.dbg_capacity()
+
+
+def test_db_npz_roundtrip(tmp_path):
+    """write_db_npz / read_db_npz: dump()'s parameters row and slot arrays
+    (:243-261); only counts > 0 slots come back (iteritems :623-631)."""
+    from pangenome_amd import host
+    keys = np.array([0, 5, 0, 2 ** 64 - 1, 9], np.uint64)
+    vals = np.array([0, 3, 0, 32, 65], np.uint16)
+    cnts = np.array([0, 2, 0, 1, 255], np.uint8)
+    host.write_db_npz(str(tmp_path / "x_db"), 5, 3, keys, vals, cnts, offset=77)
+    z = np.load(str(tmp_path / "x_db.npz"))
+    assert z["parameters"].tolist() == [5, 750000000, 3, 1, 1, 77]
+    off, k, v, c = host.read_db_npz(str(tmp_path / "x_db.npz"))
+    assert off == 77 and k.tolist() == [5, 2 ** 64 - 1, 9] and v.tolist() == [3, 32, 65] and c.tolist() == [2, 1, 255]
+    np.savez_compressed(str(tmp_path / "edges"), parameters=np.array([4, 1, 0], np.uint64),
+                        keys=np.zeros(8, np.uint64), values=np.zeros(2, np.int64))
+    with pytest.raises(ValueError):
+        host.read_db_npz(str(tmp_path / "edges.npz"))
+    assert host.resume_position(0, np.array([10, 20])) == 0
+    assert host.resume_position(20, np.array([10, 20])) == 2
+    with pytest.raises(ValueError):
+        host.resume_position(15, np.array([10, 20]))

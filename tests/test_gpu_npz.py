@@ -1,0 +1,161 @@
+"""npz persistence (dump / load_on_disk, kmer_numba.py:243-335) on the GPU.
+
+The dumped `<in>_db.npz` is compared with the dump the reference itself wrote
+for every golden fixture (its keys / values / counts slots, capacity and
+size, tests/golden/graphs/*), and its slot layout is checked with a
+restatement of oakht.pointer (:521-538): every key is found by the probe walk
+a reference lookup does.  -d, -D and -r then reproduce the reference's region
+rows from those files.
+"""
+import io
+import os
+
+import numpy as np
+import pytest
+
+from golden_util import Fixture, fixture_names
+
+pytestmark = pytest.mark.gpu
+M64 = (1 << 64) - 1
+
+
+def oak_fnv(x):
+    a = 0xCBF29CE484222325
+    for i in range(4):
+        a ^= (x >> (8 * i)) & 0xFF
+        a = (a * 0x100000001B3) & M64
+    return a
+
+
+def oak_slot(keys, counts, x):
+    """oakht.pointer (:521-538): j, j, j+1, j+4, ... until the key or an empty slot."""
+    M = keys.shape[0]
+    j0 = oak_fnv(x) % M
+    j = j0
+    for k in range(M):
+        if int(keys[j]) == x or counts[j] == 0:
+            break
+        j = (j0 + k * k) % M
+    return j
+
+
+def oak_place(keys_in, vals_in, cnts_in, M):
+    """A valid oakht layout built the way __setitem__ does (test helper)."""
+    keys = np.zeros(M, np.uint64)
+    vals = np.zeros(M, np.uint16)
+    cnts = np.zeros(M, np.uint8)
+    for x, v, c in zip(keys_in.tolist(), vals_in.tolist(), cnts_in.tolist()):
+        j = oak_slot(keys, cnts, x)
+        keys[j], vals[j], cnts[j] = x, v, c
+    return keys, vals, cnts
+
+
+def rows_of(text):
+    return [ln for ln in text.split("\n") if len(ln.split("\t")) == 5 and ln.split("\t")[3] in ("+", "-")]
+
+
+def _graph_fixtures():
+    seen, out = set(), []
+    for n in fixture_names():
+        g = Fixture(n).meta["graph"]
+        if g not in seen:
+            seen.add(g)
+            out.append(n)
+    return out
+
+
+@pytest.mark.parametrize("name", _graph_fixtures())
+def test_dump_matches_reference_dump(name, tmp_path):
+    from pangenome_amd import host, kmer
+    fx = Fixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    Ns = fx.ns if fx.ns is not None else 2 ** 63
+    g = kmer.seq2rdbg(str(q), fx.k, 5, Ns, brkpt="", chunk=2 ** 33, rc=(fx.c >> 1) == 1)
+    kmer.dump(g, str(q) + "_db")
+    z = np.load(str(q) + "_db.npz")
+    params = z["parameters"]
+    assert params.tolist() == fx.db_params.tolist()          # capacity, load, size, ksize, vsize, offset
+    keys, vals, cnts = z["keys"], z["values"], z["counts"]
+    assert keys.dtype == np.uint64 and vals.dtype == np.uint16 and cnts.dtype == np.uint8
+    sel = cnts > 0
+    o = np.argsort(keys[sel], kind="stable")
+    assert np.array_equal(keys[sel][o], fx.dbg_keys)
+    assert np.array_equal(vals[sel][o], fx.dbg_masks)
+    assert np.array_equal(cnts[sel][o], fx.dbg_counts)
+    # the layout: every key sits where oakht.pointer looks for it
+    idx = np.flatnonzero(sel)
+    sample = idx if idx.shape[0] <= 20000 else idx[np.random.default_rng(0).choice(idx.shape[0], 20000, False)]
+    for j in sample.tolist():
+        assert oak_slot(keys, cnts, int(keys[j])) == j
+    off, k2, v2, c2 = host.read_db_npz(str(q) + "_db.npz")
+    assert off == 0 and k2.shape[0] == int(params[2])
+
+
+def _run_cli(argv):
+    from pangenome_amd import kmer
+    out = io.StringIO()
+    kmer.entry_point(argv, out=out)
+    return out.getvalue()
+
+
+def test_cli_writes_db_npz_and_d_reloads_it(tmp_path):
+    fx = Fixture("pan8_k27_c3")
+    q = tmp_path / "in.fa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "in.fa_rdbg_weight.xyz.mcl").write_text("")
+    text = _run_cli(["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "3"])
+    assert "# save dBG to disk" in text and rows_of(text) == fx.rows
+    db = str(q) + "_db.npz"
+    assert os.path.isfile(db)
+    text = _run_cli(["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "3", "-d", db])
+    assert "load dBG from disk" in text.split("\n")
+    assert rows_of(text) == fx.rows
+
+
+def test_cli_D_loads_an_rdbg(tmp_path):
+    """-D: rdBG keys in an oakht file (values are not consulted, :1538 has_key)."""
+    fx = Fixture("pan8_k27_c1")
+    q = tmp_path / "in.fa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "in.fa_rdbg_weight.xyz.mcl").write_text("")
+    from pangenome_amd import host
+    keys = fx.rdbg_keys
+    M = 1048583
+    kk, vv, cc = oak_place(keys, np.full(keys.shape[0], 7, np.uint16), np.ones(keys.shape[0], np.uint8), M)
+    host.write_db_npz(str(tmp_path / "rdbg"), M, keys.shape[0], kk, vv, cc)
+    text = _run_cli(["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "1", "-D", str(tmp_path / "rdbg.npz")])
+    assert rows_of(text) == fx.rows
+
+
+def test_cli_r_resumes_a_checkpoint(tmp_path):
+    """-r: the dBG of records 0..3 with the offset seqio reports after record 3
+    (:1255-1259); resuming inserts records 4.. and ends at the full dBG, counts
+    included, and the reference's rows."""
+    from pangenome_amd import host, kmer
+    from pangenome_amd._lib import Context
+    fx = Fixture("pan8_k27_c3")
+    q = tmp_path / "in.fa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "in.fa_rdbg_weight.xyz.mcl").write_text("")
+    ctx = Context(27)
+    ctx.set_fasta(np.frombuffer(fx.fasta, np.uint8))
+    R, _ = ctx.parse()
+    ptr = ctx.records()["ptr"]
+    flags = np.zeros(R, np.uint8)
+    flags[:4] = 1
+    ctx.build_dbg(flags, 0, True)
+    cap, size, keys, vals, cnts = ctx.dbg_dump()
+    ctx.close()
+    brk = str(tmp_path / "in.fa_db_brkpt")
+    host.write_db_npz(brk, cap, size, keys, vals, cnts, offset=int(ptr[3]))
+    g = kmer.seq2rdbg(str(q), 27, 5, 2 ** 63, brkpt=brk + ".npz", chunk=2 ** 33, rc=True)
+    kmer.dump(g, str(tmp_path / "resumed"))
+    z = np.load(str(tmp_path / "resumed.npz"))
+    sel = z["counts"] > 0
+    o = np.argsort(z["keys"][sel], kind="stable")
+    assert np.array_equal(z["keys"][sel][o], fx.dbg_keys)
+    assert np.array_equal(z["values"][sel][o], fx.dbg_masks)
+    assert np.array_equal(z["counts"][sel][o], fx.dbg_counts)
+    text = _run_cli(["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "3", "-r", brk + ".npz"])
+    assert rows_of(text) == fx.rows

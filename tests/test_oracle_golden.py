@@ -21,6 +21,19 @@ def test_oracle_matches_reference(oracle_mod, name):
     assert out["rows"] == fx.rows
 
 
+@pytest.mark.parametrize("name", fixture_names())
+def test_oracle_counts_match_reference_dump(oracle_mod, name):
+    """The oakht occurrence counts and capacity the reference wrote to
+    `<in>_db.npz` (:243-261)."""
+    fx = Fixture(name)
+    run = oracle_mod.OracleRun(fx.fasta, fx.k, fx.c, fx.ns)
+    keys, masks, counts = run.dbg_counts()
+    assert np.array_equal(keys, fx.dbg_keys)
+    assert np.array_equal(counts, fx.dbg_counts)
+    assert run.dbg_capacity() == int(fx.db_params[0])
+    assert int(fx.db_params[2]) == keys.shape[0]
+
+
 def test_label_table_order(oracle_mod):
     # .mcl line index first, then unseen .xyz nodes (kmer_numba.py:1918-1944)
     xyz = "1_2\t3_4\t1\n3_4\t5_6\t2\n7_8\t1_2\t1\n"
