@@ -127,13 +127,14 @@ def plan_dbg(seq_len: np.ndarray, shape: FileShape, rc0: bool, Ns: int, chunk: i
     return flags, extra
 
 
-def plan_edges(seq_len: np.ndarray, shape: FileShape, Ns: int, chunk: int = CHUNK):
+def plan_edges(seq_len: np.ndarray, shape: FileShape, Ns: int, chunk: int = CHUNK, resume: int | None = None):
     """seq2graph (:1876-1890) over rdbg_edge_weight_jit_ (:1809-1827): walked
-    records and, per record, the checkpoint segment it belongs to."""
+    records and, per record, the checkpoint segment it belongs to.  `resume`
+    is the record a -R checkpoint restarts at (resume_position)."""
     R = seq_len.shape[0]
     flags = np.zeros(R, np.uint8)
     segment = np.full(R, -1, np.int64)
-    recs = list(range(R))
+    recs = list(range(R)) if not resume else _resumed_records(resume, R, shape)
     N = 0
     seg = 0
     n_checkpoints = 0
@@ -284,3 +285,38 @@ def resume_position(offset: int, rec_ptr: np.ndarray) -> int:
     if hit.shape[0] == 0:
         raise ValueError("checkpoint offset %d is not a record boundary of this input" % offset)
     return int(hit[0]) + 1
+
+
+def read_edge_npz(fn: str):
+    """load_on_disk(jit=True) (:305-309) of an edge checkpoint: (offset,
+    tuples[N, 4] uint64, counts[N]) in file order — array2dict's insertion
+    order (:264-286)."""
+    with np.load(fn, allow_pickle=False) as z:
+        params = np.asarray(z["parameters"])
+        if params.shape[0] != 3 or int(params[0]) != 4 or int(params[1]) != 1:
+            raise ValueError("%s: not an edge checkpoint (parameters %r)" % (fn, params.tolist()))
+        keys = np.asarray(z["keys"]).astype(np.uint64)
+        values = np.asarray(z["values"])
+        n = min(keys.shape[0] // 4, values.shape[0])
+        return int(params[2]), keys[:4 * n].reshape(n, 4), values[:n].astype(np.int64)
+
+
+def merge_edges(loaded_t, loaded_c, tuples, counts, walk_first, segment_of_record, n_checkpoints):
+    """The edge Dict of a resumed seq2graph (:1859-1887): the loaded items in
+    file order, then the walks' edges by first occurrence — a known edge adds
+    its walk count in place, a new one is appended — and the whole Dict
+    reversed at every further checkpoint dump/reload."""
+    d = {}
+    for t, c in zip(map(tuple, loaded_t.tolist()), loaded_c.tolist()):
+        d[t] = c
+    seg = segment_of_record[walk_first // 2] if walk_first.shape[0] else np.zeros(0, np.int64)
+    tl, cl = tuples.tolist(), counts.tolist()
+    for s in range(n_checkpoints + 1):
+        for i in np.flatnonzero(seg == s).tolist():
+            t = tuple(tl[i])
+            d[t] = d.get(t, 0) + cl[i]
+        if s < n_checkpoints:
+            d = dict(reversed(list(d.items())))
+    out_t = np.array(list(d.keys()), dtype=np.uint64).reshape(-1, 4)
+    out_c = np.array(list(d.values()), dtype=np.int64)
+    return out_t, out_c

@@ -9,7 +9,7 @@ runs in libpangenome_hip.so on an MI355X (pangenome_amd/csrc).  Mirrors:
   dbg2rdbg     :1313-1321                rdBG (K5 degree scan + compaction)
   seq2graph    :1853-1951                edges -> .xyz -> mcl -> labels -> rows
   dump / load_on_disk  :243-335         `<in>_db.npz` (oakht slot layout)
-  entry_point  :1971-2146                CLI (-i -k -n -c -r -d -D; -R not yet)
+  entry_point  :1971-2146                CLI (-i -k -n -c -r -d -R -D)
 
 Usage:  python -m pangenome_amd -i genomes.fa -k 27 > result.tab
 """
@@ -76,8 +76,9 @@ class DeviceGraph:
 def seq2rdbg(qry, kmer=13, bits=5, Ns=1e6, chunk=2 ** 32, brkpt="./breakpoint", saved="dBG_disk",
              hashfunc=None, jit=True, rc=True, device=0):
     """:1234-1268.  Returns the device dBG.  An existing `brkpt` npz (-r) is
-    the table so far plus the offset to resume at (:1239-1241); the GPU build
-    does not write `<in>_db_brkpt.npz` checkpoints itself (inputs > 2^33 bases)."""
+    the table so far plus the offset to resume at (:1239-1241).  The GPU
+    build does not write `<in>_db_brkpt.npz` / `<in>_rdb_brkpt.npz`
+    checkpoints itself (they appear past 2^33 bases); it reads both."""
     if seq_chk(qry) != "fasta":
         raise ValueError("%s: only FASTA input is supported (the reference's FASTQ branch is "
                          "broken, kmer_numba.py:174-186)" % qry)
@@ -117,10 +118,17 @@ def dbg2rdbg(kmer_dict):
     return kmer_dict
 
 
-def rdbg_edges(g: DeviceGraph, Ns, chunk, rc):
-    """Edge Dict of rdbg_edge_weight_jit_ (:1808-1827) in its iteration order."""
-    flags, segment, ncp = host.plan_edges(g.seq_len, g.shape, int(Ns), int(chunk))
+def rdbg_edges(g: DeviceGraph, Ns, chunk, rc, brkpt=""):
+    """Edge Dict of rdbg_edge_weight_jit_ (:1808-1827) in its iteration order;
+    an existing `brkpt` (-R) is the Dict so far and the offset to resume at."""
+    loaded, resume = None, None
+    if brkpt and os.path.isfile(brkpt):
+        offset, lt, lc = host.read_edge_npz(brkpt)
+        loaded, resume = (lt, lc), host.resume_position(offset, g.rec_ptr)
+    flags, segment, ncp = host.plan_edges(g.seq_len, g.shape, int(Ns), int(chunk), resume=resume)
     tuples, counts, walk_first = g.ctx.edges(flags, bool(rc))
+    if loaded is not None:
+        return host.merge_edges(loaded[0], loaded[1], tuples, counts, walk_first, segment, ncp)
     order = host.edge_order(walk_first, segment, ncp)
     return tuples[order], counts[order]
 
@@ -130,10 +138,8 @@ def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_
     """:1853-1951: edge weights -> `<qry>_rdbg_weight.xyz` -> mcl (or reuse)
     -> label dictionary -> print the region rows."""
     out = out or sys.stdout
-    if brkpt and os.path.isfile(brkpt):
-        raise NotImplementedError("resuming an edge checkpoint (-R) is not supported by the GPU build")
     g = rdbg_dict
-    tuples, counts = rdbg_edges(g, Ns, chunk, rc)
+    tuples, counts = rdbg_edges(g, Ns, chunk, rc, brkpt=brkpt)
     oname = qry + "_rdbg_weight.xyz"
     xyz = host.xyz_text(tuples, counts)
     with open(oname, "w") as f:
@@ -190,8 +196,6 @@ def entry_point(argv, out=None, device=0):
         manual_print(out)
         raise SystemExit()
     chunk = 2 ** 33
-    if rbk and os.path.isfile(rbk):
-        raise NotImplementedError("resuming an edge checkpoint (-R) is not supported by the GPU build")
     rc0, rc1 = (rc >> 1) == 1, (rc & 1) == 1
     if dbs or rdb:                                    # :2073-2101
         if not rdb:

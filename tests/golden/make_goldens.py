@@ -224,6 +224,64 @@ def run_fixture(K, name, input_name, fasta: bytes, k, c=2, n=None, mcl=None, chu
     return meta
 
 
+def run_resume_fixture(K, name, input_name, fasta: bytes, k, c, flag, chunk):
+    """A checkpoint written by the reference itself, then its CLI resuming from
+    it: flag "-r" (seq2rdbg's `<in>_db_brkpt.npz`, :1255-1259) or "-R"
+    (seq2graph's `<in>_rdb_brkpt.npz`, :1880-1887).  Stored under resume/."""
+    out_dir = os.path.join(HERE, "resume", name)
+    os.makedirs(out_dir)
+    work = tempfile.mkdtemp(prefix="pg_gold_")
+    qry = os.path.join(work, "input.fsa")
+    with open(qry, "wb") as f:
+        f.write(fasta)
+    with open(qry + "_rdbg_weight.xyz.mcl", "w") as f:
+        f.write("")
+    with contextlib.redirect_stdout(io.StringIO()):
+        if flag == "-r":
+            K.seq2rdbg(qry, k, 5, 2 ** 63, brkpt="", chunk=chunk, rc=(c >> 1) == 1)
+            brk = qry + "_db_brkpt.npz"
+        else:
+            kd = K.seq2rdbg(qry, k, 5, 2 ** 63, brkpt="", chunk=2 ** 33, rc=(c >> 1) == 1)
+            rd = K.dbg2rdbg(kd)
+            K.seq2graph(qry, kmer=k, bits=5, Ns=2 ** 63, rdbg_dict=rd, chunk=chunk, brkpt="", rc=(c & 1) == 1)
+            brk = qry + "_rdb_brkpt.npz"
+            os.remove(qry + "_rdbg_weight.xyz")
+    saved = os.path.join(out_dir, "brkpt.npz")
+    with np.load(brk) as z:                            # counts as numba writes them (uint8); the
+        arrs = {a: z[a] for a in z.files}              # shim widened them (emulation 4)
+    if "counts" in arrs:
+        assert arrs["counts"].max() <= 255
+        arrs["counts"] = arrs["counts"].astype(np.uint8)
+    np.savez_compressed(saved, **arrs)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        K.entry_point(["kmer_numba.py", "-i", qry, "-k", str(k), "-c", str(c), flag, saved])
+    rows = [ln for ln in buf.getvalue().split("\n")
+            if len(ln.split("\t")) == 5 and ln.split("\t")[3] in ("+", "-")]
+    with open(qry + "_rdbg_weight.xyz", "rb") as f, \
+            gzip.GzipFile(os.path.join(out_dir, "rdbg_weight.xyz.gz"), "wb", mtime=0) as g:
+        g.write(f.read())
+    with gzip.GzipFile(os.path.join(out_dir, "rows.tsv.gz"), "wb", mtime=0) as g:
+        g.write("".join(r + "\n" for r in rows).encode())
+    meta = dict(input=input_name + ".fsa", k=k, c=c, flag=flag, chunk=chunk, n_rows=len(rows),
+                generator="tests/golden/make_goldens.py (reference kmer_numba.py, pure-Python mode)")
+    if flag == "-r":                                   # the dBG the resumed run dumped: a graph file
+        db = np.load(qry + "_db.npz")
+        cnt = db["counts"]
+        keys = db["keys"][cnt > 0].astype(np.uint64)
+        o = np.argsort(keys, kind="stable")
+        graph = "%s_k%d_rc%d" % (input_name, k, c >> 1)
+        g = np.load(os.path.join(HERE, "graphs", graph + ".npz"))
+        assert np.array_equal(g["dbg_keys"], keys[o])
+        assert np.array_equal(g["dbg_masks"], db["values"][cnt > 0].astype(np.uint16)[o])
+        assert np.array_equal(g["dbg_counts"], cnt[cnt > 0].astype(np.uint8)[o])
+        meta["graph"] = graph + ".npz"
+    with open(os.path.join(out_dir, "meta.json"), "w") as f:
+        json.dump(meta, f, indent=1, sort_keys=True)
+    shutil.rmtree(work)
+    print("%-18s resume %s k=%d c=%d rows=%d" % (name, flag, k, c, len(rows)), file=sys.stderr)
+
+
 def edge_case_fasta() -> bytes:
     """Hand-built edge cases (no record of length k+1)."""
     from pangenome_amd import synth
@@ -323,6 +381,8 @@ def main():
         run_fixture(K, "pan8_k27_chunk", "pan8", pan, 27, c=3, chunk=30000)
         mcl = components_mcl_from(os.path.join(HERE, "pan8_k27_c3", "rdbg_weight.xyz.gz"))
         run_fixture(K, "pan8_k27_mcl", "pan8", pan, 27, c=3, mcl=mcl)
+        run_resume_fixture(K, "pan8_k27_r", "pan8", pan, 27, 3, "-r", 100000)
+        run_resume_fixture(K, "pan8_k27_R", "pan8", pan, 27, 3, "-R", 30000)
     finally:
         shutil.rmtree(shim, ignore_errors=True)
 

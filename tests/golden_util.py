@@ -33,3 +33,28 @@ class Fixture:
         n = self.meta["n"]
         self.ns = int(float(n)) if n is not None else None
         self.edge_chunk = self.meta["chunk"] or 2 ** 33
+
+
+def resume_names():
+    d = os.path.join(GOLDEN, "resume")
+    return sorted(x for x in os.listdir(d) if os.path.isfile(os.path.join(d, x, "meta.json"))) \
+        if os.path.isdir(d) else []
+
+
+class ResumeFixture:
+    """A checkpoint the reference wrote (brkpt.npz) and its CLI's output when
+    resuming from it with -r or -R (tests/golden/make_goldens.py)."""
+
+    def __init__(self, name):
+        self.name = name
+        self.dir = os.path.join(GOLDEN, "resume", name)
+        self.meta = json.load(open(os.path.join(self.dir, "meta.json")))
+        self.fasta = open(os.path.join(GOLDEN, "inputs", self.meta["input"]), "rb").read()
+        self.brkpt = os.path.join(self.dir, "brkpt.npz")
+        self.flag, self.k, self.c = self.meta["flag"], self.meta["k"], self.meta["c"]
+        self.xyz = gzip.open(os.path.join(self.dir, "rdbg_weight.xyz.gz")).read().decode()
+        self.rows = gzip.open(os.path.join(self.dir, "rows.tsv.gz")).read().decode().split("\n")[:-1]
+        self.graph = None
+        if "graph" in self.meta:
+            g = np.load(os.path.join(GOLDEN, "graphs", self.meta["graph"]))
+            self.graph = {k: g[k] for k in ("dbg_keys", "dbg_masks", "dbg_counts")}

@@ -134,3 +134,36 @@ def test_db_npz_roundtrip(tmp_path):
     assert host.resume_position(20, np.array([10, 20])) == 2
     with pytest.raises(ValueError):
         host.resume_position(15, np.array([10, 20]))
+
+
+def test_reference_checkpoint_files_parse():
+    """The checkpoints the reference wrote (tests/golden/resume) read back in
+    both layouts: oakht (-r) and the jit edge Dict (-R)."""
+    from golden_util import ResumeFixture, resume_names
+    from pangenome_amd import host
+    seen = set()
+    for name in resume_names():
+        fx = ResumeFixture(name)
+        if fx.flag == "-r":
+            off, k, v, c = host.read_db_npz(fx.brkpt)
+            assert off > 0 and k.shape[0] == v.shape[0] == c.shape[0] > 0 and c.min() >= 1
+        else:
+            off, t, c = host.read_edge_npz(fx.brkpt)
+            assert off > 0 and t.shape == (c.shape[0], 4) and c.min() >= 1
+        seen.add(fx.flag)
+    assert seen == {"-r", "-R"}
+
+
+def test_merge_edges_order():
+    """Resumed Dict: loaded items, known edges updated in place, new ones
+    appended, whole Dict reversed at a checkpoint (kmer_numba.py:1859-1887)."""
+    from pangenome_amd import host
+    lt = np.array([[1, 1, 2, 2], [3, 3, 4, 4]], np.uint64)
+    lc = np.array([5, 6], np.int64)
+    t = np.array([[3, 3, 4, 4], [7, 7, 8, 8], [9, 9, 9, 9]], np.uint64)
+    c = np.array([1, 1, 2], np.int64)
+    walk_first = np.array([0, 0, 2], np.int64)          # records 0, 0, 1
+    ot, oc = host.merge_edges(lt, lc, t, c, walk_first, np.array([0, 0], np.int64), 0)
+    assert ot[:, 0].tolist() == [1, 3, 7, 9] and oc.tolist() == [5, 7, 1, 2]
+    ot, oc = host.merge_edges(lt, lc, t, c, walk_first, np.array([0, 1], np.int64), 1)
+    assert ot[:, 0].tolist() == [7, 3, 1, 9] and oc.tolist() == [1, 7, 5, 2]

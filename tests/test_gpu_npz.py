@@ -159,3 +159,24 @@ def test_cli_r_resumes_a_checkpoint(tmp_path):
     assert np.array_equal(z["counts"][sel][o], fx.dbg_counts)
     text = _run_cli(["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "3", "-r", brk + ".npz"])
     assert rows_of(text) == fx.rows
+
+
+@pytest.mark.parametrize("name", __import__("golden_util").resume_names())
+def test_cli_resumes_reference_checkpoint(name, tmp_path):
+    """-r / -R from a checkpoint the reference wrote itself: same .xyz (edge
+    order included), rows and, for -r, the dumped dBG."""
+    from golden_util import ResumeFixture
+    fx = ResumeFixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    text = _run_cli(["kmer_numba.py", "-i", str(q), "-k", str(fx.k), "-c", str(fx.c), fx.flag, fx.brkpt])
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
+    assert rows_of(text) == fx.rows
+    if fx.graph is not None:
+        z = np.load(str(q) + "_db.npz")
+        sel = z["counts"] > 0
+        o = np.argsort(z["keys"][sel], kind="stable")
+        assert np.array_equal(z["keys"][sel][o], fx.graph["dbg_keys"])
+        assert np.array_equal(z["values"][sel][o], fx.graph["dbg_masks"])
+        assert np.array_equal(z["counts"][sel][o], fx.graph["dbg_counts"])
