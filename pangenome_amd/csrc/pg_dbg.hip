@@ -221,6 +221,43 @@ __device__ __forceinline__ void init_keys(const uint8_t* sc, uint32_t o, int k, 
   Kr = (uint64_t)rlo + rhi * 1220703125ull;
 }
 
+// ---- positional dedup against a reference record (see k_insert).  A window q
+// of record g with neither record end in it, whose bytes [q-1, q+k] equal the
+// reference's bytes [q'-1, q'+k] at q' = q - delta (q' interior too), has the
+// reference window's key and both masks (:1069-1080); the reference inserts
+// that window, so g's insert would OR nothing new and is skipped.  The drift
+// delta only decides how much is skipped, never what is inserted.
+constexpr int DRIFT = 512;                    // searched offsets: [-DRIFT, DRIFT]
+constexpr int RSPAN = TILE + 2 * DRIFT + 96;  // staged reference bytes
+constexpr int NANCH = 3;                      // anchors per tile
+constexpr int ALEN = 32;                      // anchor length (bytes)
+
+// bit j of the result: byte j of a equals byte j of b (ND dwords)
+template <int ND>
+__device__ __forceinline__ uint64_t byte_eq_bits(const uint32_t (&a)[ND], const uint32_t (&b)[ND]) {
+  uint64_t e = 0;
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+    const uint32_t x = a[i] ^ b[i];
+    const uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+    e |= (uint64_t)(((z >> 7) | (z >> 14) | (z >> 21) | (z >> 28)) & 0xFu) << (4 * i);
+  }
+  return e;
+}
+// bit i of the result: bits [i, i+w) of e are all set (w <= 63)
+__device__ __forceinline__ uint64_t run_and(uint64_t e, int w) {
+  uint64_t p[6];
+  p[0] = e;
+#pragma unroll
+  for (int b = 1; b < 6; ++b) p[b] = p[b - 1] & (p[b - 1] >> (1 << (b - 1)));
+  uint64_t r = ~0ull;
+  int off = 0;
+#pragma unroll
+  for (int b = 5; b >= 0; --b)
+    if ((w >> b) & 1) { r &= p[b] >> off; off += 1 << b; }
+  return r;
+}
+
 // K3.  One block per tile (record, stripe j): windows [j*TILE, (j+1)*TILE) of
 // a record with n >= k+2.  The tile's class codes (plus the k+3 bytes of
 // context around it) are staged in LDS with 16-byte loads; thread t takes IW
@@ -232,8 +269,10 @@ template <bool RC>
 __global__ void __launch_bounds__(IBLOCK)
 k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__ tiles,
          const long long* __restrict__ rec_start, const long long* __restrict__ rec_len, int k, uint64_t shift,
-         TableView T, unsigned* __restrict__ flags, int dbg) {
+         TableView T, unsigned* __restrict__ flags, int ref, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
+  __shared__ unsigned s_best[NANCH];
   const unsigned long long tile = tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
   const int r = (int)(tile >> 32);
   const long long rs = rec_start[r], rn = rec_len[r];
@@ -246,9 +285,47 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
   const long long a0 = lo & ~15ll;                            // 16-byte aligned source
   for (long long off = (long long)threadIdx.x * 16; a0 + off < hi; off += IBLOCK * 16)
     *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + a0 + off);
+  // the reference record's positions [plo, phi): this stripe +- DRIFT
+  const bool dedup = ref >= 0 && ref != r && !(dbg & 32);    // block-uniform
+  long long rfs = 0, rfn = 0, plo = 0, phi = 0, rbase = 0;
+  if (dedup) {
+    rfs = rec_start[ref];
+    rfn = rec_len[ref];
+    plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
+    phi = qt + TILE + k + 1 + DRIFT < rfn ? qt + TILE + k + 1 + DRIFT : rfn;
+    const long long ra0 = (rfs + plo) & ~15ll;
+    rbase = rfs - ra0;                                        // s_ref index of reference position 0
+    for (long long off = (long long)threadIdx.x * 16; ra0 + off < rfs + phi; off += IBLOCK * 16)
+      *reinterpret_cast<uint4*>(s_ref + off) = *reinterpret_cast<const uint4*>(cls + ra0 + off);
+    if (threadIdx.x < NANCH) s_best[threadIdx.x] = ~0u;
+  }
   __syncthreads();
   const long long base = rs - a0;                             // s_cls index of record position 0
   auto S = [&](long long q) -> uint32_t { return s_cls[base + q]; };
+  if (dedup) {
+    // drift at NANCH anchors: the smallest |delta| whose ALEN bytes match
+    for (int ai = 0; ai < NANCH; ++ai) {
+      const long long a = qt + 8 + (long long)ai * ((TILE - ALEN - 16) / (NANCH - 1));
+      if (a + ALEN > rn) continue;                            // block-uniform
+      uint32_t A[ALEN / 4];
+      lds_bytes(s_cls, (uint32_t)(base + a), A);
+      for (int d = threadIdx.x; d <= 2 * DRIFT; d += IBLOCK) {
+        const long long p = a - (d - DRIFT);
+        if (p < plo || p + ALEN > phi) continue;
+        uint32_t B1[1];
+        lds_bytes(s_ref, (uint32_t)(rbase + p), B1);
+        if (B1[0] != A[0]) continue;
+        uint32_t B[ALEN / 4];
+        lds_bytes(s_ref, (uint32_t)(rbase + p), B);
+        bool eq = true;
+#pragma unroll
+        for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
+        const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+        if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
+      }
+    }
+    __syncthreads();
+  }
 
   const long long q0 = qt + (long long)threadIdx.x * IW;
   const long long q1 = q0 + IW <= last + 1 ? q0 + IW : last + 1;
@@ -263,8 +340,9 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
     }
     ulonglong2 v[IB];
 #pragma unroll
-    for (int i = 0; i < IB; ++i)                   // IB independent probes in flight (unconditional:
-      v[i] = *reinterpret_cast<const ulonglong2*>(T.prim + 2 * (hh[i] >> T.qbits));   // no per-load branch)
+    for (int i = 0; i < IB; ++i)                   // IB independent probes in flight; a skipped
+      v[i] = mm[i] ? *reinterpret_cast<const ulonglong2*>(T.prim + 2 * (hh[i] >> T.qbits))   // window
+                   : make_ulonglong2(0ull, 0ull);                                           // sends none
     if (dbg & 2) {                                 // dev knob: loads only
 #pragma unroll
       for (int i = 0; i < IB; ++i) created += (unsigned)(v[i].x ^ v[i].y) & 1u;
@@ -280,6 +358,25 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
     uint32_t P[IW / 4], D[IW / 4 + 1];
     lds_bytes(s_cls, o - 1, P);
     lds_bytes(s_cls, o + (uint32_t)k - 1, D);
+    // windows covered by the reference at one of the anchors' drifts
+    uint32_t covered = 0;
+    if (dedup) {
+      constexpr int NB = (IW + 27 + 1 + 3) / 4;            // bytes q0-1 .. q0+IW+k-1, k <= 27
+      uint32_t G[NB];
+      lds_bytes(s_cls, o - 1, G);
+      unsigned prev = ~0u;
+      for (int ai = 0; ai < NANCH; ++ai) {
+        const unsigned b = s_best[ai];
+        if (b == ~0u || (b & 0xFFFFu) == prev) continue;
+        prev = b & 0xFFFFu;
+        const long long p0 = q0 - ((long long)(b & 0xFFFFu) - DRIFT);   // reference window of q0
+        // reference windows p0 .. p0+IW-1 interior, and their bytes staged
+        if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
+        uint32_t Rw[NB];
+        lds_bytes(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
+        covered |= (uint32_t)(run_and(byte_eq_bits(G, Rw), k + 2) & ((1u << IW) - 1u));
+      }
+    }
 #pragma unroll
     for (int h = 0; h < IW / IB; ++h) {
       uint64_t cc[IB], hh[IB];
@@ -304,6 +401,7 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
           cc[i] = le ? K : Kr;
           mm[i] = le ? mf : (mf << B_SHIFT);
         }
+        if ((covered >> x) & 1u) mm[i] = 0;        // the reference inserts this window
         hh[i] = T.perm(cc[i]);
       }
       probe(cc, hh, mm);
@@ -852,6 +950,7 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
     maxs = std::max(maxs, s);
   }
   std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  c.k3_ref = nt.size() >= 2 ? nt[0].second : -1;      // the lead is every follower's dedup reference
   std::vector<unsigned long long> tiles;
   tiles.reserve(total);
   size_t live = nt.size();
@@ -943,9 +1042,10 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
     hipLaunchKernelGGL(k_insert_grp<false>, g, b, 0, c.stream, cls, tiles, c.groups.as<int>(), rs, rl, c.k, shift, c.tv,
                        flags, dbg);
   else if (rc0)
-    hipLaunchKernelGGL(k_insert<true>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, dbg);
+    hipLaunchKernelGGL(k_insert<true>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, c.k3_ref, dbg);
   else
-    hipLaunchKernelGGL(k_insert<false>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, dbg);
+    hipLaunchKernelGGL(k_insert<false>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, c.k3_ref,
+                       dbg);
   PG_HIP(hipGetLastError());
 }
 

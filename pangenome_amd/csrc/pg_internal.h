@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -109,6 +110,7 @@ struct Ctx {
   uint64_t n_tiles = 0;
   int tile_k = 0;
   int tile_mode = 0;              // 0: per-record tiles (k_insert), 1: record groups (k_insert_grp)
+  int k3_ref = -1;                // k_insert's dedup reference record (the lead), -1: none
   DevBuf groups;                  // int32 [n_groups * GG] record ids, -1 padded
   std::vector<int64_t> tile_sig_len;   // record lengths / flags the tile list was built for
   std::vector<uint8_t> tile_sig_flag;
@@ -177,13 +179,17 @@ inline int log2u(uint64_t p) {
 }
 
 // Table geometry for k-mers of length k holding about `keys` canonical keys:
-// load <= 0.5 keys per 2-word bucket, quotient <= 38 bits (so that quotient +
-// 26 mask bits fit 64), overflow table ~1/16 of the keys.
+// load <= 0.25 keys per 2-word bucket (C3: 0.5 -> 0.25 took K3 6.31 -> 5.76 ms
+// for +0.2 ms of K5 sweep; 0.125 was slower), quotient <= 38 bits (so that
+// quotient + 26 mask bits fit 64), overflow table ~1/16 of the keys.
 inline TableView make_geometry(int k, uint64_t keys, uint64_t& buckets, uint64_t& ovf_slots) {
   uint64_t maxkey = 1;
   for (int i = 0; i < k; ++i) maxkey *= 5;
   const int kb = std::max(1, log2u(maxkey));                 // keys < 5^k <= 2^kb
-  const int bb = std::max({kb - 38, log2u(std::max<uint64_t>(keys * 2, 1)), 11});   // >= 2048 buckets
+  // keys per bucket target (PG_BUCKET_LOAD, development knob)
+  static const double load = getenv("PG_BUCKET_LOAD") ? atof(getenv("PG_BUCKET_LOAD")) : 0.25;
+  const uint64_t want = (uint64_t)((double)keys / (load > 0.05 ? load : 0.5));
+  const int bb = std::max({kb - 38, log2u(std::max<uint64_t>(want, 1)), 11});   // >= 2048 buckets
   buckets = 1ull << bb;
   ovf_slots = next_pow2(std::max<uint64_t>(4096, keys / 16));
   TableView t{};

@@ -128,6 +128,50 @@ def test_k3_forms_vs_oracle(oracle_mod, monkeypatch, form, rc0):
     ctx.close()
 
 
+@pytest.mark.parametrize("c", [0, 2])
+def test_k3_reference_dedup_vs_oracle(oracle_mod, monkeypatch, c):
+    """k_insert skips a follower window whose k+2 context bytes equal the lead
+    record's at some drift: copies of the lead with insertions (drift inside
+    and beyond the +-512 search), deletions, SNPs, an N run, lowercase bytes,
+    shorter copies (reference windows near its ends) and a reverse complement."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    monkeypatch.delenv("PG_K3", raising=False)
+    rng = np.random.default_rng(7 + c)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    lead = acgt[rng.integers(0, 4, 30_000)]
+    copies = [lead.copy()]
+    for ins in (1, 37, 300, 511, 513, 900):
+        g = lead.copy()
+        pos = int(rng.integers(1000, 20_000))
+        g = np.concatenate([g[:pos], acgt[rng.integers(0, 4, ins)], g[pos:]])
+        snp = rng.integers(0, g.shape[0], 20)
+        g[snp] = acgt[rng.integers(0, 4, 20)]
+        copies.append(g)
+    g = lead.copy()
+    g = np.concatenate([g[:5000], g[5100:]])                 # deletion
+    g[12000:12040] = ord("N")
+    g[20000:20010] = np.frombuffer(b"acgtacgtac", np.uint8)
+    copies.append(g)
+    copies.append(lead[3:29_000].copy())                     # shorter, shifted
+    copies.append(lead[:4100].copy())                        # ends inside the lead's first stripe
+    comp = np.frombuffer(bytes.maketrans(b"ACGT", b"TGCA"), np.uint8)
+    copies.append(comp[lead[::-1]])                          # reverse complement
+    fasta = b"".join(b">g%d\n" % i + g.tobytes() + b"\n" for i, g in enumerate(copies))
+    ref = oracle_mod.OracleRun(fasta, 27, c)
+    ctx = Context(27)
+    ctx.set_fasta(fasta)
+    ctx.parse()
+    ctx.build_dbg(None, 0, c == 2)
+    keys, masks = ctx.dbg()
+    rk, rm = ref.dbg()
+    assert np.array_equal(keys, rk)
+    assert np.array_equal(masks, rm)
+    ctx.build_rdbg()
+    assert np.array_equal(ctx.rdbg(), ref.rdbg())
+    ctx.close()
+
+
 def test_edge_checkpoint_reversal_vs_oracle(km, oracle_mod, tmp_path):
     from pangenome_amd import synth
     fasta = b"junk before header\n" + synth.pangenome(9, 20_000, snp=0.01, indel=1e-3, seed=5)
