@@ -221,6 +221,14 @@ __device__ __forceinline__ void init_keys(const uint8_t* sc, uint32_t o, int k, 
   Kr = (uint64_t)rlo + rhi * 1220703125ull;
 }
 
+// K3 tile: record r's windows [stripe*TILE, (stripe+1)*TILE), with the
+// record's compacted start and length carried along (one load per block).
+struct TileDesc {
+  long long rs, rn;
+  int r, stripe;
+  long long pad;
+};
+
 // ---- positional dedup against a reference record (see k_insert).  A window q
 // of record g with neither record end in it, whose bytes [q-1, q+k] equal the
 // reference's bytes [q'-1, q'+k] at q' = q - delta (q' interior too), has the
@@ -231,6 +239,7 @@ constexpr int DRIFT = 512;                    // searched offsets: [-DRIFT, DRIF
 constexpr int RSPAN = TILE + 2 * DRIFT + 96;  // staged reference bytes
 constexpr int NANCH = 3;                      // anchors per tile
 constexpr int ALEN = 32;                      // anchor length (bytes)
+constexpr int HINTW = 8;                      // first search: +-HINTW around the record's last drift
 
 // bit j of the result: byte j of a equals byte j of b (ND dwords)
 template <int ND>
@@ -258,80 +267,21 @@ __device__ __forceinline__ uint64_t run_and(uint64_t e, int w) {
   return r;
 }
 
-// K3.  One block per tile (record, stripe j): windows [j*TILE, (j+1)*TILE) of
-// a record with n >= k+2.  The tile's class codes (plus the k+3 bytes of
-// context around it) are staged in LDS with 16-byte loads; thread t takes IW
-// consecutive windows, rolls both strands' keys across them, and probes the
-// table in batches of IB windows: IB independent bucket loads in flight per
-// lane, and only windows whose entry is not already complete take the CAS /
-// atomicOr / overflow path.
+// The IW windows q0 .. q0+IW-1 (clipped at the record's last window) of one
+// record staged in s_cls (s_cls[base + q] = class of position q): both
+// strands' rolling keys, the canonical key and mask word of each window, and
+// the probes / updates in batches of IB (windows with a `covered` bit are
+// inserted by the reference record and send nothing).  Interior segments run
+// from registers; a segment holding window 0 or the last window takes the
+// generic path with the boundary rules.
 template <bool RC>
-__global__ void __launch_bounds__(IBLOCK)
-k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__ tiles,
-         const long long* __restrict__ rec_start, const long long* __restrict__ rec_len, int k, uint64_t shift,
-         TableView T, unsigned* __restrict__ flags, int ref, int dbg) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
-  __shared__ unsigned s_best[NANCH];
-  const unsigned long long tile = tiles[xcd_swizzle(blockIdx.x, gridDim.x)];
-  const int r = (int)(tile >> 32);
-  const long long rs = rec_start[r], rn = rec_len[r];
-  const long long last = rn - k;                              // last window index
-  const long long qt = (long long)(tile & 0xFFFFFFFFull) * TILE;
-  // stage positions [lo, hi) of the record: windows qt .. qt+TILE-1 read from
-  // q-2 (last-window pred) to q+k+1 (twin pred of window 0)
-  const long long lo = rs + (qt >= 2 ? qt - 2 : 0);
-  const long long hi = rs + (qt + TILE + k + 2 < rn ? qt + TILE + k + 2 : rn);
-  const long long a0 = lo & ~15ll;                            // 16-byte aligned source
-  for (long long off = (long long)threadIdx.x * 16; a0 + off < hi; off += IBLOCK * 16)
-    *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + a0 + off);
-  // the reference record's positions [plo, phi): this stripe +- DRIFT
-  const bool dedup = ref >= 0 && ref != r && !(dbg & 32);    // block-uniform
-  long long rfs = 0, rfn = 0, plo = 0, phi = 0, rbase = 0;
-  if (dedup) {
-    rfs = rec_start[ref];
-    rfn = rec_len[ref];
-    plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
-    phi = qt + TILE + k + 1 + DRIFT < rfn ? qt + TILE + k + 1 + DRIFT : rfn;
-    const long long ra0 = (rfs + plo) & ~15ll;
-    rbase = rfs - ra0;                                        // s_ref index of reference position 0
-    for (long long off = (long long)threadIdx.x * 16; ra0 + off < rfs + phi; off += IBLOCK * 16)
-      *reinterpret_cast<uint4*>(s_ref + off) = *reinterpret_cast<const uint4*>(cls + ra0 + off);
-    if (threadIdx.x < NANCH) s_best[threadIdx.x] = ~0u;
-  }
-  __syncthreads();
-  const long long base = rs - a0;                             // s_cls index of record position 0
-  auto S = [&](long long q) -> uint32_t { return s_cls[base + q]; };
-  if (dedup) {
-    // drift at NANCH anchors: the smallest |delta| whose ALEN bytes match
-    for (int ai = 0; ai < NANCH; ++ai) {
-      const long long a = qt + 8 + (long long)ai * ((TILE - ALEN - 16) / (NANCH - 1));
-      if (a + ALEN > rn) continue;                            // block-uniform
-      uint32_t A[ALEN / 4];
-      lds_bytes(s_cls, (uint32_t)(base + a), A);
-      for (int d = threadIdx.x; d <= 2 * DRIFT; d += IBLOCK) {
-        const long long p = a - (d - DRIFT);
-        if (p < plo || p + ALEN > phi) continue;
-        uint32_t B1[1];
-        lds_bytes(s_ref, (uint32_t)(rbase + p), B1);
-        if (B1[0] != A[0]) continue;
-        uint32_t B[ALEN / 4];
-        lds_bytes(s_ref, (uint32_t)(rbase + p), B);
-        bool eq = true;
-#pragma unroll
-        for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
-        const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
-        if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
-      }
-    }
-    __syncthreads();
-  }
-
-  const long long q0 = qt + (long long)threadIdx.x * IW;
+__device__ __forceinline__ void insert_segment(const uint8_t* s_cls, long long base, long long q0, long long last,
+                                               int k, uint64_t shift, const TableView& T, unsigned* flags,
+                                               uint32_t covered, int dbg, unsigned& created) {
   const long long q1 = q0 + IW <= last + 1 ? q0 + IW : last + 1;
-  unsigned created = 0;
+  auto S = [&](long long q) -> uint32_t { return s_cls[base + q]; };
   uint64_t K = 0, Kr = 0;
-  if (q0 < q1) init_keys(s_cls, (uint32_t)(base + q0), k, K, Kr);
+  init_keys(s_cls, (uint32_t)(base + q0), k, K, Kr);
   auto probe = [&](const uint64_t (&cc)[IB], const uint64_t (&hh)[IB], const uint32_t (&mm)[IB]) {
     if (dbg & 1) {                                 // dev knob: windows only
 #pragma unroll
@@ -351,32 +301,13 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
     tab_or_batch(T, cc, hh, mm, v, flags, created, dbg);
   };
   if (q0 > 0 && q0 + IW <= last) {
-    // interior thread (no window 0, no last window, all IW live): the context
+    // interior segment (no window 0, no last window, all IW live): the context
     // bytes come from LDS once, into registers; P(i) = S(q-1), D(i) = S(q+k-1)
     // for window q = q0 + i, and D(i+1) = S(q+k)
     const uint32_t o = (uint32_t)(base + q0);
     uint32_t P[IW / 4], D[IW / 4 + 1];
     lds_bytes(s_cls, o - 1, P);
     lds_bytes(s_cls, o + (uint32_t)k - 1, D);
-    // windows covered by the reference at one of the anchors' drifts
-    uint32_t covered = 0;
-    if (dedup) {
-      constexpr int NB = (IW + 27 + 1 + 3) / 4;            // bytes q0-1 .. q0+IW+k-1, k <= 27
-      uint32_t G[NB];
-      lds_bytes(s_cls, o - 1, G);
-      unsigned prev = ~0u;
-      for (int ai = 0; ai < NANCH; ++ai) {
-        const unsigned b = s_best[ai];
-        if (b == ~0u || (b & 0xFFFFu) == prev) continue;
-        prev = b & 0xFFFFu;
-        const long long p0 = q0 - ((long long)(b & 0xFFFFu) - DRIFT);   // reference window of q0
-        // reference windows p0 .. p0+IW-1 interior, and their bytes staged
-        if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
-        uint32_t Rw[NB];
-        lds_bytes(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
-        covered |= (uint32_t)(run_and(byte_eq_bits(G, Rw), k + 2) & ((1u << IW) - 1u));
-      }
-    }
 #pragma unroll
     for (int h = 0; h < IW / IB; ++h) {
       uint64_t cc[IB], hh[IB];
@@ -406,7 +337,8 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
       }
       probe(cc, hh, mm);
     }
-  } else {
+    return;
+  }
   for (long long qb = q0; qb < q1; qb += IB) {
     uint64_t cc[IB], hh[IB];
     uint32_t mm[IB];
@@ -441,8 +373,177 @@ k_insert(const uint8_t* __restrict__ cls, const unsigned long long* __restrict__
     }
     probe(cc, hh, mm);
   }
+}
+
+// K3.  One block per tile (record, stripe j): windows [j*TILE, (j+1)*TILE) of
+// a record with n >= k+2.  The tile's class codes (plus the k+3 bytes of
+// context around it) are staged in LDS with 16-byte loads; thread t takes IW
+// consecutive windows, rolls both strands' keys across them, and probes the
+// table in batches of IB windows: IB independent bucket loads in flight per
+// lane, and only windows whose entry is not already complete take the CAS /
+// atomicOr / overflow path.
+// A segment left with work after the coverage pass (k_insert<.., true>).
+struct WorkItem {
+  long long rs, last, q0;
+  uint32_t covered, pad;
+};
+
+template <bool RC, bool EMIT>
+__global__ void __launch_bounds__(IBLOCK)
+k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
+         unsigned long long* __restrict__ qcount, int k, uint64_t shift, TableView T, unsigned* __restrict__ flags,
+         int ref, long long rfs, long long rfn, int* __restrict__ hints, int dbg) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
+  __shared__ unsigned s_best[NANCH];
+  const TileDesc td = descs[xcd_swizzle(blockIdx.x, gridDim.x)];   // one dependent load per block
+  const int r = td.r;
+  const long long rs = td.rs, rn = td.rn;
+  const long long last = rn - k;                              // last window index
+  const long long qt = (long long)td.stripe * TILE;
+  const int hint = ref >= 0 && ref != r ? hints[r] : -1;     // in flight with the staging loads
+  // stage positions [lo, hi) of the record: windows qt .. qt+TILE-1 read from
+  // q-2 (last-window pred) to q+k+1 (twin pred of window 0)
+  const long long lo = rs + (qt >= 2 ? qt - 2 : 0);
+  const long long hi = rs + (qt + TILE + k + 2 < rn ? qt + TILE + k + 2 : rn);
+  const long long a0 = lo & ~15ll;                            // 16-byte aligned source
+  for (long long off = (long long)threadIdx.x * 16; a0 + off < hi; off += IBLOCK * 16)
+    *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + a0 + off);
+  // the reference record's positions [plo, phi): this stripe +- DRIFT
+  const bool dedup = ref >= 0 && ref != r && !(dbg & 32);    // block-uniform
+  long long plo = 0, phi = 0, rbase = 0;
+  if (dedup) {
+    plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
+    phi = qt + TILE + k + 1 + DRIFT < rfn ? qt + TILE + k + 1 + DRIFT : rfn;
+    const long long ra0 = (rfs + plo) & ~15ll;
+    rbase = rfs - ra0;                                        // s_ref index of reference position 0
+    for (long long off = (long long)threadIdx.x * 16; ra0 + off < rfs + phi; off += IBLOCK * 16)
+      *reinterpret_cast<uint4*>(s_ref + off) = *reinterpret_cast<const uint4*>(cls + ra0 + off);
+    if (threadIdx.x < NANCH) s_best[threadIdx.x] = ~0u;
   }
-  block_count(created, flags);                     // both paths: one barrier per wave
+  __syncthreads();
+  const long long base = rs - a0;                             // s_cls index of record position 0
+  if (dedup) {
+    // drift at NANCH anchors: the smallest |delta| whose ALEN bytes match.
+    // First +-HINTW around the drift this record's previous stripe found
+    // (hint[r]; a stale or racy hint only costs the full search), then all
+    // of [-DRIFT, DRIFT] for anchors still without a match.
+    auto anchor = [&](int ai) { return qt + 8 + (long long)ai * ((TILE - ALEN - 16) / (NANCH - 1)); };
+    auto try_d = [&](int ai, int d) {
+      const long long a = anchor(ai), p = a - (d - DRIFT);
+      if (a + ALEN > rn || d < 0 || d > 2 * DRIFT || p < plo || p + ALEN > phi) return;
+      uint32_t A1[1], B1[1];
+      lds_bytes(s_cls, (uint32_t)(base + a), A1);
+      lds_bytes(s_ref, (uint32_t)(rbase + p), B1);
+      if (B1[0] != A1[0]) return;
+      uint32_t A[ALEN / 4], B[ALEN / 4];
+      lds_bytes(s_cls, (uint32_t)(base + a), A);
+      lds_bytes(s_ref, (uint32_t)(rbase + p), B);
+      bool eq = true;
+#pragma unroll
+      for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
+      const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+      if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
+    };
+    if (hint >= 0 && threadIdx.x < NANCH * (2 * HINTW + 1))
+      try_d((int)threadIdx.x / (2 * HINTW + 1), hint - HINTW + (int)threadIdx.x % (2 * HINTW + 1));
+    __syncthreads();
+    for (int ai = 0; ai < NANCH; ++ai) {
+      if (s_best[ai] != ~0u) continue;                        // block-uniform
+      for (int d = threadIdx.x; d <= 2 * DRIFT; d += IBLOCK) try_d(ai, d);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int h = -1;
+      for (int ai = NANCH - 1; ai >= 0; --ai)
+        if (s_best[ai] != ~0u) h = (int)(s_best[ai] & 0xFFFFu);
+      if (h >= 0) hints[r] = h;
+    }
+  }
+
+  // Phase A: thread t owns segment t (windows qt + t*IW ..).  With a
+  // reference, an interior segment learns which of its windows are covered;
+  // segments left with work are compacted so that phase B runs only them.
+  __shared__ uint32_t s_work[IBLOCK];
+  __shared__ uint32_t s_scan[IBLOCK / 64];
+  uint32_t covered = 0;
+  unsigned created_acc = 0;
+  {
+    const long long q0 = qt + (long long)threadIdx.x * IW;
+    if (dedup && q0 > 0 && q0 + IW <= last) {
+      const uint32_t o = (uint32_t)(base + q0);
+      constexpr int NB = (IW + 27 + 1 + 3) / 4;              // bytes q0-1 .. q0+IW+k-1, k <= 27
+      uint32_t G[NB];
+      lds_bytes(s_cls, o - 1, G);
+      unsigned prev = ~0u;
+      for (int ai = 0; ai < NANCH; ++ai) {
+        const unsigned b = s_best[ai];
+        if (b == ~0u || (b & 0xFFFFu) == prev) continue;
+        prev = b & 0xFFFFu;
+        const long long p0 = q0 - ((long long)(b & 0xFFFFu) - DRIFT);   // reference window of q0
+        // reference windows p0 .. p0+IW-1 interior, and their bytes staged
+        if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
+        uint32_t Rw[NB];
+        lds_bytes(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
+        uint32_t diff = 0;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) diff |= G[i] ^ Rw[i];
+        if (diff == 0) { covered = (1u << IW) - 1u; break; }  // the common case: all context bytes equal
+        covered |= (uint32_t)(run_and(byte_eq_bits(G, Rw), k + 2) & ((1u << IW) - 1u));
+      }
+    }
+    if (dbg & 128) covered = (1u << IW) - 1u;      // dev knob: prologue + coverage only
+    const bool work = q0 <= last && covered != (1u << IW) - 1u;
+    uint32_t nwork;
+    const uint32_t pos = block_excl_scan<IBLOCK>(work ? 1u : 0u, s_scan, nwork);
+    if (EMIT) {                                    // to the queue: k_insert_work runs them densely
+      __shared__ unsigned long long s_qbase;
+      if (threadIdx.x == 0) s_qbase = nwork ? atomicAdd(qcount, (unsigned long long)nwork) : 0ull;
+      __syncthreads();
+      if (work) queue[s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
+      return;                                      // no barrier follows
+    }
+    if (work) s_work[pos] = threadIdx.x | (covered << 16);
+    if ((dbg & 64) && threadIdx.x == 0) {         // dev knob: segments with work / with windows
+      atomicAdd(flags + 16 * (2 + N_CNT) + 8, nwork);
+      atomicAdd(flags + 16 * (2 + N_CNT) + 9, (unsigned)(dedup ? 1 : 0));
+    }
+    if ((dbg & 64) && q0 <= last) {
+      atomicAdd(flags + 16 * (2 + N_CNT) + 10, 1u);
+      atomicAdd(flags + 16 * (2 + N_CNT) + 11, (unsigned)__builtin_popcount(covered));
+    }
+    __syncthreads();
+    if (threadIdx.x < nwork) {
+      covered = s_work[threadIdx.x] >> 16;
+      insert_segment<RC>(s_cls, base, qt + (long long)(s_work[threadIdx.x] & 0xFFFFu) * IW, last, k, shift, T,
+                         flags, covered, dbg, created_acc);
+    }
+  }
+  block_count(created_acc, flags);                 // every thread: one barrier per wave
+}
+
+// K3 work pass: one queued segment per thread, every lane busy.  The
+// segment's 64 context bytes (from position q0-2, 16-byte aligned) are
+// staged in the thread's own LDS slot and insert_segment runs on them.
+template <bool RC>
+__global__ void __launch_bounds__(IBLOCK)
+k_insert_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
+              const unsigned long long* __restrict__ qcount, int k, uint64_t shift, TableView T,
+              unsigned* __restrict__ flags, int dbg) {
+  __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][96];
+  uint8_t* slot = scratch[threadIdx.x] + 16;
+  const unsigned long long n = *qcount;
+  unsigned created = 0;
+  for (unsigned long long i = blockIdx.x * (unsigned long long)IBLOCK + threadIdx.x; i < n;
+       i += (unsigned long long)gridDim.x * IBLOCK) {
+    const WorkItem w = queue[i];
+    const long long from = w.rs + w.q0 - 2, aligned = from > 0 ? from & ~15ll : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<uint4*>(slot + 16 * j) = *reinterpret_cast<const uint4*>(cls + aligned + 16 * j);
+    insert_segment<RC>(slot, w.rs - aligned, w.q0, w.last, k, shift, T, flags, w.covered, dbg, created);
+  }
+  block_count(created, flags);
 }
 
 // K3, group form (pangenome inputs).  One block takes stripe j (GW windows) of
@@ -951,6 +1052,8 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   }
   std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
   c.k3_ref = nt.size() >= 2 ? nt[0].second : -1;      // the lead is every follower's dedup reference
+  c.k3_hint.reserve(4 * (R + 1));                       // per-record drift hints: none yet
+  PG_HIP(hipMemsetAsync(c.k3_hint.p, 0xFF, 4 * (R + 1), c.stream));
   std::vector<unsigned long long> tiles;
   tiles.reserve(total);
   size_t live = nt.size();
@@ -962,8 +1065,17 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
     while (live && nt[live - 1].first <= jf) --live;
     for (size_t i = 1; i < live; ++i) tiles.push_back(((unsigned long long)nt[i].second << 32) | jf);
   }
+  std::vector<TileDesc> descs(total);
+  for (uint64_t i = 0; i < total; ++i) {
+    const int r = (int)(tiles[i] >> 32);
+    descs[i] = TileDesc{c.h_rec_start[r], c.h_rec_len[r], r, (int)(tiles[i] & 0xFFFFFFFFull), 0};
+  }
   c.tiles.reserve(8 * (total + 1));
-  if (total) PG_HIP(hipMemcpyAsync(c.tiles.p, tiles.data(), 8 * total, hipMemcpyHostToDevice, c.stream));
+  c.tile_desc.reserve(sizeof(TileDesc) * (total + 1));
+  if (total) {
+    PG_HIP(hipMemcpyAsync(c.tiles.p, tiles.data(), 8 * total, hipMemcpyHostToDevice, c.stream));
+    PG_HIP(hipMemcpyAsync(c.tile_desc.p, descs.data(), sizeof(TileDesc) * total, hipMemcpyHostToDevice, c.stream));
+  }
   c.sync();
   c.tile_sig_len = c.h_rec_len;
   c.tile_sig_flag = flag;
@@ -1041,11 +1153,33 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
   else if (mode)
     hipLaunchKernelGGL(k_insert_grp<false>, g, b, 0, c.stream, cls, tiles, c.groups.as<int>(), rs, rl, c.k, shift, c.tv,
                        flags, dbg);
-  else if (rc0)
-    hipLaunchKernelGGL(k_insert<true>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, c.k3_ref, dbg);
-  else
-    hipLaunchKernelGGL(k_insert<false>, g, b, 0, c.stream, cls, tiles, rs, rl, c.k, shift, c.tv, flags, c.k3_ref,
-                       dbg);
+  else {
+    const long long rfs = c.k3_ref >= 0 ? c.h_rec_start[c.k3_ref] : 0, rfn = c.k3_ref >= 0 ? c.h_rec_len[c.k3_ref] : 0;
+    const TileDesc* td = c.tile_desc.as<TileDesc>();
+    int* hint = c.k3_hint.as<int>();
+    if (c.k3_ref >= 0 && !(dbg & 256)) {
+      // coverage pass, then the dense work pass over the queued segments
+      const uint64_t max_items = c.windows_fw / IW + c.n_records + 1;
+      c.k3_queue.reserve(sizeof(WorkItem) * max_items + 64);
+      auto* q = c.k3_queue.as<WorkItem>();
+      auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + sizeof(WorkItem) * max_items);
+      PG_HIP(hipMemsetAsync(qn, 0, 8, c.stream));
+      hipLaunchKernelGGL((k_insert<true, true>), g, b, 0, c.stream, cls, td, q, qn, c.k, shift, c.tv, flags, c.k3_ref,
+                         rfs, rfn, hint, dbg);
+      PG_HIP(hipGetLastError());
+      const unsigned gw = grid_for(max_items, IBLOCK, 16384);
+      if (rc0)
+        hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, c.stream, cls, q, qn, c.k, shift, c.tv, flags, dbg);
+      else
+        hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, c.stream, cls, q, qn, c.k, shift, c.tv, flags, dbg);
+    } else if (rc0) {
+      hipLaunchKernelGGL((k_insert<true, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, c.k, shift, c.tv, flags,
+                         c.k3_ref, rfs, rfn, hint, dbg);
+    } else {
+      hipLaunchKernelGGL((k_insert<false, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, c.k, shift, c.tv,
+                         flags, c.k3_ref, rfs, rfn, hint, dbg);
+    }
+  }
   PG_HIP(hipGetLastError());
 }
 
@@ -1105,7 +1239,11 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     c.ms_clear = c.t0.ms();
     c.ms_insert = c.t1.ms();
     if (dbg) {                       // dev knob run: timings only, the table is not a dBG
-      fprintf(stderr, "PG_K3_DBG=%d mode=%d insert=%.3f ms\n", dbg, mode, c.ms_insert);
+      std::vector<unsigned> f(N_FLAGS);
+      PG_HIP(hipMemcpy(f.data(), c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost));
+      const unsigned* d = f.data() + 16 * (2 + N_CNT);
+      fprintf(stderr, "PG_K3_DBG=%d mode=%d insert=%.3f ms work_segments=%u dedup_blocks=%u segments=%u "
+              "covered_windows=%u\n", dbg, mode, c.ms_insert, d[8], d[9], d[10], d[11]);
       return;
     }
     if (!overflow) {

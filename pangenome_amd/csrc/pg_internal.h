@@ -111,6 +111,9 @@ struct Ctx {
   int tile_k = 0;
   int tile_mode = 0;              // 0: per-record tiles (k_insert), 1: record groups (k_insert_grp)
   int k3_ref = -1;                // k_insert's dedup reference record (the lead), -1: none
+  DevBuf k3_hint;                 // int32 per record: last drift k_insert found (-1: none)
+  DevBuf tile_desc;               // k_insert tile descriptors (record start / length / index / stripe)
+  DevBuf k3_queue;                // segments left with work after k_insert's coverage pass, + counter
   DevBuf groups;                  // int32 [n_groups * GG] record ids, -1 padded
   std::vector<int64_t> tile_sig_len;   // record lengths / flags the tile list was built for
   std::vector<uint8_t> tile_sig_flag;
