@@ -178,7 +178,8 @@ def main():
         "config": {"workload": desc, "k": K, "strands": "-c 2 (dBG both strands)",
                    "bases_per_gpu": st_b.n_bases, "fasta_bytes_per_gpu": nbytes,
                    "parallelism": "record-sharded, owner all-to-all" if world > 1 else "single GPU"},
-        "roofline": {"kernel": "k_insert (K3)", "bound": "hbm", "achieved": round(achieved / 1e9, 2),
+        "roofline": {"kernel": "K3 = k_insert<cov> + k_insert_work (one HIP-event span)", "bound": "hbm",
+                     "achieved": round(achieved / 1e9, 2),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                      "traffic": traffic, "alg_bytes_per_launch": ins_bytes,
                      "avg_launch_ms": round(ins_avg, 4)},

@@ -15,8 +15,8 @@ run() {  # name timeout cmd...
 }
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 1200 python -m pytest tests -m gpu -x -q ;;
-    testsall) run pytest_gpu 1200 python -m pytest tests -m gpu -q ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    testsall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
