@@ -388,11 +388,20 @@ struct WorkItem {
   uint32_t covered, pad;
 };
 
+// The queue is NQ sub-queues, each with its own counter on its own 64-byte
+// line; block b appends to sub-queue b % NQ.  One counter shared by all
+// ~120 K blocks of a C3 launch serialises their atomics at the memory side
+// (1.48 ms measured, tools/rates.hip) - as long as the whole coverage pass;
+// 64 counters take 0.045 ms.  A block appends at most IBLOCK items, so
+// sub-queue capacity = ceil(grid / NQ) * IBLOCK.
+constexpr int NQ = 64;
+constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long long words)
+
 template <bool RC, bool EMIT>
 __global__ void __launch_bounds__(IBLOCK)
 k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
-         unsigned long long* __restrict__ qcount, int k, uint64_t shift, TableView T, unsigned* __restrict__ flags,
-         int ref, long long rfs, long long rfn, int* __restrict__ hints, int dbg) {
+         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift, TableView T,
+         unsigned* __restrict__ flags, int ref, long long rfs, long long rfn, int* __restrict__ hints, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ unsigned s_best[NANCH];
@@ -498,9 +507,10 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wo
     const uint32_t pos = block_excl_scan<IBLOCK>(work ? 1u : 0u, s_scan, nwork);
     if (EMIT) {                                    // to the queue: k_insert_work runs them densely
       __shared__ unsigned long long s_qbase;
-      if (threadIdx.x == 0) s_qbase = nwork ? atomicAdd(qcount, (unsigned long long)nwork) : 0ull;
+      const unsigned sub = blockIdx.x % NQ;
+      if (threadIdx.x == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
       __syncthreads();
-      if (work) queue[s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
+      if (work) queue[sub * qcap + s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
       return;                                      // no barrier follows
     }
     if (work) s_work[pos] = threadIdx.x | (covered << 16);
@@ -522,21 +532,40 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wo
   block_count(created_acc, flags);                 // every thread: one barrier per wave
 }
 
-// K3 work pass: one queued segment per thread, every lane busy.  The
-// segment's 64 context bytes (from position q0-2, 16-byte aligned) are
+// K3 work pass: one queued segment per thread, every lane busy.  The NQ
+// sub-queues are read as one concatenated list (their counts scanned in LDS).
+// The segment's 64 context bytes (from position q0-2, 16-byte aligned) are
 // staged in the thread's own LDS slot and insert_segment runs on them.
 template <bool RC>
 __global__ void __launch_bounds__(IBLOCK)
 k_insert_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
-              const unsigned long long* __restrict__ qcount, int k, uint64_t shift, TableView T,
-              unsigned* __restrict__ flags, int dbg) {
+              const unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift,
+              TableView T, unsigned* __restrict__ flags, int dbg) {
+  static_assert(NQ == 64, "one wave scans the sub-queue counts");
   __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][96];
+  __shared__ unsigned long long s_pre[NQ + 1];
+  if (threadIdx.x < 64) {
+    const unsigned long long c = qcount[QSTRIDE * threadIdx.x];
+    unsigned long long x = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long y = __shfl_up(x, o, 64);
+      if ((int)threadIdx.x >= o) x += y;
+    }
+    s_pre[threadIdx.x + 1] = x;                    // inclusive -> s_pre[j+1]
+    if (threadIdx.x == 0) s_pre[0] = 0ull;
+  }
+  __syncthreads();
   uint8_t* slot = scratch[threadIdx.x] + 16;
-  const unsigned long long n = *qcount;
+  const unsigned long long n = s_pre[NQ];
   unsigned created = 0;
   for (unsigned long long i = blockIdx.x * (unsigned long long)IBLOCK + threadIdx.x; i < n;
        i += (unsigned long long)gridDim.x * IBLOCK) {
-    const WorkItem w = queue[i];
+    int lo = 0;                                    // largest j with s_pre[j] <= i
+#pragma unroll
+    for (int step = NQ / 2; step > 0; step >>= 1)
+      if (s_pre[lo + step] <= i) lo += step;
+    const WorkItem w = queue[(unsigned long long)lo * qcap + (i - s_pre[lo])];
     const long long from = w.rs + w.q0 - 2, aligned = from > 0 ? from & ~15ll : 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j)
@@ -1002,8 +1031,17 @@ static void alloc_table(Ctx& c, uint64_t keys) {
   c.flags.reserve(4 * N_FLAGS);
 }
 
+// 16-byte streaming stores: 5.1 TB/s measured (tools/fetch_calib.hip) where
+// hipMemsetAsync's fill kernel ran the 1 GiB table at 3.3 TB/s.
+__global__ void __launch_bounds__(256) k_zero16(uint4* __restrict__ p, uint64_t n16) {
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256ull) p[i] = z;
+}
+
 static void clear_table(Ctx& c) {
-  PG_HIP(hipMemsetAsync(c.table.p, 0, 16 * c.cap, c.stream));
+  hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, c.stream,
+                     reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
+  PG_HIP(hipGetLastError());
   PG_HIP(hipMemsetAsync(c.ovf.p, 0, sizeof(Slot) * c.ovf_cap, c.stream));
   PG_HIP(hipMemsetAsync(c.flags.p, 0, 4 * N_FLAGS, c.stream));
 }
@@ -1159,25 +1197,29 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
     int* hint = c.k3_hint.as<int>();
     if (c.k3_ref >= 0 && !(dbg & 256)) {
       // coverage pass, then the dense work pass over the queued segments
-      const uint64_t max_items = c.windows_fw / IW + c.n_records + 1;
-      c.k3_queue.reserve(sizeof(WorkItem) * max_items + 64);
+      const uint64_t qcap = (ntiles + NQ - 1) / NQ * IBLOCK;       // per sub-queue
+      const uint64_t max_items = std::min<uint64_t>(NQ * qcap, c.windows_fw / IW + c.n_records + 1);
+      const size_t qbytes = sizeof(WorkItem) * NQ * qcap;
+      c.k3_queue.reserve(qbytes + 8 * QSTRIDE * NQ);
       auto* q = c.k3_queue.as<WorkItem>();
-      auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + sizeof(WorkItem) * max_items);
-      PG_HIP(hipMemsetAsync(qn, 0, 8, c.stream));
-      hipLaunchKernelGGL((k_insert<true, true>), g, b, 0, c.stream, cls, td, q, qn, c.k, shift, c.tv, flags, c.k3_ref,
-                         rfs, rfn, hint, dbg);
+      auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
+      PG_HIP(hipMemsetAsync(qn, 0, 8 * QSTRIDE * NQ, c.stream));
+      hipLaunchKernelGGL((k_insert<true, true>), g, b, 0, c.stream, cls, td, q, qn, (unsigned long long)qcap, c.k,
+                         shift, c.tv, flags, c.k3_ref, rfs, rfn, hint, dbg);
       PG_HIP(hipGetLastError());
       const unsigned gw = grid_for(max_items, IBLOCK, 16384);
       if (rc0)
-        hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, c.stream, cls, q, qn, c.k, shift, c.tv, flags, dbg);
+        hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, c.stream, cls, q, qn, (unsigned long long)qcap, c.k,
+                           shift, c.tv, flags, dbg);
       else
-        hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, c.stream, cls, q, qn, c.k, shift, c.tv, flags, dbg);
+        hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, c.stream, cls, q, qn, (unsigned long long)qcap,
+                           c.k, shift, c.tv, flags, dbg);
     } else if (rc0) {
-      hipLaunchKernelGGL((k_insert<true, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, c.k, shift, c.tv, flags,
-                         c.k3_ref, rfs, rfn, hint, dbg);
+      hipLaunchKernelGGL((k_insert<true, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, 0ull, c.k, shift,
+                         c.tv, flags, c.k3_ref, rfs, rfn, hint, dbg);
     } else {
-      hipLaunchKernelGGL((k_insert<false, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, c.k, shift, c.tv,
-                         flags, c.k3_ref, rfs, rfn, hint, dbg);
+      hipLaunchKernelGGL((k_insert<false, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, 0ull, c.k, shift,
+                         c.tv, flags, c.k3_ref, rfs, rfn, hint, dbg);
     }
   }
   PG_HIP(hipGetLastError());

@@ -190,7 +190,7 @@ inline TableView make_geometry(int k, uint64_t keys, uint64_t& buckets, uint64_t
   for (int i = 0; i < k; ++i) maxkey *= 5;
   const int kb = std::max(1, log2u(maxkey));                 // keys < 5^k <= 2^kb
   // keys per bucket target (PG_BUCKET_LOAD, development knob)
-  static const double load = getenv("PG_BUCKET_LOAD") ? atof(getenv("PG_BUCKET_LOAD")) : 0.25;
+  static const double load = getenv("PG_BUCKET_LOAD") ? atof(getenv("PG_BUCKET_LOAD")) : 0.5;
   const uint64_t want = (uint64_t)((double)keys / (load > 0.05 ? load : 0.5));
   const int bb = std::max({kb - 38, log2u(std::max<uint64_t>(want, 1)), 11});   // >= 2048 buckets
   buckets = 1ull << bb;
