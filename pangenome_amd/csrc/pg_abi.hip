@@ -76,6 +76,8 @@ void pg_destroy(pg_ctx* x) {
                         &c.rdbg_keys, &c.tiles, &c.groups, &c.k3_hint, &c.tile_desc, &c.k3_queue, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
                         &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload, &c.dump_cnt};
   for (auto* b : bufs) b->release();
+  c.rec_pack.release();
+  c.h_pin.release();
   c.t0.destroy();
   c.t1.destroy();
   (void)hipStreamDestroy(c.stream);

@@ -401,8 +401,18 @@ template <bool RC, bool EMIT>
 __global__ void __launch_bounds__(IBLOCK)
 k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
          unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift, TableView T,
-         unsigned* __restrict__ flags, int ref, long long rfs, long long rfn, int* __restrict__ hints, int dbg) {
+         unsigned* __restrict__ flags, int ref, long long rfs, long long rfn, int* __restrict__ hints,
+         uint4* __restrict__ zero, uint64_t zero_n16, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
+  if (EMIT) {
+    // the coverage pass never touches the table, and the work pass that fills
+    // it starts after this kernel: the table clear rides along here (its
+    // stores overlap the pass's load latency instead of a separate sweep)
+    const uint64_t per = (zero_n16 + gridDim.x - 1) / gridDim.x;
+    const uint64_t z0 = blockIdx.x * per, z1 = z0 + per < zero_n16 ? z0 + per : zero_n16;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    for (uint64_t i = z0 + threadIdx.x; i < z1; i += IBLOCK) zero[i] = z;
+  }
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ unsigned s_best[NANCH];
   const TileDesc td = descs[xcd_swizzle(blockIdx.x, gridDim.x)];   // one dependent load per block
@@ -822,11 +832,14 @@ void merge_preload(Ctx& c, unsigned* flags) {
 
 // K5: degree scan.  The table is swept as 16-byte elements (a primary bucket
 // = two words, or one overflow slot), RU per thread per 16 KiB unit, with
-// 16-byte loads.  A unit's members (at most 4 per element) are block-scanned
-// into an LDS stage of RCAP keys; the stage goes out with ONE global atomic
-// per flush — a single device counter takes ~90 returning atomics per us, so
-// per-tile atomics would cost more than the sweep itself.
+// 16-byte loads and the next unit in flight.  A unit's members (at most 4 per
+// element) are block-scanned into an LDS stage of RCAP keys; the stage goes
+// out with ONE global atomic per flush — a single device counter takes ~80
+// returning atomics per us (tools/rates.hip), so per-unit atomics would cost
+// more than the sweep itself, and the grid is kept to RGRID persistent blocks
+// (their final flushes all meet that counter at the end).
 constexpr int RT = 256, RU = 2;
+constexpr unsigned RGRID = 4096;                   // RU = 4 on 1024 blocks measured slower (0.29 vs 0.26 ms)
 constexpr uint64_t RUNIT = (uint64_t)RT * RU;
 constexpr int RCAP = 4 * (int)RUNIT;               // a whole unit always fits an empty stage
 
@@ -934,7 +947,7 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
   if (threadIdx.x == 0) {
     unsigned long long t = 0;
     for (int w = 0; w < RT / 64; ++w) t += red[w];
-    if (t) atomicAdd(counters + 8, t);
+    if (t) atomicAdd(counters + 8 * (1 + blockIdx.x % 64), t);   // 64 spread lines
   }
 }
 
@@ -1038,10 +1051,13 @@ __global__ void __launch_bounds__(256) k_zero16(uint4* __restrict__ p, uint64_t 
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256ull) p[i] = z;
 }
 
-static void clear_table(Ctx& c) {
-  hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, c.stream,
-                     reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
-  PG_HIP(hipGetLastError());
+// primary = false: the K3 coverage pass clears the primary buckets itself
+static void clear_table(Ctx& c, bool primary) {
+  if (primary) {
+    hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, c.stream,
+                       reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
+    PG_HIP(hipGetLastError());
+  }
   PG_HIP(hipMemsetAsync(c.ovf.p, 0, sizeof(Slot) * c.ovf_cap, c.stream));
   PG_HIP(hipMemsetAsync(c.flags.p, 0, 4 * N_FLAGS, c.stream));
 }
@@ -1050,9 +1066,10 @@ static uint64_t n_entries(const Ctx& c) { return 2 * c.cap + c.ovf_cap; }
 
 // read back [sentinel, overflow, sum of spread counters]
 static void read_flags(Ctx& c, unsigned& sentinel, unsigned& overflow, uint64_t& created) {
-  std::vector<unsigned> f(N_FLAGS);
-  PG_HIP(hipMemcpyAsync(f.data(), c.flags.p, 4 * f.size(), hipMemcpyDeviceToHost, c.stream));
+  c.h_pin.reserve(4 * N_FLAGS);
+  PG_HIP(hipMemcpyAsync(c.h_pin.p, c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost, c.stream));
   c.sync();
+  const unsigned* f = c.h_pin.as<unsigned>();
   sentinel = f[0];
   overflow = f[1];
   created = 0;
@@ -1179,6 +1196,9 @@ static int k3_mode(const Ctx& c, const std::vector<uint8_t>& flag) {
   return n >= (uint64_t)GG ? 1 : 0;
 }
 
+// the coverage pass + work pass form of k_insert (needs the lead record)
+static bool two_pass(const Ctx& c, uint64_t ntiles, int dbg) { return ntiles && c.k3_ref >= 0 && !(dbg & 256); }
+
 static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t shift, unsigned* flags, int dbg) {
   const dim3 g((unsigned)ntiles), b(IBLOCK);
   const uint8_t* cls = c.cls.as<uint8_t>();
@@ -1195,7 +1215,7 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
     const long long rfs = c.k3_ref >= 0 ? c.h_rec_start[c.k3_ref] : 0, rfn = c.k3_ref >= 0 ? c.h_rec_len[c.k3_ref] : 0;
     const TileDesc* td = c.tile_desc.as<TileDesc>();
     int* hint = c.k3_hint.as<int>();
-    if (c.k3_ref >= 0 && !(dbg & 256)) {
+    if (two_pass(c, ntiles, dbg)) {
       // coverage pass, then the dense work pass over the queued segments
       const uint64_t qcap = (ntiles + NQ - 1) / NQ * IBLOCK;       // per sub-queue
       const uint64_t max_items = std::min<uint64_t>(NQ * qcap, c.windows_fw / IW + c.n_records + 1);
@@ -1205,7 +1225,8 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
       PG_HIP(hipMemsetAsync(qn, 0, 8 * QSTRIDE * NQ, c.stream));
       hipLaunchKernelGGL((k_insert<true, true>), g, b, 0, c.stream, cls, td, q, qn, (unsigned long long)qcap, c.k,
-                         shift, c.tv, flags, c.k3_ref, rfs, rfn, hint, dbg);
+                         shift, c.tv, flags, c.k3_ref, rfs, rfn, hint, reinterpret_cast<uint4*>(c.table.p),
+                         (uint64_t)c.cap, dbg);
       PG_HIP(hipGetLastError());
       const unsigned gw = grid_for(max_items, IBLOCK, 16384);
       if (rc0)
@@ -1216,10 +1237,10 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
                            c.k, shift, c.tv, flags, dbg);
     } else if (rc0) {
       hipLaunchKernelGGL((k_insert<true, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, 0ull, c.k, shift,
-                         c.tv, flags, c.k3_ref, rfs, rfn, hint, dbg);
+                         c.tv, flags, c.k3_ref, rfs, rfn, hint, nullptr, 0ull, dbg);
     } else {
       hipLaunchKernelGGL((k_insert<false, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, 0ull, c.k, shift,
-                         c.tv, flags, c.k3_ref, rfs, rfn, hint, dbg);
+                         c.tv, flags, c.k3_ref, rfs, rfn, hint, nullptr, 0ull, dbg);
     }
   }
   PG_HIP(hipGetLastError());
@@ -1261,7 +1282,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   for (int attempt = 0; attempt < 8; ++attempt) {
     alloc_table(c, keys);
     c.t0.start(c.stream);
-    clear_table(c);
+    clear_table(c, mode != 0 || !two_pass(c, ntiles, dbg));
     c.t0.stop(c.stream);
     unsigned* flags = c.flags.as<unsigned>();
     c.t1.start(c.stream);
@@ -1304,21 +1325,24 @@ void build_rdbg(Ctx& c) {
   if (!c.built) throw Error(-22, "build_rdbg: no dBG (call pg_build_dbg first)");
   c.rdbg_keys.reserve(8 * (2 * c.n_canon + 2));
   DevBuf& cnt = c.n_sel;
-  cnt.reserve(128);
-  PG_HIP(hipMemsetAsync(cnt.p, 0, 128, c.stream));
+  constexpr size_t CNT_BYTES = 8 * 8 * 65;              // [0] member count, [8 * (1 + i)] dBG size partials
+  cnt.reserve(CNT_BYTES);
+  PG_HIP(hipMemsetAsync(cnt.p, 0, CNT_BYTES, c.stream));
   c.t0.start(c.stream);
   const uint64_t nel = c.cap + c.ovf_cap;               // 16-byte elements: buckets, then overflow slots
-  hipLaunchKernelGGL(k_reduce, dim3(grid_for(nel / RUNIT, 1, 4096)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
+  hipLaunchKernelGGL(k_reduce, dim3(grid_for(nel / RUNIT, 1, RGRID)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
                      c.k, c.rdbg_keys.as<unsigned long long>(), 2 * c.n_canon + 1, cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
   c.t0.stop(c.stream);
-  unsigned long long res[9];
-  PG_HIP(hipMemcpyAsync(res, cnt.p, sizeof(res), hipMemcpyDeviceToHost, c.stream));
+  c.h_pin.reserve(CNT_BYTES);
+  PG_HIP(hipMemcpyAsync(c.h_pin.p, cnt.p, CNT_BYTES, hipMemcpyDeviceToHost, c.stream));
   c.sync();
+  const unsigned long long* res = c.h_pin.as<unsigned long long>();
   c.ms_scan = c.t0.ms();
   if (res[0] > 2 * c.n_canon + 1) throw Error(-5, "build_rdbg: member count exceeds the table's key count");
   c.n_rdbg = res[0];
-  c.n_dbg = res[8];
+  c.n_dbg = 0;
+  for (int i = 0; i < 64; ++i) c.n_dbg += res[8 * (1 + i)];
   if (c.sentinel) {         // key 2^64-1, mask 32: always an rdBG member
     unsigned long long s = SENTINEL;
     PG_HIP(hipMemcpyAsync(c.rdbg_keys.as<unsigned long long>() + c.n_rdbg, &s, 8, hipMemcpyHostToDevice,
@@ -1397,7 +1421,7 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int s
   c.t1.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
     alloc_table(c, keys);
-    clear_table(c);
+    clear_table(c, true);
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
     c.t1.start(c.stream);
     if (n)

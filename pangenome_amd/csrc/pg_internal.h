@@ -48,6 +48,27 @@ struct DevBuf {
   }
 };
 
+// A growable pinned host buffer: device-to-host copies into it are plain DMA
+// on the stream (a pageable destination costs a staged, synchronous copy).
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  void reserve(size_t bytes) {
+    if (bytes <= cap) return;
+    if (p) PG_HIP(hipHostFree(p));
+    p = nullptr;
+    size_t nb = bytes + bytes / 8 + 256;
+    PG_HIP(hipHostMalloc(&p, nb, hipHostMallocDefault));
+    cap = nb;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 // Per-kernel timing on the context's stream (HIP events), so callers can
 // price the dominant kernel against the HBM roofline.
 struct Timer {
@@ -87,6 +108,8 @@ struct Ctx {
   DevBuf rec_flag;                // uint8 per record: take part in the current pass
   DevBuf cls;                     // uint8 per base: class code (records concatenated)
   DevBuf scratch;                 // rocPRIM temp storage
+  DevBuf rec_pack;                // int64 [5][R]: the record table gathered for one copy
+  PinBuf h_pin;                   // pinned staging for small device-to-host reads
   uint64_t n_lines = 0, n_records = 0, n_bases = 0, n_nl = 0;
   std::vector<int64_t> h_rec_start, h_rec_len, h_rec_hdr_start, h_rec_hdr_len, h_rec_ptr;
   bool parsed = false;

@@ -340,6 +340,19 @@ static void upload_byte_class() {
   done = true;
 }
 
+// the five per-record arrays side by side, for one device-to-host copy
+__global__ void k_pack_records(uint64_t R, const long long* __restrict__ rs, const long long* __restrict__ rl,
+                               const long long* __restrict__ rp, const long long* __restrict__ hdr,
+                               long long* __restrict__ out) {
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
+    out[r] = rs[r];
+    out[R + r] = rl[r];
+    out[2 * R + r] = rp[r];
+    out[3 * R + r] = hdr[r];
+    out[4 * R + r] = hdr[R + r];
+  }
+}
+
 void parse_fasta(Ctx& c) {
   upload_byte_class();
   hipStream_t st = c.stream;
@@ -363,9 +376,10 @@ void parse_fasta(Ctx& c) {
   c.scratch.reserve(bytes + 16);
   bytes = c.scratch.cap;
   PG_HIP(rocprim::inclusive_scan(c.scratch.p, bytes, fns, incl, (size_t)nspan, FnThen{}, st));
-  Fn tot;
-  PG_HIP(hipMemcpyAsync(&tot, incl + nspan - 1, sizeof tot, hipMemcpyDeviceToHost, st));
+  c.h_pin.reserve(sizeof(Fn));
+  PG_HIP(hipMemcpyAsync(c.h_pin.p, incl + nspan - 1, sizeof(Fn), hipMemcpyDeviceToHost, st));
   c.sync();
+  const Fn tot = *c.h_pin.as<Fn>();
   c.n_nl = tot.nl;
   if (tot.nl == 0) { c.parsed = true; return; }             // no line at all (:126-132)
   // the unterminated last line counts when end > start > 0 (:131)
@@ -388,15 +402,22 @@ void parse_fasta(Ctx& c) {
     hipLaunchKernelGGL(k_records, dim3(grid_for(R, 256)), dim3(256), 0, st, R, tot.c0, last_line_start,
                        c.rec_start.as<long long>(), c.rec_len.as<long long>(), hdr, c.rec_ptr.as<long long>());
     PG_HIP(hipGetLastError());
-    c.h_rec_start.resize(R); c.h_rec_len.resize(R); c.h_rec_ptr.resize(R);
-    c.h_rec_hdr_start.resize(R); c.h_rec_hdr_len.resize(R);
-    PG_HIP(hipMemcpyAsync(c.h_rec_start.data(), c.rec_start.p, 8 * R, hipMemcpyDeviceToHost, st));
-    PG_HIP(hipMemcpyAsync(c.h_rec_len.data(), c.rec_len.p, 8 * R, hipMemcpyDeviceToHost, st));
-    PG_HIP(hipMemcpyAsync(c.h_rec_ptr.data(), c.rec_ptr.p, 8 * R, hipMemcpyDeviceToHost, st));
-    PG_HIP(hipMemcpyAsync(c.h_rec_hdr_start.data(), hdr, 8 * R, hipMemcpyDeviceToHost, st));
-    PG_HIP(hipMemcpyAsync(c.h_rec_hdr_len.data(), hdr + R, 8 * R, hipMemcpyDeviceToHost, st));
+    c.rec_pack.reserve(40 * R);
+    c.h_pin.reserve(40 * R);
+    hipLaunchKernelGGL(k_pack_records, dim3(grid_for(R, 256, 1024)), dim3(256), 0, st, R, c.rec_start.as<long long>(),
+                       c.rec_len.as<long long>(), c.rec_ptr.as<long long>(), hdr, c.rec_pack.as<long long>());
+    PG_HIP(hipGetLastError());
+    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 40 * R, hipMemcpyDeviceToHost, st));
   }
   c.sync();
+  if (R) {
+    const int64_t* pk = c.h_pin.as<int64_t>();
+    c.h_rec_start.assign(pk, pk + R);
+    c.h_rec_len.assign(pk + R, pk + 2 * R);
+    c.h_rec_ptr.assign(pk + 2 * R, pk + 3 * R);
+    c.h_rec_hdr_start.assign(pk + 3 * R, pk + 4 * R);
+    c.h_rec_hdr_len.assign(pk + 4 * R, pk + 5 * R);
+  }
   uint64_t nb = 0;
   for (uint64_t r = 0; r < R; ++r) nb += (uint64_t)c.h_rec_len[r];
   c.n_bases = nb;
