@@ -61,6 +61,7 @@ int pg_create(pg_ctx** out, int device, int k) {
     x->c.device = device;
     x->c.k = k < 1 ? 1 : (k > 27 ? 27 : k);
     PG_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
+    PG_HIP(hipDeviceGetAttribute(&x->c.n_cu, hipDeviceAttributeMultiprocessorCount, device));
     *out = x;
   });
 }
@@ -73,7 +74,7 @@ void pg_destroy(pg_ctx* x) {
   pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.n_sel, &c.rec_start,
                         &c.rec_len, &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.ovf,
                         &c.flags,
-                        &c.rdbg_keys, &c.tiles, &c.groups, &c.k3_hint, &c.tile_desc, &c.k3_queue, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
+                        &c.rdbg_keys, &c.tiles, &c.groups, &c.tile_desc, &c.k3_queue, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
                         &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload, &c.dump_cnt};
   for (auto* b : bufs) b->release();
   c.rec_pack.release();

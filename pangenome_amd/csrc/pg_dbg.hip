@@ -19,6 +19,7 @@
 // stripe's tiles run on one XCD: the first genome's probe of a bucket misses,
 // the other genomes' probes of it hit that XCD's L2 / the Infinity Cache.
 #include <algorithm>
+#include <type_traits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -239,7 +240,6 @@ constexpr int DRIFT = 512;                    // searched offsets: [-DRIFT, DRIF
 constexpr int RSPAN = TILE + 2 * DRIFT + 96;  // staged reference bytes
 constexpr int NANCH = 3;                      // anchors per tile
 constexpr int ALEN = 32;                      // anchor length (bytes)
-constexpr int HINTW = 8;                      // first search: +-HINTW around the record's last drift
 
 // bit j of the result: byte j of a equals byte j of b (ND dwords)
 template <int ND>
@@ -382,164 +382,316 @@ __device__ __forceinline__ void insert_segment(const uint8_t* s_cls, long long b
 // table in batches of IB windows: IB independent bucket loads in flight per
 // lane, and only windows whose entry is not already complete take the CAS /
 // atomicOr / overflow path.
-// A segment left with work after the coverage pass (k_insert<.., true>).
+// A segment left with work after the coverage pass (k_cover).
 struct WorkItem {
   long long rs, last, q0;
   uint32_t covered, pad;
 };
 
 // The queue is NQ sub-queues, each with its own counter on its own 64-byte
-// line; block b appends to sub-queue b % NQ.  One counter shared by all
-// ~120 K blocks of a C3 launch serialises their atomics at the memory side
+// line; a tile appends to sub-queue (its block) % NQ.  One counter shared by
+// all ~120 K tiles of a C3 launch serialises their atomics at the memory side
 // (1.48 ms measured, tools/rates.hip) - as long as the whole coverage pass;
-// 64 counters take 0.045 ms.  A block appends at most IBLOCK items, so
-// sub-queue capacity = ceil(grid / NQ) * IBLOCK.
+// 64 counters take 0.045 ms.  A tile appends at most IBLOCK items.
 constexpr int NQ = 64;
 constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long long words)
 
-template <bool RC, bool EMIT>
-__global__ void __launch_bounds__(IBLOCK)
-k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
-         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift, TableView T,
-         unsigned* __restrict__ flags, int ref, long long rfs, long long rfn, int* __restrict__ hints,
-         uint4* __restrict__ zero, uint64_t zero_n16, int dbg) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
-  if (EMIT) {
-    // the coverage pass never touches the table, and the work pass that fills
-    // it starts after this kernel: the table clear rides along here (its
-    // stores overlap the pass's load latency instead of a separate sweep)
-    const uint64_t per = (zero_n16 + gridDim.x - 1) / gridDim.x;
-    const uint64_t z0 = blockIdx.x * per, z1 = z0 + per < zero_n16 ? z0 + per : zero_n16;
-    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-    for (uint64_t i = z0 + threadIdx.x; i < z1; i += IBLOCK) zero[i] = z;
+// Drift of the tile's record against a reference record at NANCH anchors:
+// s_best[a] = (|delta| << 16) | (delta + DRIFT) of the smallest |delta| in
+// [-DRIFT, DRIFT] whose ALEN bytes match, ~0u if none.  The search is
+// dword-parallel: a task is one reference dword w (4 candidate starts), whose
+// shifted words are compared with the anchor's first 4 bytes (the stream is
+// ~2 bits per byte, so ~1 in 256 candidates passes) before the full ALEN-byte
+// check.  Per anchor (its geometry block-uniform, so scalar) one dword task
+// per thread (two for the first few), ~20 VALU; the earlier per-offset search
+// (a stale per-record hint first, then 1025 offsets per anchor at ~35 VALU
+// each) made the coverage pass VALU-bound (0.28 of its 0.81 ms,
+// PG_K3_DBG=512).  Ends with a block barrier.
+constexpr int ASTEP = (TILE - ALEN - 16) / (NANCH - 1);      // anchor spacing
+__device__ __forceinline__ void find_drift(const uint8_t* s_cls, long long base, const uint8_t* s_ref,
+                                           long long rbase, long long qt, long long rn, long long plo,
+                                           long long phi, unsigned* s_best) {
+  constexpr int NW = (2 * DRIFT + 3) / 4 + 2;                 // dword tasks per anchor
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
+#pragma unroll 1
+  for (int ai = 0; ai < NANCH; ++ai) {
+    const long long a = qt + 8 + (long long)ai * ASTEP;       // anchor: record positions [a, a + ALEN)
+    if (a + ALEN > rn) continue;
+    const int ia = (int)(base + a);                           // its s_cls index
+    const int ibhi = (int)(rbase + a + DRIFT);                // s_ref index of its match at delta = -DRIFT
+    const int lo = max(ibhi - 2 * DRIFT, (int)(rbase + plo)), hi = min(ibhi, (int)(rbase + phi) - ALEN);
+    uint32_t A1[1];
+    lds_bytes(s_cls, (uint32_t)ia, A1);                       // one address: a broadcast read
+    for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += IBLOCK) {
+      const uint32_t W0 = rw[w], W1 = rw[w + 1];
+#pragma unroll
+      for (int sb = 0; sb < 4; ++sb) {
+        const int ib = 4 * w + sb;
+        if (ib < lo || ib > hi || __builtin_amdgcn_alignbyte(W1, W0, sb) != A1[0]) continue;
+        uint32_t A[ALEN / 4], B[ALEN / 4];
+        lds_bytes(s_cls, (uint32_t)ia, A);
+        lds_bytes(s_ref, (uint32_t)ib, B);
+        bool eq = true;
+#pragma unroll
+        for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
+        const int d = ibhi - ib;                              // delta + DRIFT
+        const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+        if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
+      }
+    }
   }
+  __syncthreads();
+}
+
+// Covered windows of the interior segment q0 .. q0+IW-1 (bit i: window q0+i):
+// its bytes [q-1, q+k] equal the reference's at q - delta for one of the
+// anchors' drifts (reference window interior and staged too).
+__device__ __forceinline__ uint32_t segment_covered(const uint8_t* s_cls, long long base, const uint8_t* s_ref,
+                                                    long long rbase, long long q0, int k, long long rfn,
+                                                    long long plo, long long phi, const unsigned* s_best) {
+  const uint32_t o = (uint32_t)(base + q0);
+  constexpr int NB = (IW + 27 + 1 + 3) / 4;                  // bytes q0-1 .. q0+IW+k-1, k <= 27
+  uint32_t G[NB];
+  lds_bytes(s_cls, o - 1, G);
+  uint32_t covered = 0;
+  unsigned prev = ~0u;
+  for (int ai = 0; ai < NANCH; ++ai) {
+    const unsigned b = s_best[ai];
+    if (b == ~0u || (b & 0xFFFFu) == prev) continue;
+    prev = b & 0xFFFFu;
+    const long long p0 = q0 - ((long long)(b & 0xFFFFu) - DRIFT);   // reference window of q0
+    if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
+    uint32_t Rw[NB];
+    lds_bytes(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) diff |= G[i] ^ Rw[i];
+    if (diff == 0) return (1u << IW) - 1u;                    // the common case: all context bytes equal
+    covered |= (uint32_t)(run_and(byte_eq_bits(G, Rw), k + 2) & ((1u << IW) - 1u));
+  }
+  return covered;
+}
+
+// 4*ND bytes of LDS from byte index idx through 16-byte reads (ds_read_b128:
+// lanes 16 B apart hit distinct banks, where the dword reads of lds_bytes are
+// 4-way conflicted), realigned in registers.  idx & 15 must be the same for
+// every lane of the wave (it selects the shift by a uniform branch).
+template <int ND>
+__device__ __forceinline__ void lds_bytes16(const uint8_t* s, uint32_t idx, uint32_t (&out)[ND]) {
+  constexpr int NW = ((ND + 3) / 4 + 1) * 4;       // dwords read: ceil(ND/4)+1 chunks of 16 B
+  uint32_t raw[NW];
+  const uint32_t a = idx & ~15u;
+#pragma unroll
+  for (int q = 0; q < NW / 4; ++q) {
+    const uint4 v = *reinterpret_cast<const uint4*>(s + a + 16u * q);
+    raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
+  }
+  const uint32_t sb = idx & 3u;
+  auto take = [&](auto W) {
+    constexpr int w = decltype(W)::value;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) out[i] = __builtin_amdgcn_alignbyte(raw[w + i + 1], raw[w + i], sb);
+  };
+  switch ((idx >> 2) & 3u) {
+    case 0: take(std::integral_constant<int, 0>{}); break;
+    case 1: take(std::integral_constant<int, 1>{}); break;
+    case 2: take(std::integral_constant<int, 2>{}); break;
+    default: take(std::integral_constant<int, 3>{}); break;
+  }
+}
+
+// segment_covered with conflict-free 16-byte LDS reads (lds_bytes16): the
+// segment start q0 - 1 has the same alignment in every lane of a tile
+// (segments are IW = 16 windows apart), and so does its reference window.
+__device__ __forceinline__ uint32_t segment_covered16(const uint8_t* s_cls, long long base, const uint8_t* s_ref,
+                                                      long long rbase, long long q0, int k, long long rfn,
+                                                      long long plo, long long phi, const unsigned* s_best) {
+  static_assert(IW == 16, "uniform 16-byte alignment of segment starts");
+  constexpr int NB = (IW + 27 + 1 + 3) / 4;                  // bytes q0-1 .. q0+IW+k-1, k <= 27
+  uint32_t G[NB];
+  lds_bytes16(s_cls, (uint32_t)(base + q0 - 1), G);
+  uint32_t covered = 0;
+  unsigned prev = ~0u;
+  for (int ai = 0; ai < NANCH; ++ai) {
+    const unsigned b = s_best[ai];
+    if (b == ~0u || (b & 0xFFFFu) == prev) continue;
+    prev = b & 0xFFFFu;
+    const long long p0 = q0 - ((long long)(b & 0xFFFFu) - DRIFT);   // reference window of q0
+    if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
+    uint32_t Rw[NB];
+    lds_bytes16(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
+    uint32_t diff = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) diff |= G[i] ^ Rw[i];
+    if (diff == 0) return (1u << IW) - 1u;                    // the common case: all context bytes equal
+    covered |= (uint32_t)(run_and(byte_eq_bits(G, Rw), k + 2) & ((1u << IW) - 1u));
+  }
+  return covered;
+}
+
+// Staging geometry of tile (record [rs, rs+rn), stripe): class positions
+// [lo, hi) from the 16-byte aligned a0 (windows qt .. qt+TILE-1 read from q-2,
+// the last-window pred, to q+k+1, the twin pred of window 0), and the
+// reference positions [plo, phi) = this stripe +- DRIFT from ra0.
+struct Stage {
+  long long qt, a0, hi, plo, phi, ra0, rend;
+};
+// the reference span of stripe qt (record [rfs, rfs + rfn))
+__device__ __forceinline__ void ref_span(Stage& g, int k, long long rfs, long long rfn) {
+  g.plo = g.qt - 1 - DRIFT > 0 ? g.qt - 1 - DRIFT : 0;
+  g.phi = g.qt + TILE + k + 1 + DRIFT < rfn ? g.qt + TILE + k + 1 + DRIFT : rfn;
+  g.ra0 = (rfs + g.plo) & ~15ll;
+  g.rend = rfs + g.phi;
+}
+__device__ __forceinline__ Stage stage_of(const TileDesc& td, int k, bool dedup, long long rfs, long long rfn) {
+  Stage g;
+  g.qt = (long long)td.stripe * TILE;
+  const long long lo = td.rs + (g.qt >= 2 ? g.qt - 2 : 0);
+  g.hi = td.rs + (g.qt + TILE + k + 2 < td.rn ? g.qt + TILE + k + 2 : td.rn);
+  g.a0 = lo & ~15ll;
+  g.plo = g.phi = g.ra0 = g.rend = 0;
+  if (dedup) ref_span(g, k, rfs, rfn);
+  return g;
+}
+
+// K3 (fused form: PG_K3_DBG=256 or no reference).  One block per tile
+// (record, stripe j): windows [j*TILE, (j+1)*TILE) of a record with n >= k+2.
+// The tile's class codes (plus the k+3 bytes of context around it) are
+// staged in LDS with 16-byte loads; thread t takes IW consecutive windows,
+// rolls both strands' keys across them, and probes the table in batches of
+// IB windows: IB independent bucket loads in flight per lane, and only
+// windows whose entry is not already complete take the CAS / atomicOr /
+// overflow path.  Segments fully covered by the reference record send
+// nothing; the rest are compacted so that only they run insert_segment.
+template <bool RC>
+__global__ void __launch_bounds__(IBLOCK)
+k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, int k, uint64_t shift, TableView T,
+         unsigned* __restrict__ flags, int ref, long long rfs, long long rfn, int dbg) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ unsigned s_best[NANCH];
+  __shared__ uint32_t s_work[IBLOCK];
+  __shared__ uint32_t s_scan[IBLOCK / 64];
   const TileDesc td = descs[xcd_swizzle(blockIdx.x, gridDim.x)];   // one dependent load per block
   const int r = td.r;
   const long long rs = td.rs, rn = td.rn;
   const long long last = rn - k;                              // last window index
-  const long long qt = (long long)td.stripe * TILE;
-  const int hint = ref >= 0 && ref != r ? hints[r] : -1;     // in flight with the staging loads
-  // stage positions [lo, hi) of the record: windows qt .. qt+TILE-1 read from
-  // q-2 (last-window pred) to q+k+1 (twin pred of window 0)
-  const long long lo = rs + (qt >= 2 ? qt - 2 : 0);
-  const long long hi = rs + (qt + TILE + k + 2 < rn ? qt + TILE + k + 2 : rn);
-  const long long a0 = lo & ~15ll;                            // 16-byte aligned source
-  for (long long off = (long long)threadIdx.x * 16; a0 + off < hi; off += IBLOCK * 16)
-    *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + a0 + off);
-  // the reference record's positions [plo, phi): this stripe +- DRIFT
   const bool dedup = ref >= 0 && ref != r && !(dbg & 32);    // block-uniform
-  long long plo = 0, phi = 0, rbase = 0;
+  const Stage g = stage_of(td, k, dedup, rfs, rfn);
+  for (long long off = (long long)threadIdx.x * 16; g.a0 + off < g.hi; off += IBLOCK * 16)
+    *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + g.a0 + off);
   if (dedup) {
-    plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
-    phi = qt + TILE + k + 1 + DRIFT < rfn ? qt + TILE + k + 1 + DRIFT : rfn;
-    const long long ra0 = (rfs + plo) & ~15ll;
-    rbase = rfs - ra0;                                        // s_ref index of reference position 0
-    for (long long off = (long long)threadIdx.x * 16; ra0 + off < rfs + phi; off += IBLOCK * 16)
-      *reinterpret_cast<uint4*>(s_ref + off) = *reinterpret_cast<const uint4*>(cls + ra0 + off);
+    for (long long off = (long long)threadIdx.x * 16; g.ra0 + off < g.rend; off += IBLOCK * 16)
+      *reinterpret_cast<uint4*>(s_ref + off) = *reinterpret_cast<const uint4*>(cls + g.ra0 + off);
     if (threadIdx.x < NANCH) s_best[threadIdx.x] = ~0u;
   }
   __syncthreads();
-  const long long base = rs - a0;                             // s_cls index of record position 0
-  if (dedup) {
-    // drift at NANCH anchors: the smallest |delta| whose ALEN bytes match.
-    // First +-HINTW around the drift this record's previous stripe found
-    // (hint[r]; a stale or racy hint only costs the full search), then all
-    // of [-DRIFT, DRIFT] for anchors still without a match.
-    auto anchor = [&](int ai) { return qt + 8 + (long long)ai * ((TILE - ALEN - 16) / (NANCH - 1)); };
-    auto try_d = [&](int ai, int d) {
-      const long long a = anchor(ai), p = a - (d - DRIFT);
-      if (a + ALEN > rn || d < 0 || d > 2 * DRIFT || p < plo || p + ALEN > phi) return;
-      uint32_t A1[1], B1[1];
-      lds_bytes(s_cls, (uint32_t)(base + a), A1);
-      lds_bytes(s_ref, (uint32_t)(rbase + p), B1);
-      if (B1[0] != A1[0]) return;
-      uint32_t A[ALEN / 4], B[ALEN / 4];
-      lds_bytes(s_cls, (uint32_t)(base + a), A);
-      lds_bytes(s_ref, (uint32_t)(rbase + p), B);
-      bool eq = true;
-#pragma unroll
-      for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
-      const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
-      if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
-    };
-    if (hint >= 0 && threadIdx.x < NANCH * (2 * HINTW + 1))
-      try_d((int)threadIdx.x / (2 * HINTW + 1), hint - HINTW + (int)threadIdx.x % (2 * HINTW + 1));
-    __syncthreads();
-    for (int ai = 0; ai < NANCH; ++ai) {
-      if (s_best[ai] != ~0u) continue;                        // block-uniform
-      for (int d = threadIdx.x; d <= 2 * DRIFT; d += IBLOCK) try_d(ai, d);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int h = -1;
-      for (int ai = NANCH - 1; ai >= 0; --ai)
-        if (s_best[ai] != ~0u) h = (int)(s_best[ai] & 0xFFFFu);
-      if (h >= 0) hints[r] = h;
-    }
-  }
-
-  // Phase A: thread t owns segment t (windows qt + t*IW ..).  With a
-  // reference, an interior segment learns which of its windows are covered;
-  // segments left with work are compacted so that phase B runs only them.
-  __shared__ uint32_t s_work[IBLOCK];
-  __shared__ uint32_t s_scan[IBLOCK / 64];
+  const long long base = rs - g.a0, rbase = rfs - g.ra0;      // LDS index of record position 0
+  if (dedup) find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, s_best);
   uint32_t covered = 0;
   unsigned created_acc = 0;
-  {
-    const long long q0 = qt + (long long)threadIdx.x * IW;
-    if (dedup && q0 > 0 && q0 + IW <= last) {
-      const uint32_t o = (uint32_t)(base + q0);
-      constexpr int NB = (IW + 27 + 1 + 3) / 4;              // bytes q0-1 .. q0+IW+k-1, k <= 27
-      uint32_t G[NB];
-      lds_bytes(s_cls, o - 1, G);
-      unsigned prev = ~0u;
-      for (int ai = 0; ai < NANCH; ++ai) {
-        const unsigned b = s_best[ai];
-        if (b == ~0u || (b & 0xFFFFu) == prev) continue;
-        prev = b & 0xFFFFu;
-        const long long p0 = q0 - ((long long)(b & 0xFFFFu) - DRIFT);   // reference window of q0
-        // reference windows p0 .. p0+IW-1 interior, and their bytes staged
-        if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
-        uint32_t Rw[NB];
-        lds_bytes(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
-        uint32_t diff = 0;
-#pragma unroll
-        for (int i = 0; i < NB; ++i) diff |= G[i] ^ Rw[i];
-        if (diff == 0) { covered = (1u << IW) - 1u; break; }  // the common case: all context bytes equal
-        covered |= (uint32_t)(run_and(byte_eq_bits(G, Rw), k + 2) & ((1u << IW) - 1u));
-      }
-    }
-    if (dbg & 128) covered = (1u << IW) - 1u;      // dev knob: prologue + coverage only
-    const bool work = q0 <= last && covered != (1u << IW) - 1u;
-    uint32_t nwork;
-    const uint32_t pos = block_excl_scan<IBLOCK>(work ? 1u : 0u, s_scan, nwork);
-    if (EMIT) {                                    // to the queue: k_insert_work runs them densely
-      __shared__ unsigned long long s_qbase;
-      const unsigned sub = blockIdx.x % NQ;
-      if (threadIdx.x == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
-      __syncthreads();
-      if (work) queue[sub * qcap + s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
-      return;                                      // no barrier follows
-    }
-    if (work) s_work[pos] = threadIdx.x | (covered << 16);
-    if ((dbg & 64) && threadIdx.x == 0) {         // dev knob: segments with work / with windows
-      atomicAdd(flags + 16 * (2 + N_CNT) + 8, nwork);
-      atomicAdd(flags + 16 * (2 + N_CNT) + 9, (unsigned)(dedup ? 1 : 0));
-    }
-    if ((dbg & 64) && q0 <= last) {
-      atomicAdd(flags + 16 * (2 + N_CNT) + 10, 1u);
-      atomicAdd(flags + 16 * (2 + N_CNT) + 11, (unsigned)__builtin_popcount(covered));
-    }
-    __syncthreads();
-    if (threadIdx.x < nwork) {
-      covered = s_work[threadIdx.x] >> 16;
-      insert_segment<RC>(s_cls, base, qt + (long long)(s_work[threadIdx.x] & 0xFFFFu) * IW, last, k, shift, T,
-                         flags, covered, dbg, created_acc);
-    }
+  const long long q0 = g.qt + (long long)threadIdx.x * IW;
+  if (dedup && q0 > 0 && q0 + IW <= last)
+    covered = segment_covered(s_cls, base, s_ref, rbase, q0, k, rfn, g.plo, g.phi, s_best);
+  const bool work = q0 <= last && covered != (1u << IW) - 1u;
+  uint32_t nwork;
+  const uint32_t pos = block_excl_scan<IBLOCK>(work ? 1u : 0u, s_scan, nwork);
+  if (work) s_work[pos] = threadIdx.x | (covered << 16);
+  if ((dbg & 64) && threadIdx.x == 0) {           // dev knob: segments with work / with windows
+    atomicAdd(flags + 16 * (2 + N_CNT) + 8, nwork);
+    atomicAdd(flags + 16 * (2 + N_CNT) + 9, (unsigned)(dedup ? 1 : 0));
+  }
+  if ((dbg & 64) && q0 <= last) {
+    atomicAdd(flags + 16 * (2 + N_CNT) + 10, 1u);
+    atomicAdd(flags + 16 * (2 + N_CNT) + 11, (unsigned)__builtin_popcount(covered));
+  }
+  __syncthreads();
+  if (threadIdx.x < nwork) {
+    covered = s_work[threadIdx.x] >> 16;
+    insert_segment<RC>(s_cls, base, g.qt + (long long)(s_work[threadIdx.x] & 0xFFFFu) * IW, last, k, shift, T,
+                       flags, covered, dbg, created_acc);
   }
   block_count(created_acc, flags);                 // every thread: one barrier per wave
+}
+
+// K3 coverage pass (two-pass form, the default with a lead record).  One
+// block per tile, like k_insert: the drift against the lead (find_drift),
+// each segment's covered windows (segment_covered16), and the segments left
+// with work appended to the queue for k_insert_work.
+// Second reference.  Every follower also differs from the lead at the lead's
+// own variant sites, where all followers share the other allele: with the
+// lead alone those windows were probed once per follower (C3: ~14 M of 51 M
+// probes found their key already there).  So a second record (ref2) is
+// searched too, and a window covered by either reference is skipped.  ref2's
+// own windows are deduped against the lead only; a window it leaves to the
+// lead has the lead's context, key and masks, so "covered by ref2" still
+// means "inserted".
+// The table clear rides along (the pass never touches the table, and the
+// work pass that fills it starts after this kernel): each block zeroes its
+// share after its queue writes.  A persistent, software-pipelined form of
+// this kernel (register prefetch of the next tile) measured slower: 1.02 vs
+// 0.76 ms at 64 VGPRs with spills, against one-tile blocks at 8 waves/SIMD.
+__global__ void __launch_bounds__(IBLOCK)
+k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
+        unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
+        long long rfn, int ref2, long long r2s, long long r2n, uint4* __restrict__ zero, uint64_t zero_n16,
+        int dbg) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ref2[RSPAN];
+  __shared__ unsigned s_best[NANCH], s_best2[NANCH];
+  __shared__ uint32_t s_scan[IBLOCK / 64];
+  __shared__ unsigned long long s_qbase;
+  const TileDesc td = descs[xcd_swizzle(blockIdx.x, gridDim.x)];
+  const long long rs = td.rs, rn = td.rn, last = rn - k;
+  const bool dedup = ref >= 0 && ref != td.r && !(dbg & 32);  // block-uniform
+  const bool dedup2 = dedup && ref2 >= 0 && ref2 != td.r && !(dbg & 16384);
+  const Stage g = stage_of(td, k, dedup, rfs, rfn);
+  Stage g2 = g;
+  if (dedup2) ref_span(g2, k, r2s, r2n);
+  for (long long off = (long long)threadIdx.x * 16; g.a0 + off < g.hi; off += IBLOCK * 16)
+    *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + g.a0 + off);
+  // dev knobs (PG_K3_DBG, timing only): 512 no drift search (delta 0), 1024
+  // no segment compare, 2048 no reference staging, 4096 no queue atomic /
+  // writes, 8192 no table clear, 16384 no second reference
+  if (dedup) {
+    if (!(dbg & 2048))
+      for (long long off = (long long)threadIdx.x * 16; g.ra0 + off < g.rend; off += IBLOCK * 16)
+        *reinterpret_cast<uint4*>(s_ref + off) = *reinterpret_cast<const uint4*>(cls + g.ra0 + off);
+    if (threadIdx.x < NANCH) s_best[threadIdx.x] = (dbg & 512) ? (unsigned)DRIFT : ~0u;
+  }
+  if (dedup2) {
+    for (long long off = (long long)threadIdx.x * 16; g2.ra0 + off < g2.rend; off += IBLOCK * 16)
+      *reinterpret_cast<uint4*>(s_ref2 + off) = *reinterpret_cast<const uint4*>(cls + g2.ra0 + off);
+    if (threadIdx.x < NANCH) s_best2[threadIdx.x] = (dbg & 512) ? (unsigned)DRIFT : ~0u;
+  }
+  __syncthreads();
+  const long long base = rs - g.a0, rbase = rfs - g.ra0, rbase2 = r2s - g2.ra0;   // LDS index of position 0
+  if (dedup && !(dbg & 512)) find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, s_best);
+  if (dedup2 && !(dbg & 512)) find_drift(s_cls, base, s_ref2, rbase2, g.qt, rn, g2.plo, g2.phi, s_best2);
+  const long long q0 = g.qt + (long long)threadIdx.x * IW;
+  constexpr uint32_t ALL = (1u << IW) - 1u;
+  uint32_t covered = 0;
+  if (dedup && q0 > 0 && q0 + IW <= last && !(dbg & 1024)) {
+    covered = segment_covered16(s_cls, base, s_ref, rbase, q0, k, rfn, g.plo, g.phi, s_best);
+    if (dedup2 && covered != ALL)
+      covered |= segment_covered16(s_cls, base, s_ref2, rbase2, q0, k, r2n, g2.plo, g2.phi, s_best2);
+  }
+  if (dbg & 128) covered = ALL;                    // dev knob: prologue + coverage only
+  const bool work = q0 <= last && covered != ALL;
+  uint32_t nwork;
+  const uint32_t pos = block_excl_scan<IBLOCK>(work ? 1u : 0u, s_scan, nwork);
+  const unsigned sub = blockIdx.x % NQ;
+  if (!(dbg & 4096)) {
+    if (threadIdx.x == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
+    __syncthreads();
+    if (work) queue[sub * qcap + s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
+  }
+  if (dbg & 8192) return;
+  const uint64_t per = (zero_n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t z0 = blockIdx.x * per, z1 = z0 + per < zero_n16 ? z0 + per : zero_n16;
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  for (uint64_t i = z0 + threadIdx.x; i < z1; i += IBLOCK) zero[i] = z;
 }
 
 // K3 work pass: one queued segment per thread, every lane busy.  The NQ
@@ -1107,8 +1259,7 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   }
   std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
   c.k3_ref = nt.size() >= 2 ? nt[0].second : -1;      // the lead is every follower's dedup reference
-  c.k3_hint.reserve(4 * (R + 1));                       // per-record drift hints: none yet
-  PG_HIP(hipMemsetAsync(c.k3_hint.p, 0xFF, 4 * (R + 1), c.stream));
+  c.k3_ref2 = nt.size() >= 3 ? nt[1].second : -1;     // the second reference (k_cover)
   std::vector<unsigned long long> tiles;
   tiles.reserve(total);
   size_t live = nt.size();
@@ -1214,7 +1365,6 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
   else {
     const long long rfs = c.k3_ref >= 0 ? c.h_rec_start[c.k3_ref] : 0, rfn = c.k3_ref >= 0 ? c.h_rec_len[c.k3_ref] : 0;
     const TileDesc* td = c.tile_desc.as<TileDesc>();
-    int* hint = c.k3_hint.as<int>();
     if (two_pass(c, ntiles, dbg)) {
       // coverage pass, then the dense work pass over the queued segments
       const uint64_t qcap = (ntiles + NQ - 1) / NQ * IBLOCK;       // per sub-queue
@@ -1224,9 +1374,10 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       auto* q = c.k3_queue.as<WorkItem>();
       auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
       PG_HIP(hipMemsetAsync(qn, 0, 8 * QSTRIDE * NQ, c.stream));
-      hipLaunchKernelGGL((k_insert<true, true>), g, b, 0, c.stream, cls, td, q, qn, (unsigned long long)qcap, c.k,
-                         shift, c.tv, flags, c.k3_ref, rfs, rfn, hint, reinterpret_cast<uint4*>(c.table.p),
-                         (uint64_t)c.cap, dbg);
+      const long long r2s = c.k3_ref2 >= 0 ? c.h_rec_start[c.k3_ref2] : 0;
+      const long long r2n = c.k3_ref2 >= 0 ? c.h_rec_len[c.k3_ref2] : 0;
+      hipLaunchKernelGGL(k_cover, g, b, 0, c.stream, cls, td, q, qn, (unsigned long long)qcap, c.k, c.k3_ref, rfs,
+                         rfn, c.k3_ref2, r2s, r2n, reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap, dbg);
       PG_HIP(hipGetLastError());
       const unsigned gw = grid_for(max_items, IBLOCK, 16384);
       if (rc0)
@@ -1236,11 +1387,11 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
         hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, c.stream, cls, q, qn, (unsigned long long)qcap,
                            c.k, shift, c.tv, flags, dbg);
     } else if (rc0) {
-      hipLaunchKernelGGL((k_insert<true, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, 0ull, c.k, shift,
-                         c.tv, flags, c.k3_ref, rfs, rfn, hint, nullptr, 0ull, dbg);
+      hipLaunchKernelGGL(k_insert<true>, g, b, 0, c.stream, cls, td, c.k, shift, c.tv, flags, c.k3_ref, rfs, rfn,
+                         dbg);
     } else {
-      hipLaunchKernelGGL((k_insert<false, false>), g, b, 0, c.stream, cls, td, nullptr, nullptr, 0ull, c.k, shift,
-                         c.tv, flags, c.k3_ref, rfs, rfn, hint, nullptr, 0ull, dbg);
+      hipLaunchKernelGGL(k_insert<false>, g, b, 0, c.stream, cls, td, c.k, shift, c.tv, flags, c.k3_ref, rfs, rfn,
+                         dbg);
     }
   }
   PG_HIP(hipGetLastError());

@@ -94,6 +94,7 @@ struct Ctx {
   int device = 0;
   int k = 27;
   hipStream_t stream = nullptr;
+  int n_cu = 256;                 // compute units (persistent-kernel grids)
 
   // ---- input FASTA (device-resident; either owned or borrowed)
   DevBuf fasta_own;
@@ -134,7 +135,7 @@ struct Ctx {
   int tile_k = 0;
   int tile_mode = 0;              // 0: per-record tiles (k_insert), 1: record groups (k_insert_grp)
   int k3_ref = -1;                // k_insert's dedup reference record (the lead), -1: none
-  DevBuf k3_hint;                 // int32 per record: last drift k_insert found (-1: none)
+  int k3_ref2 = -1;               // k_cover's second reference record, -1: none
   DevBuf tile_desc;               // k_insert tile descriptors (record start / length / index / stripe)
   DevBuf k3_queue;                // segments left with work after k_insert's coverage pass, + counter
   DevBuf groups;                  // int32 [n_groups * GG] record ids, -1 padded
