@@ -74,7 +74,7 @@ void pg_destroy(pg_ctx* x) {
   pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.n_sel, &c.rec_start,
                         &c.rec_len, &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.ovf,
                         &c.flags,
-                        &c.rdbg_keys, &c.tiles, &c.groups, &c.tile_desc, &c.k3_queue, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
+                        &c.rdbg_keys, &c.tiles, &c.groups, &c.tile_desc, &c.k3_queue, &c.k3_hint, &c.part_cnt, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
                         &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload, &c.dump_cnt};
   for (auto* b : bufs) b->release();
   c.rec_pack.release();
@@ -225,7 +225,9 @@ int pg_dbg_partition(pg_ctx* x, int nparts, void* d_out, uint64_t out_cap, uint6
   return guard([&] {
     if (!x || !counts) throw pg::Error(PG_EINVAL, "pg_dbg_partition: bad arguments");
     PG_HIP(hipSetDevice(x->c.device));
-    const uint64_t total = pg::partition_dbg(x->c, nparts, nullptr, 0, counts);
+    // the scatter reuses the counts of a count pass over the same table
+    const bool counted = x->c.part_gen == x->c.build_gen && x->c.part_nparts == nparts;
+    const uint64_t total = d_out && counted ? x->c.part_total : pg::partition_dbg(x->c, nparts, nullptr, 0, counts);
     if (d_out) {
       if (out_cap < total) throw pg::Error(PG_ERANGE, "pg_dbg_partition: output too small");
       pg::partition_dbg(x->c, nparts, d_out, out_cap, counts);

@@ -397,50 +397,95 @@ constexpr int NQ = 64;
 constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long long words)
 
 // Drift of the tile's record against a reference record at NANCH anchors:
-// s_best[a] = (|delta| << 16) | (delta + DRIFT) of the smallest |delta| in
-// [-DRIFT, DRIFT] whose ALEN bytes match, ~0u if none.  The search is
-// dword-parallel: a task is one reference dword w (4 candidate starts), whose
-// shifted words are compared with the anchor's first 4 bytes (the stream is
-// ~2 bits per byte, so ~1 in 256 candidates passes) before the full ALEN-byte
-// check.  Per anchor (its geometry block-uniform, so scalar) one dword task
-// per thread (two for the first few), ~20 VALU; the earlier per-offset search
-// (a stale per-record hint first, then 1025 offsets per anchor at ~35 VALU
-// each) made the coverage pass VALU-bound (0.28 of its 0.81 ms,
-// PG_K3_DBG=512).  Ends with a block barrier.
+// s_best[a] = (|delta| << 16) | (delta + DRIFT) of a delta in [-DRIFT, DRIFT]
+// whose ALEN bytes match, ~0u if none.  Any match serves: the drift only
+// decides how much is skipped, never what is inserted.
+//
+// The coverage pass is VALU-bound (PMC: ~1200 VALU per wave per tile, at
+// 4 cycles per wave64 instruction), so the search is staged:
+//  1. around the record's last drift found by any of its tiles (`hint`,
+//     +-HWIN): one wave per anchor, <= 34 dword tasks.  Tiles in flight are
+//     ~20 stripes apart, over which the drift of the synthetic pangenomes
+//     moves by ~25 (indels of 1-10 bp, 2e-4 per base per pair), so this
+//     almost always hits;
+//  2. the full [-DRIFT, DRIFT] for anchors still without a match.
+// A task is one reference dword w (4 candidate starts), whose shifted words
+// are compared with the anchor's first 4 bytes (~1 in 256 candidates passes
+// on a ~2-bit stream) before the full ALEN-byte check.  Ends with a barrier;
+// thread 0 publishes the drift to *hint_out.
 constexpr int ASTEP = (TILE - ALEN - 16) / (NANCH - 1);      // anchor spacing
+constexpr int HWIN = 64;                                     // stage-1 window: hint +- HWIN
 __device__ __forceinline__ void find_drift(const uint8_t* s_cls, long long base, const uint8_t* s_ref,
                                            long long rbase, long long qt, long long rn, long long plo,
-                                           long long phi, unsigned* s_best) {
-  constexpr int NW = (2 * DRIFT + 3) / 4 + 2;                 // dword tasks per anchor
+                                           long long phi, int hint, unsigned* s_best, int* hint_out) {
+  static_assert(NANCH * 64 <= IBLOCK && (2 * HWIN) / 4 + 2 <= 64, "one wave per anchor in stage 1");
+  constexpr int NW = (2 * DRIFT + 3) / 4 + 2;                 // dword tasks per anchor (full range)
   const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
+  // anchor ai's candidates: reference starts ib in [lo, hi] (s_ref indices);
+  // ib = ibhi - d for d = delta + DRIFT
+  auto geom = [&](int ai, int& ia, int& ibhi, int& lo, int& hi) {
+    const long long a = qt + 8 + (long long)ai * ASTEP;       // anchor: record positions [a, a + ALEN)
+    ia = (int)(base + a);
+    ibhi = (int)(rbase + a + DRIFT);
+    lo = max(ibhi - 2 * DRIFT, (int)(rbase + plo));
+    hi = a + ALEN > rn ? -1 : min(ibhi, (int)(rbase + phi) - ALEN);
+  };
+  // The prefilter compares 8 bytes: with 4, ~63% of waves had a lane whose
+  // candidate passed, and the whole wave then ran the full check (SIMT).
+  auto task = [&](int ai, int ia, int ibhi, int lo, int hi, int w) {
+    uint32_t x[2];
+    lds_bytes(s_cls, (uint32_t)ia, x);                        // one address per anchor: broadcast
+    const uint32_t W0 = rw[w], W1 = rw[w + 1], W2 = rw[w + 2];
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const int ib = 4 * w + sb;
+      if (ib < lo || ib > hi || __builtin_amdgcn_alignbyte(W1, W0, sb) != x[0] ||
+          __builtin_amdgcn_alignbyte(W2, W1, sb) != x[1])
+        continue;
+      uint32_t A[ALEN / 4], B[ALEN / 4];
+      lds_bytes(s_cls, (uint32_t)ia, A);
+      lds_bytes(s_ref, (uint32_t)ib, B);
+      bool eq = true;
+#pragma unroll
+      for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
+      const int d = ibhi - ib;                                // delta + DRIFT
+      const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+      if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
+    }
+  };
+  if (hint >= 0) {                                            // block-uniform
+    const int ai = (int)threadIdx.x >> 6, m = (int)threadIdx.x & 63;
+    if (ai < NANCH) {
+      int ia, ibhi, lo, hi;
+      geom(ai, ia, ibhi, lo, hi);
+      lo = max(lo, ibhi - (hint + HWIN));
+      hi = min(hi, ibhi - (hint - HWIN));
+      const int w = (lo >> 2) + m;
+      if (lo <= hi && 4 * w <= hi) task(ai, ia, ibhi, lo, hi, w);
+    }
+    __syncthreads();
+  }
+  // Stage 2 only when stage 1 found no anchor at all: an anchor that misses
+  // next to found ones sits on a variant (or an indel), where the full range
+  // finds nothing either (PMC: stage 2 ran for ~1.5 anchors per tile when it
+  // ran per missing anchor); segment_covered tries the drifts that were found.
+  const bool any = (s_best[0] & s_best[1] & s_best[2]) != ~0u;   // block-uniform
+  static_assert(NANCH == 3, "any-anchor test");
 #pragma unroll 1
   for (int ai = 0; ai < NANCH; ++ai) {
-    const long long a = qt + 8 + (long long)ai * ASTEP;       // anchor: record positions [a, a + ALEN)
-    if (a + ALEN > rn) continue;
-    const int ia = (int)(base + a);                           // its s_cls index
-    const int ibhi = (int)(rbase + a + DRIFT);                // s_ref index of its match at delta = -DRIFT
-    const int lo = max(ibhi - 2 * DRIFT, (int)(rbase + plo)), hi = min(ibhi, (int)(rbase + phi) - ALEN);
-    uint32_t A1[1];
-    lds_bytes(s_cls, (uint32_t)ia, A1);                       // one address: a broadcast read
-    for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += IBLOCK) {
-      const uint32_t W0 = rw[w], W1 = rw[w + 1];
-#pragma unroll
-      for (int sb = 0; sb < 4; ++sb) {
-        const int ib = 4 * w + sb;
-        if (ib < lo || ib > hi || __builtin_amdgcn_alignbyte(W1, W0, sb) != A1[0]) continue;
-        uint32_t A[ALEN / 4], B[ALEN / 4];
-        lds_bytes(s_cls, (uint32_t)ia, A);
-        lds_bytes(s_ref, (uint32_t)ib, B);
-        bool eq = true;
-#pragma unroll
-        for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
-        const int d = ibhi - ib;                              // delta + DRIFT
-        const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
-        if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
-      }
-    }
+    if (any || s_best[ai] != ~0u) continue;                   // block-uniform
+    int ia, ibhi, lo, hi;
+    geom(ai, ia, ibhi, lo, hi);
+    for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += IBLOCK)
+      task(ai, ia, ibhi, lo, hi, w);
   }
   __syncthreads();
+  if (threadIdx.x == 0) {
+    int h = -1;
+    for (int ai = NANCH - 1; ai >= 0; --ai)
+      if (s_best[ai] != ~0u) h = (int)(s_best[ai] & 0xFFFFu);
+    if (h >= 0) *hint_out = h;
+  }
 }
 
 // Covered windows of the interior segment q0 .. q0+IW-1 (bit i: window q0+i):
@@ -520,11 +565,23 @@ __device__ __forceinline__ uint32_t segment_covered16(const uint8_t* s_cls, long
     if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
     uint32_t Rw[NB];
     lds_bytes16(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
-    uint32_t diff = 0;
+    // dwords holding a differing byte; window i (bytes i .. i+k+1) is covered
+    // when it avoids every such dword.  Dword granularity is conservative (a
+    // window next to a mismatch may be left to the work pass, which only costs
+    // a probe) and costs ~30 VALU where the byte-exact run test cost ~150 —
+    // and a wave pays it whenever any of its 64 segments is partial (C3: ~13%
+    // are, so nearly every wave), which made the compare the largest part of
+    // this pass (PMC: 327 of 659 VALU per wave).
+    uint32_t nz = 0;
 #pragma unroll
-    for (int i = 0; i < NB; ++i) diff |= G[i] ^ Rw[i];
-    if (diff == 0) return (1u << IW) - 1u;                    // the common case: all context bytes equal
-    covered |= (uint32_t)(run_and(byte_eq_bits(G, Rw), k + 2) & ((1u << IW) - 1u));
+    for (int i = 0; i < NB; ++i) nz |= (G[i] != Rw[i] ? 1u : 0u) << i;
+    nz &= (2u << ((k + IW) >> 2)) - 1u;                       // bytes past k+IW do not matter
+    if (nz == 0) return (1u << IW) - 1u;                      // the common case: all context bytes equal
+    const int first = 4 * __builtin_ctz(nz), last = 4 * (31 - __builtin_clz(nz)) + 3;
+    const int ulo = max(0, first - k - 1), uhi = min(IW - 1, last);
+    if (ulo <= uhi) covered |= ((1u << IW) - 1u) & ~(((2u << uhi) - 1u) & ~((1u << ulo) - 1u));
+    else covered = (1u << IW) - 1u;
+    if (covered == (1u << IW) - 1u) return covered;
   }
   return covered;
 }
@@ -587,7 +644,8 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, in
   }
   __syncthreads();
   const long long base = rs - g.a0, rbase = rfs - g.ra0;      // LDS index of record position 0
-  if (dedup) find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, s_best);
+  int dummy = -1;
+  if (dedup) find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, -1, s_best, &dummy);
   uint32_t covered = 0;
   unsigned created_acc = 0;
   const long long q0 = g.qt + (long long)threadIdx.x * IW;
@@ -634,8 +692,8 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, in
 __global__ void __launch_bounds__(IBLOCK)
 k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
-        long long rfn, int ref2, long long r2s, long long r2n, uint4* __restrict__ zero, uint64_t zero_n16,
-        int dbg) {
+        long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints, int nrec,
+        uint4* __restrict__ zero, uint64_t zero_n16, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref2[RSPAN];
@@ -646,6 +704,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   const long long rs = td.rs, rn = td.rn, last = rn - k;
   const bool dedup = ref >= 0 && ref != td.r && !(dbg & 32);  // block-uniform
   const bool dedup2 = dedup && ref2 >= 0 && ref2 != td.r && !(dbg & 16384);
+  const int h1 = dedup ? hints[td.r] : -1, h2 = dedup2 ? hints[nrec + td.r] : -1;   // in flight with staging
   const Stage g = stage_of(td, k, dedup, rfs, rfn);
   Stage g2 = g;
   if (dedup2) ref_span(g2, k, r2s, r2n);
@@ -667,8 +726,10 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   }
   __syncthreads();
   const long long base = rs - g.a0, rbase = rfs - g.ra0, rbase2 = r2s - g2.ra0;   // LDS index of position 0
-  if (dedup && !(dbg & 512)) find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, s_best);
-  if (dedup2 && !(dbg & 512)) find_drift(s_cls, base, s_ref2, rbase2, g.qt, rn, g2.plo, g2.phi, s_best2);
+  if (dedup && !(dbg & 512))
+    find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, h1, s_best, hints + td.r);
+  if (dedup2 && !(dbg & 512))
+    find_drift(s_cls, base, s_ref2, rbase2, g.qt, rn, g2.plo, g2.phi, h2, s_best2, hints + nrec + td.r);
   const long long q0 = g.qt + (long long)threadIdx.x * IW;
   constexpr uint32_t ALL = (1u << IW) - 1u;
   uint32_t covered = 0;
@@ -1147,24 +1208,40 @@ __global__ void k_part_count(TableView T, uint64_t nw, uint64_t ntot, int nparts
     if (hist[i]) atomicAdd(&counts[i], hist[i]);
 }
 
-__global__ void k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts,
-                               unsigned long long* __restrict__ cursor, Slot* __restrict__ out) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntot;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t m = entry_mask(T, nw, i);
-    const uint64_t c = m ? entry_key(T, nw, i) : 0ull;
-    const int own = m ? owner_of(c, nparts) : -1;
-    for (int o = 0; o < nparts; ++o) {
-      const unsigned long long b = __ballot(own == o);
-      if (!b) continue;
-      const int leader = __builtin_ctzll(b);
-      unsigned long long base = 0;
-      if (lane == leader) base = atomicAdd(&cursor[o], (unsigned long long)__builtin_popcountll(b));
-      base = __shfl(base, leader, 64);
-      if (own == o) out[base + __builtin_popcountll(b & lt)] = Slot{c + 1ull, m, 0u};
+// Owner-partitioned copy of the table's entries.  Per chunk of PCH entries a
+// block counts its entries per owner in LDS, reserves each owner's run with
+// ONE global atomic, then writes.  (One atomic per wave and owner on the
+// shared owner cursors serialised ~8 M same-address atomics at the memory
+// side for a C3 table, tens of ms; see NQ above.)  Record order inside an
+// owner's run is arbitrary: the owner OR-merges them.
+constexpr int PT = 256, PE = 8, PCH = PT * PE;
+__global__ void __launch_bounds__(PT)
+k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts, unsigned long long* __restrict__ cursor,
+               Slot* __restrict__ out) {
+  __shared__ unsigned s_cnt[64];
+  __shared__ unsigned long long s_base[64];
+  for (uint64_t c0 = blockIdx.x * (uint64_t)PCH; c0 < ntot; c0 += (uint64_t)gridDim.x * PCH) {
+    if (threadIdx.x < 64) s_cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t m[PE], rank[PE];
+    uint64_t key[PE];
+    int own[PE];
+#pragma unroll
+    for (int j = 0; j < PE; ++j) {
+      const uint64_t i = c0 + (uint64_t)j * PT + threadIdx.x;
+      m[j] = i < ntot ? entry_mask(T, nw, i) : 0u;
+      key[j] = m[j] ? entry_key(T, nw, i) : 0ull;
+      own[j] = m[j] ? owner_of(key[j], nparts) : 0;
+      rank[j] = m[j] ? atomicAdd(&s_cnt[own[j]], 1u) : 0u;
     }
+    __syncthreads();
+    if ((int)threadIdx.x < nparts && s_cnt[threadIdx.x])
+      s_base[threadIdx.x] = atomicAdd(&cursor[threadIdx.x], (unsigned long long)s_cnt[threadIdx.x]);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < PE; ++j)
+      if (m[j]) out[s_base[own[j]] + rank[j]] = Slot{key[j] + 1ull, m[j], 0u};
+    __syncthreads();
   }
 }
 
@@ -1260,6 +1337,7 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
   c.k3_ref = nt.size() >= 2 ? nt[0].second : -1;      // the lead is every follower's dedup reference
   c.k3_ref2 = nt.size() >= 3 ? nt[1].second : -1;     // the second reference (k_cover)
+  c.k3_hint.reserve(8 * (R + 1));                       // per-record drift hints, both references
   std::vector<unsigned long long> tiles;
   tiles.reserve(total);
   size_t live = nt.size();
@@ -1374,10 +1452,12 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       auto* q = c.k3_queue.as<WorkItem>();
       auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
       PG_HIP(hipMemsetAsync(qn, 0, 8 * QSTRIDE * NQ, c.stream));
+      PG_HIP(hipMemsetAsync(c.k3_hint.p, 0xFF, 8 * (c.n_records + 1), c.stream));   // no drift known yet
       const long long r2s = c.k3_ref2 >= 0 ? c.h_rec_start[c.k3_ref2] : 0;
       const long long r2n = c.k3_ref2 >= 0 ? c.h_rec_len[c.k3_ref2] : 0;
       hipLaunchKernelGGL(k_cover, g, b, 0, c.stream, cls, td, q, qn, (unsigned long long)qcap, c.k, c.k3_ref, rfs,
-                         rfn, c.k3_ref2, r2s, r2n, reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap, dbg);
+                         rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records,
+                         reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap, dbg);
       PG_HIP(hipGetLastError());
       const unsigned gw = grid_for(max_items, IBLOCK, 16384);
       if (rc0)
@@ -1465,6 +1545,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
       c.sentinel = sentinel ? 1 : 0;
       c.cap_hint = std::max<uint64_t>(1024, created + created / 4);
       c.built = true;
+      ++c.build_gen;
       return;
     }
     keys = std::max<uint64_t>(keys * 4, created * 2);
@@ -1544,26 +1625,39 @@ uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap) {
 uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts) {
   if (!c.built) throw Error(-22, "partition_dbg: no dBG");
   if (nparts < 1 || nparts > 64) throw Error(-22, "partition_dbg: nparts must be in [1, 64]");
-  DevBuf cnt;
+  DevBuf& cnt = c.part_cnt;                             // [0, 64) counts, [64, 128) cursors
   cnt.reserve(16 * 64);
-  PG_HIP(hipMemsetAsync(cnt.p, 0, 16 * 64, c.stream));
   auto* counts = cnt.as<unsigned long long>();
-  hipLaunchKernelGGL(k_part_count, dim3(grid_for(n_entries(c), 256, 4096)), dim3(256), 0, c.stream, c.tv,
-                     2 * c.cap, n_entries(c), nparts, counts);
-  PG_HIP(hipGetLastError());
-  std::vector<unsigned long long> h(nparts), off(nparts);
-  PG_HIP(hipMemcpyAsync(h.data(), counts, 8 * nparts, hipMemcpyDeviceToHost, c.stream));
-  c.sync();
+  c.h_pin.reserve(16 * 64);
+  auto* h = c.h_pin.as<unsigned long long>();
+  if (!d_out) {                                         // count pass
+    PG_HIP(hipMemsetAsync(cnt.p, 0, 8 * 64, c.stream));
+    hipLaunchKernelGGL(k_part_count, dim3(grid_for(n_entries(c), 256, 4096)), dim3(256), 0, c.stream, c.tv,
+                       2 * c.cap, n_entries(c), nparts, counts);
+    PG_HIP(hipGetLastError());
+    PG_HIP(hipMemcpyAsync(h, counts, 8 * nparts, hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    uint64_t total = 0;
+    for (int i = 0; i < nparts; ++i) { h_counts[i] = h[i]; total += h[i]; }
+    c.part_total = total;
+    c.part_nparts = nparts;
+    c.part_gen = c.build_gen;
+    for (int i = 0; i < nparts; ++i) c.part_counts[i] = h[i];
+    return total;
+  }
+  // scatter pass: the counts of the last count pass give every owner's run
   uint64_t total = 0;
-  for (int i = 0; i < nparts; ++i) { off[i] = total; total += h[i]; h_counts[i] = h[i]; }
-  if (d_out && out_cap >= total && total) {
-    PG_HIP(hipMemcpyAsync(counts + 64, off.data(), 8 * nparts, hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_part_scatter, dim3(grid_for(n_entries(c), 256, 4096)), dim3(256), 0, c.stream, c.tv,
+  for (int i = 0; i < nparts; ++i) { h[64 + i] = total; total += c.part_counts[i]; h_counts[i] = c.part_counts[i]; }
+  if (c.part_gen != c.build_gen || c.part_nparts != nparts)
+    throw Error(-22, "partition_dbg: call with d_out = NULL (count pass) first");
+  if (out_cap < total) throw Error(-22, "partition_dbg: output buffer too small");
+  if (total) {
+    PG_HIP(hipMemcpyAsync(counts + 64, h + 64, 8 * nparts, hipMemcpyHostToDevice, c.stream));
+    hipLaunchKernelGGL(k_part_scatter, dim3(grid_for(n_entries(c), PCH, 4096)), dim3(PT), 0, c.stream, c.tv,
                        2 * c.cap, n_entries(c), nparts, counts + 64, reinterpret_cast<Slot*>(d_out));
     PG_HIP(hipGetLastError());
     c.sync();
   }
-  cnt.release();
   return total;
 }
 
@@ -1589,6 +1683,7 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int s
       c.sentinel = s ? 1 : 0;
       c.built = true;
       c.reduced = false;
+      ++c.build_gen;
       return;
     }
     keys *= 4;

@@ -136,6 +136,13 @@ struct Ctx {
   int tile_mode = 0;              // 0: per-record tiles (k_insert), 1: record groups (k_insert_grp)
   int k3_ref = -1;                // k_insert's dedup reference record (the lead), -1: none
   int k3_ref2 = -1;               // k_cover's second reference record, -1: none
+  DevBuf part_cnt;                // multi-GPU partition: owner counts and cursors
+  uint64_t part_counts[64] = {};  // counts of the last count pass
+  uint64_t part_total = 0;
+  int part_nparts = 0;
+  uint64_t part_gen = ~0ull;      // build_gen of the table the counts are for
+  uint64_t build_gen = 0;         // bumped by every table build / merge
+  DevBuf k3_hint;                 // int32 [2][R]: last drift k_cover found per record and reference
   DevBuf tile_desc;               // k_insert tile descriptors (record start / length / index / stripe)
   DevBuf k3_queue;                // segments left with work after k_insert's coverage pass, + counter
   DevBuf groups;                  // int32 [n_groups * GG] record ids, -1 padded
