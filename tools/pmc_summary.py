@@ -54,7 +54,7 @@ def collect(pattern: str, drop_first: bool):
 
 def main(config: str = "c3"):
     pmc = collect("pmc3_*", True)
-    cov = next(k for k in pmc if k.startswith("pg::k_insert<"))
+    cov = next(k for k in pmc if k.startswith("pg::k_cover") or k.startswith("pg::k_insert<"))
     work = next((k for k in pmc if k.startswith("pg::k_insert_work")), None)
     kb = 1024.0
     t_cov = 2 * pmc[cov]["FETCH_SIZE"] * kb + pmc[cov]["WRITE_SIZE"] * kb
