@@ -61,6 +61,8 @@ int pg_create(pg_ctx** out, int device, int k) {
     x->c.device = device;
     x->c.k = k < 1 ? 1 : (k > 27 ? 27 : k);
     PG_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
+    PG_HIP(hipStreamCreateWithFlags(&x->c.stream2, hipStreamNonBlocking));
+    for (auto& e : x->c.ev) PG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     PG_HIP(hipDeviceGetAttribute(&x->c.n_cu, hipDeviceAttributeMultiprocessorCount, device));
     *out = x;
   });
@@ -81,6 +83,9 @@ void pg_destroy(pg_ctx* x) {
   c.h_pin.release();
   c.t0.destroy();
   c.t1.destroy();
+  for (auto& e : c.ev)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c.stream2);
   (void)hipStreamDestroy(c.stream);
   delete x;
 }

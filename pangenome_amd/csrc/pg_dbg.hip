@@ -414,10 +414,11 @@ constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long 
 // on a ~2-bit stream) before the full ALEN-byte check.  Ends with a barrier;
 // thread 0 publishes the drift to *hint_out.
 constexpr int ASTEP = (TILE - ALEN - 16) / (NANCH - 1);      // anchor spacing
-constexpr int HWIN = 64;                                     // stage-1 window: hint +- HWIN
+constexpr int HWIN = 120;                                    // stage-1 window: hint +- HWIN
 __device__ __forceinline__ void find_drift(const uint8_t* s_cls, long long base, const uint8_t* s_ref,
                                            long long rbase, long long qt, long long rn, long long plo,
-                                           long long phi, int hint, unsigned* s_best, int* hint_out) {
+                                           long long phi, int hint, unsigned* s_best, int* hint_out,
+                                           unsigned* diag = nullptr) {
   static_assert(NANCH * 64 <= IBLOCK && (2 * HWIN) / 4 + 2 <= 64, "one wave per anchor in stage 1");
   constexpr int NW = (2 * DRIFT + 3) / 4 + 2;                 // dword tasks per anchor (full range)
   const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
@@ -471,6 +472,10 @@ __device__ __forceinline__ void find_drift(const uint8_t* s_cls, long long base,
   // ran per missing anchor); segment_covered tries the drifts that were found.
   const bool any = (s_best[0] & s_best[1] & s_best[2]) != ~0u;   // block-uniform
   static_assert(NANCH == 3, "any-anchor test");
+  if (diag && threadIdx.x == 0) {                             // dev counters: hint stage ran / missed
+    atomicAdd(diag, hint >= 0 ? 1u : 0u);
+    atomicAdd(diag + 1, any ? 0u : 1u);
+  }
 #pragma unroll 1
   for (int ai = 0; ai < NANCH; ++ai) {
     if (any || s_best[ai] != ~0u) continue;                   // block-uniform
@@ -693,18 +698,23 @@ __global__ void __launch_bounds__(IBLOCK)
 k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
         long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints, int nrec,
-        uint4* __restrict__ zero, uint64_t zero_n16, int dbg) {
+        uint4* __restrict__ zero, uint64_t zero_n16, uint64_t tile0, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref2[RSPAN];
   __shared__ unsigned s_best[NANCH], s_best2[NANCH];
   __shared__ uint32_t s_scan[IBLOCK / 64];
   __shared__ unsigned long long s_qbase;
-  const TileDesc td = descs[xcd_swizzle(blockIdx.x, gridDim.x)];
+  const TileDesc td = descs[tile0 + xcd_swizzle(blockIdx.x, gridDim.x)];   // this launch: tiles tile0 ..
   const long long rs = td.rs, rn = td.rn, last = rn - k;
   const bool dedup = ref >= 0 && ref != td.r && !(dbg & 32);  // block-uniform
   const bool dedup2 = dedup && ref2 >= 0 && ref2 != td.r && !(dbg & 16384);
-  const int h1 = dedup ? hints[td.r] : -1, h2 = dedup2 ? hints[nrec + td.r] : -1;   // in flight with staging
+  // hints per (XCD, reference, record): the XCD swizzle gives each XCD its
+  // own contiguous eighth of the tile list, so one shared hint per record
+  // alternated between stripes ~150 apart and the hint window missed on
+  // 15-24 % of the tiles
+  int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
+  const int h1 = dedup ? hx[td.r] : -1, h2 = dedup2 ? hx[nrec + td.r] : -1;   // in flight with staging
   const Stage g = stage_of(td, k, dedup, rfs, rfn);
   Stage g2 = g;
   if (dedup2) ref_span(g2, k, r2s, r2n);
@@ -726,10 +736,12 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   }
   __syncthreads();
   const long long base = rs - g.a0, rbase = rfs - g.ra0, rbase2 = r2s - g2.ra0;   // LDS index of position 0
+  unsigned* diag = (dbg & 64) ? reinterpret_cast<unsigned*>(hints + 16 * nrec + 2) : nullptr;   // dev counters
   if (dedup && !(dbg & 512))
-    find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, h1, s_best, hints + td.r);
+    find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, h1, s_best, hx + td.r, diag);
   if (dedup2 && !(dbg & 512))
-    find_drift(s_cls, base, s_ref2, rbase2, g.qt, rn, g2.plo, g2.phi, h2, s_best2, hints + nrec + td.r);
+    find_drift(s_cls, base, s_ref2, rbase2, g.qt, rn, g2.plo, g2.phi, h2, s_best2, hx + nrec + td.r,
+               diag ? diag + 2 : nullptr);
   const long long q0 = g.qt + (long long)threadIdx.x * IW;
   constexpr uint32_t ALL = (1u << IW) - 1u;
   uint32_t covered = 0;
@@ -1337,7 +1349,7 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
   c.k3_ref = nt.size() >= 2 ? nt[0].second : -1;      // the lead is every follower's dedup reference
   c.k3_ref2 = nt.size() >= 3 ? nt[1].second : -1;     // the second reference (k_cover)
-  c.k3_hint.reserve(8 * (R + 1));                       // per-record drift hints, both references
+  c.k3_hint.reserve(64 * (R + 1) + 64);                 // drift hints per XCD, reference, record (+ dev counters)
   std::vector<unsigned long long> tiles;
   tiles.reserve(total);
   size_t live = nt.size();
@@ -1425,6 +1437,8 @@ static int k3_mode(const Ctx& c, const std::vector<uint8_t>& flag) {
   return n >= (uint64_t)GG ? 1 : 0;
 }
 
+// chunks of the tile list whose work pass overlaps the next coverage pass
+constexpr int K3_CHUNKS = 2;
 // the coverage pass + work pass form of k_insert (needs the lead record)
 static bool two_pass(const Ctx& c, uint64_t ntiles, int dbg) { return ntiles && c.k3_ref >= 0 && !(dbg & 256); }
 
@@ -1444,28 +1458,62 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
     const long long rfs = c.k3_ref >= 0 ? c.h_rec_start[c.k3_ref] : 0, rfn = c.k3_ref >= 0 ? c.h_rec_len[c.k3_ref] : 0;
     const TileDesc* td = c.tile_desc.as<TileDesc>();
     if (two_pass(c, ntiles, dbg)) {
-      // coverage pass, then the dense work pass over the queued segments
-      const uint64_t qcap = (ntiles + NQ - 1) / NQ * IBLOCK;       // per sub-queue
-      const uint64_t max_items = std::min<uint64_t>(NQ * qcap, c.windows_fw / IW + c.n_records + 1);
-      const size_t qbytes = sizeof(WorkItem) * NQ * qcap;
-      c.k3_queue.reserve(qbytes + 8 * QSTRIDE * NQ);
+      // Coverage pass, then the dense work pass over the queued segments, in
+      // NCH chunks of the tile list on two streams: the work pass of chunk i
+      // (memory-side-atomic-bound) runs beside the coverage pass of chunk
+      // i+1 (issue-bound), and the table clear beside the first coverage
+      // pass.  Coverage never touches the table, so only the clear must
+      // precede the first work pass.
+      const char* ce = getenv("PG_K3_CHUNKS");                  // dev knob
+      int nch = ce ? std::max(1, std::min(6, atoi(ce))) : K3_CHUNKS;
+      if (ntiles < (uint64_t)nch * 4096) nch = 1;
+      uint64_t t0[8], qoff[8], qcapc[8];
+      uint64_t items = 0;
+      for (int i = 0; i <= nch; ++i) t0[i] = ntiles * (uint64_t)i / (uint64_t)nch;
+      for (int i = 0; i < nch; ++i) {
+        qcapc[i] = (t0[i + 1] - t0[i] + NQ - 1) / NQ * IBLOCK;   // per sub-queue
+        qoff[i] = items;
+        items += NQ * qcapc[i];
+      }
+      const size_t qbytes = sizeof(WorkItem) * items;
+      const size_t cbytes = 8 * QSTRIDE * NQ;                    // counters per chunk
+      c.k3_queue.reserve(qbytes + cbytes * nch);
       auto* q = c.k3_queue.as<WorkItem>();
       auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
-      PG_HIP(hipMemsetAsync(qn, 0, 8 * QSTRIDE * NQ, c.stream));
-      PG_HIP(hipMemsetAsync(c.k3_hint.p, 0xFF, 8 * (c.n_records + 1), c.stream));   // no drift known yet
+      PG_HIP(hipMemsetAsync(qn, 0, cbytes * nch, c.stream));
+      PG_HIP(hipMemsetAsync(c.k3_hint.p, 0xFF, 64 * (c.n_records + 1), c.stream));   // no drift known yet
+      if (dbg & 64) PG_HIP(hipMemsetAsync(c.k3_hint.as<int>() + 16 * c.n_records + 2, 0, 16, c.stream));
       const long long r2s = c.k3_ref2 >= 0 ? c.h_rec_start[c.k3_ref2] : 0;
       const long long r2n = c.k3_ref2 >= 0 ? c.h_rec_len[c.k3_ref2] : 0;
-      hipLaunchKernelGGL(k_cover, g, b, 0, c.stream, cls, td, q, qn, (unsigned long long)qcap, c.k, c.k3_ref, rfs,
-                         rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records,
-                         reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap, dbg);
+      hipStream_t s0 = c.stream, s1 = c.stream2;
+      // the clear on s1, after everything already queued on s0
+      PG_HIP(hipEventRecord(c.ev[0], s0));
+      PG_HIP(hipStreamWaitEvent(s1, c.ev[0], 0));
+      hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, s1,
+                         reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
       PG_HIP(hipGetLastError());
-      const unsigned gw = grid_for(max_items, IBLOCK, 16384);
-      if (rc0)
-        hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, c.stream, cls, q, qn, (unsigned long long)qcap, c.k,
-                           shift, c.tv, flags, dbg);
-      else
-        hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, c.stream, cls, q, qn, (unsigned long long)qcap,
-                           c.k, shift, c.tv, flags, dbg);
+      for (int i = 0; i < nch; ++i) {
+        const uint64_t nt = t0[i + 1] - t0[i];
+        auto* qi = q + qoff[i];
+        auto* qni = qn + (cbytes / 8) * i;
+        hipLaunchKernelGGL(k_cover, dim3((unsigned)nt), b, 0, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
+                           c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records,
+                           nullptr, 0ull, (uint64_t)t0[i], dbg);
+        PG_HIP(hipGetLastError());
+        PG_HIP(hipEventRecord(c.ev[1 + i], s0));
+        PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: clear, work 0 .. i-1, then this
+        const uint64_t mi = std::min<uint64_t>(NQ * qcapc[i], c.windows_fw / IW + c.n_records + 1);
+        const unsigned gw = grid_for(mi, IBLOCK, 16384);
+        if (rc0)
+          hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, s1, cls, qi, qni, (unsigned long long)qcapc[i],
+                             c.k, shift, c.tv, flags, dbg);
+        else
+          hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, s1, cls, qi, qni, (unsigned long long)qcapc[i],
+                             c.k, shift, c.tv, flags, dbg);
+        PG_HIP(hipGetLastError());
+      }
+      PG_HIP(hipEventRecord(c.ev[15], s1));                     // join: s0 continues after the last work pass
+      PG_HIP(hipStreamWaitEvent(s0, c.ev[15], 0));
     } else if (rc0) {
       hipLaunchKernelGGL(k_insert<true>, g, b, 0, c.stream, cls, td, c.k, shift, c.tv, flags, c.k3_ref, rfs, rfn,
                          dbg);
@@ -1532,6 +1580,12 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     read_flags(c, sentinel, overflow, created);
     c.ms_clear = c.t0.ms();
     c.ms_insert = c.t1.ms();
+    if (dbg & 64) {                  // dev counters of k_cover's drift search
+      unsigned d[4];
+      PG_HIP(hipMemcpy(d, c.k3_hint.as<int>() + 16 * c.n_records + 2, 16, hipMemcpyDeviceToHost));
+      fprintf(stderr, "PG_K3_DBG drift search: ref1 hinted %u full %u, ref2 hinted %u full %u, tiles %llu\n", d[0],
+              d[1], d[2], d[3], (unsigned long long)ntiles);
+    }
     if (dbg) {                       // dev knob run: timings only, the table is not a dBG
       std::vector<unsigned> f(N_FLAGS);
       PG_HIP(hipMemcpy(f.data(), c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost));

@@ -94,6 +94,8 @@ struct Ctx {
   int device = 0;
   int k = 27;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;  // side stream: K3 work passes overlap the next coverage pass
+  hipEvent_t ev[16] = {};         // ordering events between the two streams
   int n_cu = 256;                 // compute units (persistent-kernel grids)
 
   // ---- input FASTA (device-resident; either owned or borrowed)
@@ -142,7 +144,7 @@ struct Ctx {
   int part_nparts = 0;
   uint64_t part_gen = ~0ull;      // build_gen of the table the counts are for
   uint64_t build_gen = 0;         // bumped by every table build / merge
-  DevBuf k3_hint;                 // int32 [2][R]: last drift k_cover found per record and reference
+  DevBuf k3_hint;                 // int32 [8 XCDs][2 references][R]: last drift k_cover found
   DevBuf tile_desc;               // k_insert tile descriptors (record start / length / index / stripe)
   DevBuf k3_queue;                // segments left with work after k_insert's coverage pass, + counter
   DevBuf groups;                  // int32 [n_groups * GG] record ids, -1 padded

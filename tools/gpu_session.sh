@@ -28,6 +28,9 @@ for step in "$@"; do
            run pmc_$tag 600 rocprofv3 --pmc $ctr --kernel-include-regex "k_insert|k_reduce|k_emit|k_span_sum" -d gpurun_out/pmc_$tag -o pmc --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline
          done ;;
     listctr) run listctr 300 rocprofv3 -L ;;
+    chunksweep) for n in 1 2 3 4; do
+           PG_K3_CHUNKS=$n run bench_chunks_$n 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline
+         done ;;
     loadsweep) for l in 0.25 0.5 0.7; do
            PG_BUCKET_LOAD=$l run bench_load_$l 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline
          done ;;
