@@ -777,7 +777,10 @@ k_insert_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queu
               const unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift,
               TableView T, unsigned* __restrict__ flags, int dbg) {
   static_assert(NQ == 64, "one wave scans the sub-queue counts");
-  __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][96];
+  // 16-byte front pad + 64 staged bytes per thread (the realigning dword reads
+  // past them land in the next row, or read 0 past the allocation); 20 KiB so
+  // that a work block fits beside the coverage blocks of the next chunk
+  __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][80];
   __shared__ unsigned long long s_pre[NQ + 1];
   if (threadIdx.x < 64) {
     const unsigned long long c = qcount[QSTRIDE * threadIdx.x];
@@ -1063,10 +1066,10 @@ void merge_preload(Ctx& c, unsigned* flags) {
 // returning atomics per us (tools/rates.hip), so per-unit atomics would cost
 // more than the sweep itself, and the grid is kept to RGRID persistent blocks
 // (their final flushes all meet that counter at the end).
-constexpr int RT = 256, RU = 2;
+constexpr int RT = 256, RU_DEF = 2;
 constexpr unsigned RGRID = 4096;                   // RU = 4 on 1024 blocks measured slower (0.29 vs 0.26 ms)
-constexpr uint64_t RUNIT = (uint64_t)RT * RU;
-constexpr int RCAP = 4 * (int)RUNIT;               // a whole unit always fits an empty stage
+template <int RU> constexpr uint64_t runit() { return (uint64_t)RT * RU; }
+template <int RU> constexpr int rcap() { return 4 * (int)runit<RU>(); }   // a whole unit fits an empty stage
 
 // Stage entries are the bucket-hash value h = perm(c) with bit 63 = "B
 // orientation"; keys are rebuilt here, one entry per lane (dense), rather than
@@ -1085,37 +1088,39 @@ __device__ __forceinline__ void reduce_flush(const TableView& T, unsigned long l
   __syncthreads();
 }
 
+template <int RU>
 __device__ __forceinline__ void reduce_load(const TableView& T, uint64_t nb, uint64_t nel, uint64_t u,
                                             uint4 (&e)[RU]) {
 #pragma unroll
   for (int j = 0; j < RU; ++j) {
-    const uint64_t i = u * RUNIT + (uint64_t)j * RT + threadIdx.x;
+    const uint64_t i = u * runit<RU>() + (uint64_t)j * RT + threadIdx.x;
     e[j] = i >= nel ? make_uint4(0, 0, 0, 0)
                     : i < nb ? *reinterpret_cast<const uint4*>(T.prim + 2 * i)
                              : *reinterpret_cast<const uint4*>(T.ovf + (i - nb));
   }
 }
 
+template <int RU>
 __global__ void __launch_bounds__(RT)
 k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __restrict__ out, uint64_t cap,
          unsigned long long* __restrict__ counters) {
-  __shared__ unsigned long long stage[RCAP];
+  __shared__ unsigned long long stage[rcap<RU>()];
   __shared__ uint32_t lds[RT / 64];
   __shared__ unsigned long long s_base;
   __shared__ unsigned long long red[RT / 64];
   uint32_t staged = 0;                             // block-uniform
   unsigned long long ndbg = 0;
-  const uint64_t nunit = (nel + RUNIT - 1) / RUNIT;
+  const uint64_t nunit = (nel + runit<RU>() - 1) / runit<RU>();
   uint4 e[RU];
-  if (blockIdx.x < nunit) reduce_load(T, nb, nel, blockIdx.x, e);
+  if (blockIdx.x < nunit) reduce_load<RU>(T, nb, nel, blockIdx.x, e);
   for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
     uint4 nx[RU];                                  // next unit in flight while this one is reduced
-    if (u + gridDim.x < nunit) reduce_load(T, nb, nel, u + gridDim.x, nx);
+    if (u + gridDim.x < nunit) reduce_load<RU>(T, nb, nel, u + gridDim.x, nx);
     uint32_t m[RU][2];
     uint32_t cnt = 0;
 #pragma unroll
     for (int j = 0; j < RU; ++j) {
-      const uint64_t i = u * RUNIT + (uint64_t)j * RT + threadIdx.x;
+      const uint64_t i = u * runit<RU>() + (uint64_t)j * RT + threadIdx.x;
       const bool w0 = e[j].x | e[j].y, w1 = e[j].z | e[j].w;
       if (i < nb) {
         m[j][0] = w0 ? (e[j].x & MW_MASK) : 0u;
@@ -1134,7 +1139,7 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
     }
     uint32_t tot;
     const uint32_t pre = block_excl_scan<RT>(cnt, lds, tot);
-    if (staged + tot > (uint32_t)RCAP) {           // block-uniform
+    if (staged + tot > (uint32_t)rcap<RU>()) {           // block-uniform
       reduce_flush(T, stage, staged, &s_base, out, cap, counters);
       staged = 0;
     }
@@ -1142,7 +1147,7 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
       uint32_t o = staged + pre;
 #pragma unroll
       for (int j = 0; j < RU; ++j) {
-        const uint64_t i = u * RUNIT + (uint64_t)j * RT + threadIdx.x;
+        const uint64_t i = u * runit<RU>() + (uint64_t)j * RT + threadIdx.x;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const uint32_t mm = m[j][h];
@@ -1438,7 +1443,9 @@ static int k3_mode(const Ctx& c, const std::vector<uint8_t>& flag) {
 }
 
 // chunks of the tile list whose work pass overlaps the next coverage pass
-constexpr int K3_CHUNKS = 2;
+constexpr int K3_CHUNKS = 4;
+constexpr int K3_COVPAD = 8 * 1024;           // dynamic LDS pad per coverage block (chunked form)
+constexpr int K3_WBLK = 2;                    // work blocks per CU (chunked form)
 // the coverage pass + work pass form of k_insert (needs the lead record)
 static bool two_pass(const Ctx& c, uint64_t ntiles, int dbg) { return ntiles && c.k3_ref >= 0 && !(dbg & 256); }
 
@@ -1467,6 +1474,14 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       const char* ce = getenv("PG_K3_CHUNKS");                  // dev knob
       int nch = ce ? std::max(1, std::min(6, atoi(ce))) : K3_CHUNKS;
       if (ntiles < (uint64_t)nch * 4096) nch = 1;
+      // Overlap needs room on every CU: the coverage blocks are held to ~6 per
+      // CU by padding their LDS (covpad bytes of dynamic LDS), which leaves a
+      // work block (20 KiB) per CU; the work pass then runs as a persistent
+      // grid of wgrid blocks beside the next chunk's coverage pass.
+      const char* pe = getenv("PG_K3_COVPAD");                   // dev knobs
+      const char* we = getenv("PG_K3_WGRID");
+      const size_t covpad = nch > 1 ? (size_t)(pe ? atoi(pe) : K3_COVPAD) : 0;
+      const unsigned wgrid = we ? (unsigned)atoi(we) : (unsigned)c.n_cu * K3_WBLK;
       uint64_t t0[8], qoff[8], qcapc[8];
       uint64_t items = 0;
       for (int i = 0; i <= nch; ++i) t0[i] = ntiles * (uint64_t)i / (uint64_t)nch;
@@ -1496,14 +1511,14 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
         const uint64_t nt = t0[i + 1] - t0[i];
         auto* qi = q + qoff[i];
         auto* qni = qn + (cbytes / 8) * i;
-        hipLaunchKernelGGL(k_cover, dim3((unsigned)nt), b, 0, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
+        hipLaunchKernelGGL(k_cover, dim3((unsigned)nt), b, covpad, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
                            c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records,
                            nullptr, 0ull, (uint64_t)t0[i], dbg);
         PG_HIP(hipGetLastError());
         PG_HIP(hipEventRecord(c.ev[1 + i], s0));
         PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: clear, work 0 .. i-1, then this
         const uint64_t mi = std::min<uint64_t>(NQ * qcapc[i], c.windows_fw / IW + c.n_records + 1);
-        const unsigned gw = grid_for(mi, IBLOCK, 16384);
+        const unsigned gw = nch > 1 ? wgrid : grid_for(mi, IBLOCK, 16384);
         if (rc0)
           hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, s1, cls, qi, qni, (unsigned long long)qcapc[i],
                              c.k, shift, c.tv, flags, dbg);
@@ -1616,8 +1631,19 @@ void build_rdbg(Ctx& c) {
   PG_HIP(hipMemsetAsync(cnt.p, 0, CNT_BYTES, c.stream));
   c.t0.start(c.stream);
   const uint64_t nel = c.cap + c.ovf_cap;               // 16-byte elements: buckets, then overflow slots
-  hipLaunchKernelGGL(k_reduce, dim3(grid_for(nel / RUNIT, 1, RGRID)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
-                     c.k, c.rdbg_keys.as<unsigned long long>(), 2 * c.n_canon + 1, cnt.as<unsigned long long>());
+  const int ru = getenv("PG_K5_RU") ? atoi(getenv("PG_K5_RU")) : RU_DEF;            // dev knobs
+  const unsigned rg = getenv("PG_K5_GRID") ? (unsigned)atoi(getenv("PG_K5_GRID")) : RGRID;
+  auto* rk = c.rdbg_keys.as<unsigned long long>();
+  auto* rc = cnt.as<unsigned long long>();
+  if (ru == 1)
+    hipLaunchKernelGGL(k_reduce<1>, dim3(grid_for(nel / runit<1>(), 1, rg)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
+                       c.k, rk, 2 * c.n_canon + 1, rc);
+  else if (ru == 4)
+    hipLaunchKernelGGL(k_reduce<4>, dim3(grid_for(nel / runit<4>(), 1, rg)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
+                       c.k, rk, 2 * c.n_canon + 1, rc);
+  else
+    hipLaunchKernelGGL(k_reduce<2>, dim3(grid_for(nel / runit<2>(), 1, rg)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
+                       c.k, rk, 2 * c.n_canon + 1, rc);
   PG_HIP(hipGetLastError());
   c.t0.stop(c.stream);
   c.h_pin.reserve(CNT_BYTES);

@@ -31,6 +31,14 @@ for step in "$@"; do
     chunksweep) for n in 1 2 3 4; do
            PG_K3_CHUNKS=$n run bench_chunks_$n 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline
          done ;;
+    k5sweep) for cfg in "2 4096" "2 2304" "1 4096" "1 8192" "4 2048" "4 1024"; do
+           set -- $cfg
+           PG_K5_RU=$1 PG_K5_GRID=$2 run bench_k5_$1_$2 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline
+         done ;;
+    ovsweep) for cfg in ${OVCFG:-"4 8192 512"}; do
+           set -- $cfg
+           PG_K3_CHUNKS=$1 PG_K3_COVPAD=$2 PG_K3_WGRID=$3 run bench_ov_$1_$2_$3 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline
+         done ;;
     loadsweep) for l in 0.25 0.5 0.7; do
            PG_BUCKET_LOAD=$l run bench_load_$l 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline
          done ;;
