@@ -591,6 +591,71 @@ __device__ __forceinline__ uint32_t segment_covered16(const uint8_t* s_cls, long
   return covered;
 }
 
+// The distinct drifts the anchors found, with everything segment_cover
+// needs precomputed once per tile in 32-bit tile-relative form (block-uniform,
+// so scalar): segment q0 = qt + rel may use drift j iff lo[j] <= rel <= hi[j]
+// (its reference window p0 = q0 - delta interior and staged), and then reads
+// the reference bytes at LDS index o + off[j], o = the segment's s_cls index.
+struct Drifts {
+  int n;
+  int off[NANCH], lo[NANCH], hi[NANCH];
+};
+__device__ __forceinline__ Drifts drifts_of(const unsigned* s_best, long long qt, long long base, long long rbase,
+                                            long long rfn, long long plo, long long phi, int k) {
+  Drifts D;
+  D.n = 0;
+#pragma unroll
+  for (int j = 0; j < NANCH; ++j) D.off[j] = D.lo[j] = D.hi[j] = 0;
+  const long long pl = plo + 1 > 1 ? plo + 1 : 1;                       // p0 - 1 >= plo, p0 >= 1
+  const long long ph = rfn - k - IW < phi - IW - k ? rfn - k - IW : phi - IW - k;   // p0 + IW <= rfn - k, .. <= phi
+#pragma unroll
+  for (int ai = 0; ai < NANCH; ++ai) {
+    const unsigned b = s_best[ai];
+    if (b == ~0u) continue;
+    const int d = (int)(b & 0xFFFFu) - DRIFT;                           // delta: q0 - p0
+    bool dup = false;
+#pragma unroll
+    for (int j = 0; j < ai; ++j) dup |= j < D.n && D.off[j] == (int)(rbase - base) - d;
+    if (dup) continue;
+    const long long lo = pl + d - qt, hi = ph + d - qt;
+    const int l32 = (int)(lo < -(1ll << 30) ? -(1ll << 30) : lo), h32 = (int)(hi > (1ll << 30) ? (1ll << 30) : hi);
+    const int o32 = (int)(rbase - base) - d;
+#pragma unroll
+    for (int j = 0; j <= ai; ++j)                             // static indices: registers, not scratch
+      if (j == D.n) { D.lo[j] = l32; D.hi[j] = h32; D.off[j] = o32; }
+    ++D.n;
+  }
+  return D;
+}
+
+// Covered windows of the interior segment whose context bytes start at s_cls
+// index o (rel = q0 - qt), against the reference drifts D (see
+// segment_covered16; same rule, 32-bit and precomputed).
+__device__ __forceinline__ uint32_t segment_cover(const uint8_t* s_cls, const uint8_t* s_ref, uint32_t o, int rel,
+                                                  const uint32_t (&G)[(IW + 27 + 1 + 3) / 4], const Drifts& D,
+                                                  int k) {
+  constexpr int NB = (IW + 27 + 1 + 3) / 4;
+  constexpr uint32_t ALL = (1u << IW) - 1u;
+  uint32_t covered = 0;
+#pragma unroll
+  for (int j = 0; j < NANCH; ++j) {
+    if (j >= D.n) break;                                      // block-uniform
+    if (rel < D.lo[j] || rel > D.hi[j]) continue;
+    uint32_t Rw[NB];
+    lds_bytes16(s_ref, o + (uint32_t)D.off[j], Rw);
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) nz |= (G[i] != Rw[i] ? 1u : 0u) << i;
+    nz &= (2u << ((k + IW) >> 2)) - 1u;                       // bytes past k+IW do not matter
+    if (nz == 0) return ALL;                                  // the common case: all context bytes equal
+    const int first = 4 * __builtin_ctz(nz), last = 4 * (31 - __builtin_clz(nz)) + 3;
+    const int ulo = max(0, first - k - 1), uhi = min(IW - 1, last);
+    covered |= ALL & ~(((2u << uhi) - 1u) & ~((1u << ulo) - 1u));
+    if (covered == ALL) return ALL;
+  }
+  return covered;
+}
+
 // Staging geometry of tile (record [rs, rs+rn), stripe): class positions
 // [lo, hi) from the 16-byte aligned a0 (windows qt .. qt+TILE-1 read from q-2,
 // the last-window pred, to q+k+1, the twin pred of window 0), and the
@@ -746,9 +811,15 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   constexpr uint32_t ALL = (1u << IW) - 1u;
   uint32_t covered = 0;
   if (dedup && q0 > 0 && q0 + IW <= last && !(dbg & 1024)) {
-    covered = segment_covered16(s_cls, base, s_ref, rbase, q0, k, rfn, g.plo, g.phi, s_best);
+    constexpr int NB = (IW + 27 + 1 + 3) / 4;                // bytes q0-1 .. q0+IW+k-1, k <= 27
+    const uint32_t o = (uint32_t)(base + q0 - 1);
+    const int rel = (int)threadIdx.x * IW;
+    uint32_t G[NB];
+    lds_bytes16(s_cls, o, G);
+    covered = segment_cover(s_cls, s_ref, o, rel, G, drifts_of(s_best, g.qt, base, rbase, rfn, g.plo, g.phi, k), k);
     if (dedup2 && covered != ALL)
-      covered |= segment_covered16(s_cls, base, s_ref2, rbase2, q0, k, r2n, g2.plo, g2.phi, s_best2);
+      covered |= segment_cover(s_cls, s_ref2, o, rel, G,
+                               drifts_of(s_best2, g.qt, base, rbase2, r2n, g2.plo, g2.phi, k), k);
   }
   if (dbg & 128) covered = ALL;                    // dev knob: prologue + coverage only
   const bool work = q0 <= last && covered != ALL;
@@ -1473,7 +1544,8 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       // precede the first work pass.
       const char* ce = getenv("PG_K3_CHUNKS");                  // dev knob
       int nch = ce ? std::max(1, std::min(6, atoi(ce))) : K3_CHUNKS;
-      if (ntiles < (uint64_t)nch * 4096) nch = 1;
+      const char* me = getenv("PG_K3_CHUNK_MIN");              // dev knob (tests): tiles per chunk
+      if (ntiles < (uint64_t)nch * (uint64_t)(me ? atoi(me) : 4096)) nch = 1;
       // Overlap needs room on every CU: the coverage blocks are held to ~6 per
       // CU by padding their LDS (covpad bytes of dynamic LDS), which leaves a
       // work block (20 KiB) per CU; the work pass then runs as a persistent

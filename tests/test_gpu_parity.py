@@ -226,3 +226,36 @@ def test_full_size_properties(km):
     # record lengths agree with a host parse
     lens = [len(b"".join(rec.split(b"\n")[1:])) for rec in fasta.split(b">")[1:]]
     assert ctx.records()["seq_len"].tolist() == lens
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+@pytest.mark.parametrize("c", [0, 2])
+def test_k3_chunked_two_references_vs_oracle(oracle_mod, monkeypatch, chunks, c):
+    """The two-pass K3 on two streams (coverage of chunk i+1 beside the work
+    pass of chunk i), with the lead and a second reference record: genomes
+    sharing the lead's variant sites (so ref2 covers them), an N run, a
+    lowercase stretch and records shorter than a stripe."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    monkeypatch.delenv("PG_K3", raising=False)
+    monkeypatch.setenv("PG_K3_CHUNKS", str(chunks))
+    monkeypatch.setenv("PG_K3_CHUNK_MIN", "1")
+    fasta = synth.pangenome(12, 150_000, snp=2e-3, indel=3e-4, seed=77 + chunks)
+    recs = [b">" + r for r in fasta.split(b">")[1:]]
+    body = bytearray(recs[3])
+    body[5000:5040] = b"N" * 40
+    body[9000:9100] = bytes(body[9000:9100]).lower()
+    recs[3] = bytes(body)
+    fasta = b"".join(recs) + b">short\n" + b"ACGT" * 300 + b"\n"
+    ref = oracle_mod.OracleRun(fasta, 27, c)
+    ctx = Context(27)
+    ctx.set_fasta(fasta)
+    ctx.parse()
+    ctx.build_dbg(None, 0, c == 2)
+    keys, masks = ctx.dbg()
+    rk, rm = ref.dbg()
+    assert np.array_equal(keys, rk)
+    assert np.array_equal(masks, rm)
+    ctx.build_rdbg()
+    assert np.array_equal(ctx.rdbg(), ref.rdbg())
+    ctx.close()
