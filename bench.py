@@ -91,11 +91,18 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d (launch N>1 with torch.distributed.run)" % (args.gpus, world))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # PG_BENCH_REHEARSE=1 (development only): every rank on cuda:0 with gloo,
+    # to exercise the N>1 orchestration on a one-GPU box; never a bench number
+    rehearse = os.environ.get("PG_BENCH_REHEARSE") == "1"
+    dev_index = 0 if rehearse else local
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=device)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     from pangenome_amd._lib import Context
     from pangenome_amd.dist import exchange_and_reduce
@@ -105,7 +112,7 @@ def main():
     nbytes = len(fasta)
     del fasta
     torch.cuda.synchronize()
-    ctx = Context(K, local)
+    ctx = Context(K, dev_index)
 
     def step():
         ctx.set_fasta_device(d_fasta.data_ptr(), nbytes, keepalive=d_fasta)
@@ -135,10 +142,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        comm = torch.device("cpu") if rehearse else device
+        t = torch.tensor([elapsed], dtype=torch.float64, device=comm)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tot = torch.tensor([last[0].n_bases, last[0].n_windows // 2, nbytes], dtype=torch.int64, device=device)
+        tot = torch.tensor([last[0].n_bases, last[0].n_windows // 2, nbytes], dtype=torch.int64, device=comm)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
         bases_all, wfw_all, bytes_all = [int(x) for x in tot.tolist()]
     else:
@@ -191,6 +199,8 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.config)
+    if rehearse:
+        out["data"] += "; REHEARSAL: all ranks on cuda:0 over gloo, not a measurement"
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
