@@ -4,18 +4,21 @@ and the calibration passes of tools/calib.sh (gpurun_out/calib_*/) into
 profiles/traffic_<config>.json, the file bench.py reads `roofline.traffic`
 from.  Development tool; not part of the product.
 
-Per kernel and counter, the first dispatch of the process is dropped (the
-warm-up build runs on a larger first-guess table) and the rest averaged.
+Per kernel and counter, values are summed over the dispatches of one bench
+step (K3 runs in chunks) and averaged over the steps after the first (the
+warm-up build runs on a larger first-guess table).
 
 HBM bytes per K3 launch (coverage pass + work pass), from the calibration
 (tools/fetch_calib.hip, profiles/fetch_calib.json):
   * FETCH_SIZE counts 64 B per memory read request.  A random 16-B or 8-B
     load is one 64-B request (counted exactly); a coalesced 16 B/lane stream
     issues 128-B requests, counted at half (MI355X_MICROARCH.md).  The
-    coverage pass is a class-stream read (its random bucket probes hit L2),
-    so its FETCH_SIZE is doubled; the work pass is dominated by random
-    bucket loads, so its FETCH_SIZE is taken as is (its streamed class bytes,
-    <= 0.5 GB, are then under-counted by half - a lower bound).
+    coverage passes (k_cover) stream the class codes and their reference
+    spans and never touch the table, so their FETCH_SIZE is doubled; the work
+    passes are dominated by random bucket loads, so their FETCH_SIZE is taken
+    as is (their segment reads are then under-counted by half - a lower
+    bound).  The table clear (k_zero16, on the side stream inside K3's event
+    span) is streaming 16-byte stores, counted exactly.
   * WRITE_SIZE counts a returning 64-bit atomic (CAS) as 64 B, a
     non-returning atomicOr as 32 B and streaming stores exactly.
 """
@@ -39,17 +42,33 @@ def short(name: str) -> str:
 
 
 def collect(pattern: str, drop_first: bool):
+    """Per kernel and counter: the value per BUILD (one bench step), i.e. the
+    sum over the kernel's dispatches of a step (K3 runs in chunks: several
+    k_cover / k_insert_work dispatches per step), averaged over the steps;
+    the first step (the warm-up build on the larger first-guess table) is
+    dropped.  A step is delimited by the k_reduce dispatches (one per step)."""
     vals = collections.defaultdict(list)
+    per_file_reduce = {}
     for f in sorted(glob.glob(os.path.join(OUT, pattern, "pmc_counter_collection.csv"))):
-        for r in csv.DictReader(open(f)):
-            vals[(short(r["Kernel_Name"]), r["Counter_Name"])].append((int(r["Dispatch_Id"]),
-                                                                        float(r["Counter_Value"])))
-    out = collections.defaultdict(dict)
-    for (k, c), v in vals.items():
-        v.sort()
-        xs = [x for _, x in (v[1:] if drop_first and len(v) > 1 else v)]
-        out[k][c] = sum(xs) / len(xs)
-    return out
+        rows = list(csv.DictReader(open(f)))
+        for r in rows:
+            vals[(short(r["Kernel_Name"]), r["Counter_Name"], f)].append((int(r["Dispatch_Id"]),
+                                                                           float(r["Counter_Value"])))
+        per_file_reduce[f] = sorted({int(r["Dispatch_Id"]) for r in rows if "k_reduce" in r["Kernel_Name"]})
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for (k, c, f), v in vals.items():
+        bounds = per_file_reduce.get(f) or []
+        if not bounds:                                 # no step structure (calibration runs)
+            acc[k][c].append(sum(x for _, x in v) / len(v))
+            continue
+        steps = collections.defaultdict(float)
+        for d, x in v:
+            steps[sum(1 for b in bounds if b < d)] += x   # step index = k_reduce dispatches before d
+        keys = sorted(steps)
+        if drop_first and len(keys) > 1:
+            keys = keys[1:]
+        acc[k][c].append(sum(steps[s] for s in keys) / len(keys))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
 def main(config: str = "c3"):
@@ -59,13 +78,16 @@ def main(config: str = "c3"):
     kb = 1024.0
     t_cov = 2 * pmc[cov]["FETCH_SIZE"] * kb + pmc[cov]["WRITE_SIZE"] * kb
     t_work = (pmc[work]["FETCH_SIZE"] + pmc[work]["WRITE_SIZE"]) * kb if work else 0.0
+    zk = next((k for k in pmc if k.startswith("pg::k_zero16")), None)
+    t_zero = (2 * pmc[zk]["FETCH_SIZE"] + pmc[zk]["WRITE_SIZE"]) * kb if zk else 0.0
     hit = {k: v["TCC_HIT_sum"] / (v["TCC_HIT_sum"] + v["TCC_MISS_sum"]) for k, v in pmc.items()
            if "TCC_HIT_sum" in v and v["TCC_HIT_sum"] + v["TCC_MISS_sum"] > 0}
     res = {
-        "kernel": "K3 = %s (coverage pass) + %s (work pass)" % (cov, work),
+        "kernel": "K3 = %s (coverage passes) + %s (work passes) + the table clear, all chunks of one build"
+                  % (cov, work),
         "config": "%s (bench.py default), 1 x MI355X" % config,
-        "k_insert_hbm_bytes_per_launch": int(t_cov + t_work),
-        "per_pass_bytes": {cov: int(t_cov), work: int(t_work)},
+        "k_insert_hbm_bytes_per_launch": int(t_cov + t_work + t_zero),
+        "per_pass_bytes": {cov: int(t_cov), work: int(t_work), zk: int(t_zero)},
         "method": __doc__.split("HBM bytes per K3 launch", 1)[1].strip(),
         "raw_per_launch": {k: dict(sorted(v.items())) for k, v in sorted(pmc.items())},
         "l2_hit_rate": hit,
