@@ -142,6 +142,16 @@ int pg_rows(pg_ctx* ctx, const uint8_t* rec_flags, int rc1, uint64_t* n_rows);
  * in print order. */
 int pg_rows_export(pg_ctx* ctx, int64_t* rows5, uint64_t cap);
 
+/* ---- text output (host only; no context).  The reference formats these in
+ *      Python loops (kmer_numba.py:1893-1904, :1946-1949).
+ * pg_format_xyz: "%d_%d\t%d_%d\t%d\n" per edge (tuples as unsigned).
+ * pg_format_rows: "qid\tstart\tend\t+|-\tlabel\n" per row; qid of record r
+ * is names[name_off[r] .. name_off[r+1]).  With out == NULL both return the
+ * buffer size they need; otherwise the bytes written, 0 if cap is short. */
+uint64_t pg_format_xyz(const uint64_t* tuples, const int64_t* counts, uint64_t n, char* out, uint64_t cap);
+uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, const int64_t* name_off, char* out,
+                        uint64_t cap);
+
 /* Timings and counters of the last build (see pg_stats). */
 int pg_get_stats(const pg_ctx* ctx, pg_stats* stats);
 

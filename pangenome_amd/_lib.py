@@ -58,6 +58,8 @@ SIGNATURES = {
     "pg_dbg_dump": (C.c_int, [_P, _U64P, _P, _P, _P, _U64P]),
     "pg_dbg_load": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_oakht_capacity": (C.c_uint64, [C.c_uint64]),
+    "pg_format_xyz": (C.c_uint64, [_P, _P, C.c_uint64, _P, C.c_uint64]),
+    "pg_format_rows": (C.c_uint64, [_P, C.c_uint64, _P, _P, _P, C.c_uint64]),
 }
 
 _lib = None
@@ -241,3 +243,36 @@ class Context:
         if n.value:
             check(self.lib.pg_rows_export(self.h, ptr(out), n.value), "pg_rows_export")
         return out
+
+
+# ------------------------------------------------------------------ text output
+def format_xyz(tuples: np.ndarray, counts: np.ndarray) -> bytes:
+    """The `.xyz` side file's text (kmer_numba.py:1901), formatted natively."""
+    lib = load()
+    t = np.ascontiguousarray(tuples, dtype=np.uint64)
+    c = np.ascontiguousarray(counts, dtype=np.int64)
+    n = c.shape[0]
+    cap = lib.pg_format_xyz(None, None, n, None, 0)
+    buf = np.empty(max(cap, 1), np.uint8)
+    m = lib.pg_format_xyz(ptr(t), ptr(c), n, ptr(buf), cap)
+    if n and not m:
+        raise PangenomeError("pg_format_xyz: buffer too small")
+    return buf[:m].tobytes()
+
+
+def format_rows(rows: np.ndarray, names: list) -> bytes:
+    """The region rows (:1947-1949) for records named names[r], natively."""
+    lib = load()
+    r5 = np.ascontiguousarray(rows, dtype=np.int64).reshape(-1, 5)
+    blob = b"".join(names)
+    off = np.zeros(len(names) + 1, np.int64)
+    if names:
+        off[1:] = np.cumsum([len(x) for x in names])
+    nb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
+    n = r5.shape[0]
+    cap = lib.pg_format_rows(ptr(r5), n, ptr(nb), ptr(off), None, 0)
+    buf = np.empty(max(cap, 1), np.uint8)
+    m = lib.pg_format_rows(ptr(r5), n, ptr(nb), ptr(off), ptr(buf), cap)
+    if n and not m:
+        raise PangenomeError("pg_format_rows: buffer too small")
+    return buf[:m].tobytes()

@@ -291,4 +291,50 @@ int pg_rows_export(pg_ctx* x, int64_t* rows5, uint64_t cap) {
   });
 }
 
+// ---- text of the side file and the region rows (host only, no device work)
+static inline char* put_u64(char* o, uint64_t v) {
+  char t[24];
+  int n = 0;
+  do { t[n++] = (char)('0' + v % 10); v /= 10; } while (v);
+  while (n) *o++ = t[--n];
+  return o;
+}
+static inline char* put_i64(char* o, int64_t v) {
+  if (v < 0) { *o++ = '-'; return put_u64(o, (uint64_t)0 - (uint64_t)v); }
+  return put_u64(o, (uint64_t)v);
+}
+
+uint64_t pg_format_xyz(const uint64_t* t, const int64_t* counts, uint64_t n, char* out, uint64_t cap) {
+  if (!out) return n * 106;                               // upper bound: 4 x 20 digits + count + 5 separators
+  if (cap < n * 106) return 0;
+  char* o = out;
+  for (uint64_t i = 0; i < n; ++i) {
+    o = put_u64(o, t[4 * i]); *o++ = '_'; o = put_u64(o, t[4 * i + 1]); *o++ = '\t';
+    o = put_u64(o, t[4 * i + 2]); *o++ = '_'; o = put_u64(o, t[4 * i + 3]); *o++ = '\t';
+    o = put_i64(o, counts[i]); *o++ = '\n';
+  }
+  return (uint64_t)(o - out);
+}
+
+uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, const int64_t* name_off, char* out,
+                        uint64_t cap) {
+  uint64_t need = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const int64_t r = rows5[5 * i];
+    need += (uint64_t)(name_off[r + 1] - name_off[r]) + 3 * 21 + 6;
+  }
+  if (!out) return need;
+  if (cap < need) return 0;
+  char* o = out;
+  for (uint64_t i = 0; i < n; ++i) {
+    const int64_t* w = rows5 + 5 * i;
+    const int64_t r = w[0];
+    std::memcpy(o, names + name_off[r], (size_t)(name_off[r + 1] - name_off[r]));
+    o += name_off[r + 1] - name_off[r];
+    *o++ = '\t'; o = put_i64(o, w[1]); *o++ = '\t'; o = put_i64(o, w[2]);
+    *o++ = '\t'; *o++ = w[3] == 1 ? '+' : '-'; *o++ = '\t'; o = put_i64(o, w[4]); *o++ = '\n';
+  }
+  return (uint64_t)(o - out);
+}
+
 }  // extern "C"

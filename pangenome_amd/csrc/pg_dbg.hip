@@ -831,7 +831,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
     __syncthreads();
     if (work) queue[sub * qcap + s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
   }
-  if (dbg & 8192) return;
+  if ((dbg & 8192) || zero_n16 == 0) return;           // (the chunked launches clear on the side stream)
   const uint64_t per = (zero_n16 + gridDim.x - 1) / gridDim.x;
   const uint64_t z0 = blockIdx.x * per, z1 = z0 + per < zero_n16 ? z0 + per : zero_n16;
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -1634,10 +1634,15 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   c.dump_ready = false;
   const int mode = k3_mode(c, flag);
   const uint64_t ntiles = mode ? make_group_tiles(c, flag) : make_tiles(c, flag);
-  // expected canonical keys: learned from the previous build, else an upper
-  // bound (every forward window distinct, plus the staged npz slots); an
-  // overflow rebuilds larger
-  uint64_t keys = c.cap_hint ? c.cap_hint : std::max<uint64_t>(1024, c.windows_fw + c.n_preload);
+  // expected canonical keys: learned from the previous build, else the
+  // forward windows (every one distinct) divided by the number of long
+  // records up to 4 (a pangenome of G genomes repeats most k-mers G times;
+  // C3's first build would otherwise size a 17 GB table for 19.5 M keys),
+  // plus the staged npz slots; an overflow rebuilds larger
+  uint64_t nlong = 0;
+  for (uint64_t r = 0; r < R; ++r) nlong += flag[r] && c.h_rec_len[r] >= c.k + 2;
+  const uint64_t redund = std::max<uint64_t>(1, std::min<uint64_t>(4, nlong));
+  uint64_t keys = c.cap_hint ? c.cap_hint : std::max<uint64_t>(1024, c.windows_fw / redund + c.n_preload);
   const uint64_t shift = pow5(c.k - 1);
   // PG_K3_DBG (development only): 1 = windows only, 2 = HBM loads without
   // updates, 4 = group form without its HBM phase; PG_K3_KEYS fixes the table

@@ -226,6 +226,41 @@ def label_dict(mcl_text: str, xyz_lines) -> dict:
     return lab
 
 
+def label_table(mcl_text: str, tuples: np.ndarray):
+    """label_dict + label_arrays without the text round trip: the `.mcl` line
+    index of every token (a later line wins, as dict assignment does), then
+    every `.xyz` node (n0_v0 then n1_v1 of each edge, in edge order) not seen
+    yet, numbered in first-appearance order.  Returns (keys, vals, ids) as
+    int64 (keys carry the uint64 key's bits)."""
+    seen = {}
+    flag = 0
+    for line in mcl_text.splitlines(keepends=True):
+        for tok in line[:-1].split("\t"):
+            p = tok.split("_")[:2]
+            seen[(int(p[0]), int(p[1]))] = flag
+        flag += 1
+    t = np.ascontiguousarray(tuples, dtype=np.uint64).reshape(-1, 4)
+    nodes = np.empty((2 * t.shape[0], 2), np.uint64)
+    nodes[0::2] = t[:, 0:2]
+    nodes[1::2] = t[:, 2:4]
+    if nodes.shape[0]:
+        vv = np.ascontiguousarray(nodes).view(np.dtype((np.void, 16))).ravel()
+        _, first = np.unique(vv, return_index=True)
+        uniq = nodes[np.sort(first)]
+    else:
+        uniq = nodes
+    if seen:
+        keep = np.fromiter(((int(a), int(b)) not in seen for a, b in uniq.tolist()), dtype=bool, count=uniq.shape[0])
+        uniq = uniq[keep]
+    mk = np.array([k for k, _ in seen.keys()], dtype=np.uint64)
+    mv = np.array([v for _, v in seen.keys()], dtype=np.uint64)
+    mi = np.fromiter(seen.values(), dtype=np.int64, count=len(seen))
+    keys = np.concatenate([mk, uniq[:, 0]]).view(np.int64)
+    vals = np.concatenate([mv, uniq[:, 1]]).view(np.int64)
+    ids = np.concatenate([mi, flag + np.arange(uniq.shape[0], dtype=np.int64)])
+    return keys, vals, ids
+
+
 def label_arrays(lab: dict):
     n = len(lab)
     keys = np.fromiter((a for a, _ in lab.keys()), dtype=np.int64, count=n)
@@ -256,7 +291,11 @@ def write_db_npz(fn: str, capacity: int, size: int, keys, values, counts, offset
     ksize, vsize, offset] and the keys / values / counts slot arrays."""
     fn = fn[:-4] if fn.endswith(".npz") else fn
     params = np.asarray([capacity, DB_LOAD, size, 1, 1, offset], dtype=np.uint64)
-    np.savez_compressed(fn, parameters=params, keys=keys, values=values, counts=counts)
+    # np.savez (members stored) rather than the reference's savez_compressed:
+    # the same zip of .npy members, read identically by np.load / the
+    # reference's load_on_disk, ~1.4x the bytes, but deflate ran at ~30 MB/s
+    # on the slot arrays (C3: 26 s of a 42 s CLI run, ~1 s stored)
+    np.savez(fn, parameters=params, keys=keys, values=values, counts=counts)
 
 
 def read_db_npz(fn: str):

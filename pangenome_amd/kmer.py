@@ -21,8 +21,34 @@ from time import time
 
 import numpy as np
 
+from collections.abc import Mapping
+
 from . import host
-from ._lib import Context
+from ._lib import Context, format_rows, format_xyz
+
+
+class LabelTable(Mapping):
+    """seq2graph's label dictionary {(key, value): label} (:1918-1944), kept as
+    arrays; the Python dict is built only if it is looked into."""
+
+    def __init__(self, keys, vals, ids):
+        self.keys_, self.vals_, self.ids_ = keys, vals, ids
+        self._d = None
+
+    def _dict(self):
+        if self._d is None:
+            k = self.keys_.view(np.uint64).tolist()
+            self._d = dict(zip(zip(k, self.vals_.tolist()), self.ids_.tolist()))
+        return self._d
+
+    def __getitem__(self, key):
+        return self._dict()[key]
+
+    def __iter__(self):
+        return iter(self._dict())
+
+    def __len__(self):
+        return int(self.ids_.shape[0])
 
 
 # --------------------------------------------------------------- input files
@@ -141,9 +167,8 @@ def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_
     g = rdbg_dict
     tuples, counts = rdbg_edges(g, Ns, chunk, rc, brkpt=brkpt)
     oname = qry + "_rdbg_weight.xyz"
-    xyz = host.xyz_text(tuples, counts)
-    with open(oname, "w") as f:
-        f.write(xyz)
+    with open(oname, "wb") as f:                      # "%d_%d\t%d_%d\t%d\n" (:1893-1904)
+        f.write(format_xyz(tuples, counts))
     if cluster:
         if os.path.isfile("%s.mcl" % oname):
             print("# the mcl has been ran", file=out)
@@ -152,14 +177,20 @@ def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_
             os.system("mcl %s --abc -I 1.5 -te 8 -o %s.mcl -q x -V all" % (oname, oname))
     with open(oname + ".mcl", "r") as f:
         mcl_text = f.read()
-    lab = host.label_dict(mcl_text, xyz.splitlines(keepends=True))
-    g.ctx.set_labels(*host.label_arrays(lab))
+    keys, vals, ids = host.label_table(mcl_text, tuples)     # :1918-1944
+    g.ctx.set_labels(keys, vals, ids)
     flags = host.plan_rows(g.seq_len, g.shape, g.buf, int(Ns))
     rows = g.ctx.rows(flags, bool(rc))
-    text = host.format_rows(rows, g.buf, g.hdr_start, g.hdr_len)
+    names = [bytes(g.buf[int(hs) + 1:int(hs) + int(hl)]) for hs, hl in zip(g.hdr_start, g.hdr_len)]
+    text = format_rows(rows, names)                   # print('%s\t%d\t%d\t%s\t%d') (:1946-1949)
     if text:
-        out.write("\n".join(text) + "\n")
-    return lab
+        if hasattr(out, "buffer"):
+            out.flush()
+            out.buffer.write(text)
+            out.buffer.flush()
+        else:
+            out.write(text.decode())
+    return LabelTable(keys, vals, ids)
 
 
 # ---------------------------------------------------------------------- CLI

@@ -167,3 +167,40 @@ def test_merge_edges_order():
     assert ot[:, 0].tolist() == [1, 3, 7, 9] and oc.tolist() == [5, 7, 1, 2]
     ot, oc = host.merge_edges(lt, lc, t, c, walk_first, np.array([0, 1], np.int64), 1)
     assert ot[:, 0].tolist() == [7, 3, 1, 9] and oc.tolist() == [1, 7, 5, 2]
+
+
+def test_label_table_matches_label_dict():
+    """The array form of the label dictionary equals the text-parsing one
+    (which test_label_dict_matches_oracle pins to the oracle), with and
+    without a non-empty .mcl (repeated tokens: a later line wins)."""
+    from pangenome_amd import host
+    rng = np.random.default_rng(5)
+    nodes = rng.integers(0, 40, (300, 2)).astype(np.uint64)
+    nodes[:, 0] = nodes[:, 0] * np.uint64(1_000_003) + np.uint64(2 ** 62)
+    e = rng.integers(0, 300, (500, 2))
+    tuples = np.concatenate([nodes[e[:, 0]], nodes[e[:, 1]]], axis=1)
+    counts = rng.integers(1, 9, 500)
+    xyz = host.xyz_text(tuples, counts)
+    toks = ["%d_%d" % tuple(nodes[i]) for i in rng.integers(0, 300, 40)]
+    for mcl in ("", "\t".join(toks[:10]) + "\n" + "\t".join(toks[5:25]) + "\n" + toks[30] + "\n"):
+        lab = host.label_dict(mcl, xyz.splitlines(keepends=True))
+        k, v, i = host.label_table(mcl, tuples)
+        got = dict(zip(zip(k.view(np.uint64).tolist(), v.tolist()), i.tolist()))
+        assert got == lab
+        assert list(got) == list(lab)                  # same insertion order
+
+
+def test_native_text_formatters():
+    """pg_format_xyz / pg_format_rows produce the reference's text
+    (kmer_numba.py:1901 and :1949), including unsigned 64-bit keys and
+    negative or large fields."""
+    from pangenome_amd import _lib, host
+    t = np.array([[2 ** 64 - 1, 32, 0, 1], [123456789012345678, 5, 7, 40]], np.uint64)
+    c = np.array([1, 987654321], np.int64)
+    assert _lib.format_xyz(t, c).decode() == host.xyz_text(t, c)
+    rows = np.array([[0, 0, 27, 1, 3], [1, 5, 2 ** 31 - 1, 0, 0], [0, 10, 12, 0, 2 ** 40]], np.int64)
+    names = [b"g0 desc", "quéry".encode()]
+    want = "".join("%s\t%d\t%d\t%s\t%d\n" % (names[r].decode(), s, e, "+" if st == 1 else "-", lab)
+                   for r, s, e, st, lab in rows.tolist())
+    assert _lib.format_rows(rows, names).decode() == want
+    assert _lib.format_xyz(np.zeros((0, 4), np.uint64), np.zeros(0, np.int64)) == b""
