@@ -550,47 +550,6 @@ __device__ __forceinline__ void lds_bytes16(const uint8_t* s, uint32_t idx, uint
   }
 }
 
-// segment_covered with conflict-free 16-byte LDS reads (lds_bytes16): the
-// segment start q0 - 1 has the same alignment in every lane of a tile
-// (segments are IW = 16 windows apart), and so does its reference window.
-__device__ __forceinline__ uint32_t segment_covered16(const uint8_t* s_cls, long long base, const uint8_t* s_ref,
-                                                      long long rbase, long long q0, int k, long long rfn,
-                                                      long long plo, long long phi, const unsigned* s_best) {
-  static_assert(IW == 16, "uniform 16-byte alignment of segment starts");
-  constexpr int NB = (IW + 27 + 1 + 3) / 4;                  // bytes q0-1 .. q0+IW+k-1, k <= 27
-  uint32_t G[NB];
-  lds_bytes16(s_cls, (uint32_t)(base + q0 - 1), G);
-  uint32_t covered = 0;
-  unsigned prev = ~0u;
-  for (int ai = 0; ai < NANCH; ++ai) {
-    const unsigned b = s_best[ai];
-    if (b == ~0u || (b & 0xFFFFu) == prev) continue;
-    prev = b & 0xFFFFu;
-    const long long p0 = q0 - ((long long)(b & 0xFFFFu) - DRIFT);   // reference window of q0
-    if (p0 < 1 || p0 + IW > rfn - k || p0 - 1 < plo || p0 + IW + k > phi) continue;
-    uint32_t Rw[NB];
-    lds_bytes16(s_ref, (uint32_t)(rbase + p0 - 1), Rw);
-    // dwords holding a differing byte; window i (bytes i .. i+k+1) is covered
-    // when it avoids every such dword.  Dword granularity is conservative (a
-    // window next to a mismatch may be left to the work pass, which only costs
-    // a probe) and costs ~30 VALU where the byte-exact run test cost ~150 —
-    // and a wave pays it whenever any of its 64 segments is partial (C3: ~13%
-    // are, so nearly every wave), which made the compare the largest part of
-    // this pass (PMC: 327 of 659 VALU per wave).
-    uint32_t nz = 0;
-#pragma unroll
-    for (int i = 0; i < NB; ++i) nz |= (G[i] != Rw[i] ? 1u : 0u) << i;
-    nz &= (2u << ((k + IW) >> 2)) - 1u;                       // bytes past k+IW do not matter
-    if (nz == 0) return (1u << IW) - 1u;                      // the common case: all context bytes equal
-    const int first = 4 * __builtin_ctz(nz), last = 4 * (31 - __builtin_clz(nz)) + 3;
-    const int ulo = max(0, first - k - 1), uhi = min(IW - 1, last);
-    if (ulo <= uhi) covered |= ((1u << IW) - 1u) & ~(((2u << uhi) - 1u) & ~((1u << ulo) - 1u));
-    else covered = (1u << IW) - 1u;
-    if (covered == (1u << IW) - 1u) return covered;
-  }
-  return covered;
-}
-
 // The distinct drifts the anchors found, with everything segment_cover
 // needs precomputed once per tile in 32-bit tile-relative form (block-uniform,
 // so scalar): segment q0 = qt + rel may use drift j iff lo[j] <= rel <= hi[j]
@@ -629,11 +588,19 @@ __device__ __forceinline__ Drifts drifts_of(const unsigned* s_best, long long qt
 }
 
 // Covered windows of the interior segment whose context bytes start at s_cls
-// index o (rel = q0 - qt), against the reference drifts D (see
-// segment_covered16; same rule, 32-bit and precomputed).
+// index o (rel = q0 - qt), against the reference drifts D: segment_covered's
+// rule, on 16-byte LDS reads (lds_bytes16: the segment start q0 - 1 has the
+// same alignment in every lane of a tile, and so does its reference window),
+// with a partial segment resolved at dword granularity.  Dword granularity is
+// conservative (a window next to a mismatch may be left to the work pass,
+// which only costs a probe) and costs ~30 VALU where the byte-exact run test
+// cost ~150 — and a wave pays it whenever any of its 64 segments is partial
+// (C3: ~13 % are, so nearly every wave), which made the compare the largest
+// part of this pass (PMC: 327 of 659 VALU per wave).
 __device__ __forceinline__ uint32_t segment_cover(const uint8_t* s_cls, const uint8_t* s_ref, uint32_t o, int rel,
                                                   const uint32_t (&G)[(IW + 27 + 1 + 3) / 4], const Drifts& D,
                                                   int k) {
+  static_assert(IW == 16, "uniform 16-byte alignment of segment starts");
   constexpr int NB = (IW + 27 + 1 + 3) / 4;
   constexpr uint32_t ALL = (1u << IW) - 1u;
   uint32_t covered = 0;
@@ -744,7 +711,7 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, in
 
 // K3 coverage pass (two-pass form, the default with a lead record).  One
 // block per tile, like k_insert: the drift against the lead (find_drift),
-// each segment's covered windows (segment_covered16), and the segments left
+// each segment's covered windows (segment_cover), and the segments left
 // with work appended to the queue for k_insert_work.
 // Second reference.  Every follower also differs from the lead at the lead's
 // own variant sites, where all followers share the other allele: with the
