@@ -437,21 +437,31 @@ __device__ __forceinline__ void find_drift(const uint8_t* s_cls, long long base,
     uint32_t x[2];
     lds_bytes(s_cls, (uint32_t)ia, x);                        // one address per anchor: broadcast
     const uint32_t W0 = rw[w], W1 = rw[w + 1], W2 = rw[w + 2];
+    // the 4 candidates' prefilter as a bit set, without branches: one
+    // divergent branch per task (rarely taken) instead of one per candidate
+    uint32_t hit = 0;
 #pragma unroll
     for (int sb = 0; sb < 4; ++sb) {
       const int ib = 4 * w + sb;
-      if (ib < lo || ib > hi || __builtin_amdgcn_alignbyte(W1, W0, sb) != x[0] ||
-          __builtin_amdgcn_alignbyte(W2, W1, sb) != x[1])
-        continue;
-      uint32_t A[ALEN / 4], B[ALEN / 4];
+      const bool h = (ib >= lo) & (ib <= hi) & (__builtin_amdgcn_alignbyte(W1, W0, sb) == x[0]) &
+                     (__builtin_amdgcn_alignbyte(W2, W1, sb) == x[1]);
+      hit |= (uint32_t)h << sb;
+    }
+    if (hit) {
+      uint32_t A[ALEN / 4];
       lds_bytes(s_cls, (uint32_t)ia, A);
-      lds_bytes(s_ref, (uint32_t)ib, B);
-      bool eq = true;
+      do {
+        const int ib = 4 * w + __builtin_ctz(hit);
+        hit &= hit - 1u;
+        uint32_t B[ALEN / 4];
+        lds_bytes(s_ref, (uint32_t)ib, B);
+        bool eq = true;
 #pragma unroll
-      for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
-      const int d = ibhi - ib;                                // delta + DRIFT
-      const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
-      if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
+        for (int i = 0; i < ALEN / 4; ++i) eq &= B[i] == A[i];
+        const int d = ibhi - ib;                              // delta + DRIFT
+        const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+        if (eq) atomicMin(&s_best[ai], (ad << 16) | (unsigned)d);
+      } while (hit);
     }
   };
   if (hint >= 0) {                                            // block-uniform
@@ -604,21 +614,22 @@ __device__ __forceinline__ uint32_t segment_cover(const uint8_t* s_cls, const ui
   constexpr int NB = (IW + 27 + 1 + 3) / 4;
   constexpr uint32_t ALL = (1u << IW) - 1u;
   uint32_t covered = 0;
+  // branch-free per lane: a segment outside drift j's valid range reads its
+  // (staged, in-bounds) bytes anyway and discards the result
 #pragma unroll
   for (int j = 0; j < NANCH; ++j) {
     if (j >= D.n) break;                                      // block-uniform
-    if (rel < D.lo[j] || rel > D.hi[j]) continue;
+    const bool ok = (rel >= D.lo[j]) & (rel <= D.hi[j]);
     uint32_t Rw[NB];
-    lds_bytes16(s_ref, o + (uint32_t)D.off[j], Rw);
+    lds_bytes16(s_ref, o + (uint32_t)(ok ? D.off[j] : 0), Rw);
     uint32_t nz = 0;
 #pragma unroll
     for (int i = 0; i < NB; ++i) nz |= (G[i] != Rw[i] ? 1u : 0u) << i;
     nz &= (2u << ((k + IW) >> 2)) - 1u;                       // bytes past k+IW do not matter
-    if (nz == 0) return ALL;                                  // the common case: all context bytes equal
-    const int first = 4 * __builtin_ctz(nz), last = 4 * (31 - __builtin_clz(nz)) + 3;
+    const int first = 4 * __builtin_ctz(nz | 0x80000000u), last = 4 * (31 - __builtin_clz(nz | 1u)) + 3;
     const int ulo = max(0, first - k - 1), uhi = min(IW - 1, last);
-    covered |= ALL & ~(((2u << uhi) - 1u) & ~((1u << ulo) - 1u));
-    if (covered == ALL) return ALL;
+    const uint32_t c = nz == 0 ? ALL : ALL & ~(((2u << uhi) - 1u) & ~((1u << ulo) - 1u));
+    covered |= ok ? c : 0u;
   }
   return covered;
 }
@@ -750,20 +761,28 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   const Stage g = stage_of(td, k, dedup, rfs, rfn);
   Stage g2 = g;
   if (dedup2) ref_span(g2, k, r2s, r2n);
-  for (long long off = (long long)threadIdx.x * 16; g.a0 + off < g.hi; off += IBLOCK * 16)
-    *reinterpret_cast<uint4*>(s_cls + off) = *reinterpret_cast<const uint4*>(cls + g.a0 + off);
+  // staging: at most two 16-byte chunks per thread and span, predicated
+  // (the spans are < 2 * IBLOCK * 16 bytes: SPAN, RSPAN)
+  static_assert(SPAN + 16 <= 2 * IBLOCK * 16 && RSPAN <= 2 * IBLOCK * 16, "two chunks per thread");
+  auto stage2 = [&](uint8_t* dst, long long from, long long to) {
+    const long long o0 = (long long)threadIdx.x * 16, o1 = o0 + IBLOCK * 16;
+    const bool l0 = from + o0 < to, l1 = from + o1 < to;
+    uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+    if (l0) v0 = *reinterpret_cast<const uint4*>(cls + from + o0);
+    if (l1) v1 = *reinterpret_cast<const uint4*>(cls + from + o1);
+    if (l0) *reinterpret_cast<uint4*>(dst + o0) = v0;
+    if (l1) *reinterpret_cast<uint4*>(dst + o1) = v1;
+  };
+  stage2(s_cls, g.a0, g.hi);
   // dev knobs (PG_K3_DBG, timing only): 512 no drift search (delta 0), 1024
   // no segment compare, 2048 no reference staging, 4096 no queue atomic /
   // writes, 8192 no table clear, 16384 no second reference
   if (dedup) {
-    if (!(dbg & 2048))
-      for (long long off = (long long)threadIdx.x * 16; g.ra0 + off < g.rend; off += IBLOCK * 16)
-        *reinterpret_cast<uint4*>(s_ref + off) = *reinterpret_cast<const uint4*>(cls + g.ra0 + off);
+    if (!(dbg & 2048)) stage2(s_ref, g.ra0, g.rend);
     if (threadIdx.x < NANCH) s_best[threadIdx.x] = (dbg & 512) ? (unsigned)DRIFT : ~0u;
   }
   if (dedup2) {
-    for (long long off = (long long)threadIdx.x * 16; g2.ra0 + off < g2.rend; off += IBLOCK * 16)
-      *reinterpret_cast<uint4*>(s_ref2 + off) = *reinterpret_cast<const uint4*>(cls + g2.ra0 + off);
+    stage2(s_ref2, g2.ra0, g2.rend);
     if (threadIdx.x < NANCH) s_best2[threadIdx.x] = (dbg & 512) ? (unsigned)DRIFT : ~0u;
   }
   __syncthreads();
