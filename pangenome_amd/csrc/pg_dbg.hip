@@ -796,16 +796,24 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   const long long q0 = g.qt + (long long)threadIdx.x * IW;
   constexpr uint32_t ALL = (1u << IW) - 1u;
   uint32_t covered = 0;
+  // the drift sets once per block (one lane's scalar work, read back from
+  // LDS) instead of once per wave
+  __shared__ Drifts s_dr[2];
+  if (dedup && !(dbg & 1024)) {                      // block-uniform
+    if (threadIdx.x == 0) {
+      s_dr[0] = drifts_of(s_best, g.qt, base, rbase, rfn, g.plo, g.phi, k);
+      if (dedup2) s_dr[1] = drifts_of(s_best2, g.qt, base, rbase2, r2n, g2.plo, g2.phi, k);
+    }
+    __syncthreads();
+  }
   if (dedup && q0 > 0 && q0 + IW <= last && !(dbg & 1024)) {
     constexpr int NB = (IW + 27 + 1 + 3) / 4;                // bytes q0-1 .. q0+IW+k-1, k <= 27
     const uint32_t o = (uint32_t)(base + q0 - 1);
     const int rel = (int)threadIdx.x * IW;
     uint32_t G[NB];
     lds_bytes16(s_cls, o, G);
-    covered = segment_cover(s_cls, s_ref, o, rel, G, drifts_of(s_best, g.qt, base, rbase, rfn, g.plo, g.phi, k), k);
-    if (dedup2 && covered != ALL)
-      covered |= segment_cover(s_cls, s_ref2, o, rel, G,
-                               drifts_of(s_best2, g.qt, base, rbase2, r2n, g2.plo, g2.phi, k), k);
+    covered = segment_cover(s_cls, s_ref, o, rel, G, s_dr[0], k);
+    if (dedup2 && covered != ALL) covered |= segment_cover(s_cls, s_ref2, o, rel, G, s_dr[1], k);
   }
   if (dbg & 128) covered = ALL;                    // dev knob: prologue + coverage only
   const bool work = q0 <= last && covered != ALL;
@@ -1166,58 +1174,55 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
   __shared__ unsigned long long s_base;
   __shared__ unsigned long long red[RT / 64];
   uint32_t staged = 0;                             // block-uniform
-  unsigned long long ndbg = 0;
+  uint32_t ndbg = 0;                               // per thread: <= 4 per element it visits
   const uint64_t nunit = (nel + runit<RU>() - 1) / runit<RU>();
   uint4 e[RU];
   if (blockIdx.x < nunit) reduce_load<RU>(T, nb, nel, blockIdx.x, e);
   for (uint64_t u = blockIdx.x; u < nunit; u += gridDim.x) {
     uint4 nx[RU];                                  // next unit in flight while this one is reduced
     if (u + gridDim.x < nunit) reduce_load<RU>(T, nb, nel, u + gridDim.x, nx);
-    uint32_t m[RU][2];
-    uint32_t cnt = 0;
+    // membership bits, computed once: bit 4j + 2h + o = word h of element j
+    // (an overflow slot has one key, in "word 0"), orientation o (B = 1)
+    const uint64_t ubase = u * runit<RU>();
+    const bool prim = ubase + runit<RU>() <= nb;      // block-uniform: no overflow slot in this unit
+    uint32_t mem = 0;
 #pragma unroll
     for (int j = 0; j < RU; ++j) {
-      const uint64_t i = u * runit<RU>() + (uint64_t)j * RT + threadIdx.x;
-      const bool w0 = e[j].x | e[j].y, w1 = e[j].z | e[j].w;
-      if (i < nb) {
-        m[j][0] = w0 ? (e[j].x & MW_MASK) : 0u;
-        m[j][1] = w1 ? (e[j].z & MW_MASK) : 0u;
-      } else {                                     // Slot {key1, mask, aux}
-        m[j][0] = w0 ? e[j].z : 0u;
-        m[j][1] = 0u;
-      }
+      const bool isp = prim || ubase + (uint64_t)j * RT + threadIdx.x < nb;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const uint32_t mm = m[j][h];
-        const bool pa = mm & PRES_A, pb = mm & PRES_B;
-        ndbg += (unsigned long long)pa + (unsigned long long)pb;
-        cnt += (uint32_t)(pa && rdbg_member(mm & MASK12)) + (uint32_t)(pb && rdbg_member((mm >> B_SHIFT) & MASK12));
+        const uint32_t lo = h ? e[j].z : e[j].x, hi = h ? e[j].w : e[j].y;
+        const uint32_t mm = isp ? ((lo | hi) ? (lo & (uint32_t)MW_MASK) : 0u)
+                                : (h == 0 && (e[j].x | e[j].y) ? e[j].z : 0u);   // Slot {key1, mask, aux}
+        const uint32_t pa = (mm >> 12) & 1u, pb = (mm >> 25) & 1u;     // PRES_A, PRES_B
+        ndbg += pa + pb;
+        mem |= (uint32_t)(pa && rdbg_member(mm & MASK12)) << (4 * j + 2 * h);
+        mem |= (uint32_t)(pb && rdbg_member((mm >> B_SHIFT) & MASK12)) << (4 * j + 2 * h + 1);
       }
     }
+    const uint32_t cnt = (uint32_t)__builtin_popcount(mem);
     uint32_t tot;
     const uint32_t pre = block_excl_scan<RT>(cnt, lds, tot);
     if (staged + tot > (uint32_t)rcap<RU>()) {           // block-uniform
       reduce_flush(T, stage, staged, &s_base, out, cap, counters);
       staged = 0;
     }
-    if (cnt) {
+    if (mem) {
       uint32_t o = staged + pre;
 #pragma unroll
       for (int j = 0; j < RU; ++j) {
-        const uint64_t i = u * runit<RU>() + (uint64_t)j * RT + threadIdx.x;
+        const uint64_t i = ubase + (uint64_t)j * RT + threadIdx.x;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const uint32_t mm = m[j][h];
-          const bool ma = (mm & PRES_A) && rdbg_member(mm & MASK12);
-          const bool mb = (mm & PRES_B) && rdbg_member((mm >> B_SHIFT) & MASK12);
-          if (ma || mb) {
+          const uint32_t b = (mem >> (4 * j + 2 * h)) & 3u;
+          if (b) {
             const unsigned long long w = h ? ((unsigned long long)e[j].z | (unsigned long long)e[j].w << 32)
                                            : ((unsigned long long)e[j].x | (unsigned long long)e[j].y << 32);
             // perm(c): the bucket / quotient split of a primary word; overflow
             // slots hold c + 1 (rare: hash it here)
             const uint64_t hv = i < nb ? ((i << T.qbits) | (uint64_t)(w >> MW_BITS)) : T.perm(w - 1ull);
-            if (ma) stage[o++] = hv;
-            if (mb) stage[o++] = hv | (1ull << 63);
+            if (b & 1u) stage[o++] = hv;
+            if (b & 2u) stage[o++] = hv | (1ull << 63);
           }
         }
       }
@@ -1228,8 +1233,9 @@ k_reduce(TableView T, uint64_t nb, uint64_t nel, int k, unsigned long long* __re
     for (int j = 0; j < RU; ++j) e[j] = nx[j];
   }
   if (staged) reduce_flush(T, stage, staged, &s_base, out, cap, counters);
-  for (int o = 32; o > 0; o >>= 1) ndbg += __shfl_down(ndbg, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ndbg;
+  unsigned long long nd = ndbg;
+  for (int o = 32; o > 0; o >>= 1) nd += __shfl_down(nd, o, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = nd;
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long t = 0;
