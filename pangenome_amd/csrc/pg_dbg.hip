@@ -720,6 +720,14 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, in
   block_count(created_acc, flags);                 // every thread: one barrier per wave
 }
 
+// tiles [t, te) of XCD x in chunk c of nch (host and device)
+__host__ __device__ __forceinline__ void xcd_chunk(uint64_t ntiles, int c, int nch, uint64_t x, uint64_t& t,
+                                                   uint64_t& te) {
+  const uint64_t xs = ntiles * x / 8, xl = ntiles * (x + 1) / 8 - xs;
+  t = xs + xl * (uint64_t)c / (uint64_t)nch;
+  te = xs + xl * (uint64_t)(c + 1) / (uint64_t)nch;
+}
+
 // K3 coverage pass (two-pass form, the default with a lead record).  One
 // block per tile, like k_insert: the drift against the lead (find_drift),
 // each segment's covered windows (segment_cover), and the segments left
@@ -732,23 +740,30 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, in
 // own windows are deduped against the lead only; a window it leaves to the
 // lead has the lead's context, key and masks, so "covered by ref2" still
 // means "inserted".
-// The table clear rides along (the pass never touches the table, and the
-// work pass that fills it starts after this kernel): each block zeroes its
-// share after its queue writes.  A persistent, software-pipelined form of
+// Chunks and XCDs: each XCD owns a contiguous eighth of the tile list
+// (stripe-major, so its blocks share reference spans in its own L2), and
+// chunk c of nch launches takes the c-th part of every XCD's eighth, so an
+// XCD's drift hints carry over from the end of its previous chunk to the
+// start of the next (a contiguous chunk jumped each XCD a quarter genome
+// ahead, and the stage-2 search then ran on ~9 % of tiles).  A persistent, software-pipelined form of
 // this kernel (register prefetch of the next tile) measured slower: 1.02 vs
 // 0.76 ms at 64 VGPRs with spills, against one-tile blocks at 8 waves/SIMD.
 __global__ void __launch_bounds__(IBLOCK)
 k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
         long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints, int nrec,
-        uint4* __restrict__ zero, uint64_t zero_n16, uint64_t tile0, int dbg) {
+        uint64_t ntiles, int chunk, int nch, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref2[RSPAN];
   __shared__ unsigned s_best[NANCH], s_best2[NANCH];
   __shared__ uint32_t s_scan[IBLOCK / 64];
   __shared__ unsigned long long s_qbase;
-  const TileDesc td = descs[tile0 + xcd_swizzle(blockIdx.x, gridDim.x)];   // this launch: tiles tile0 ..
+  uint64_t t, te;
+  xcd_chunk(ntiles, chunk, nch, blockIdx.x & 7, t, te);
+  t += blockIdx.x >> 3;
+  if (t >= te) return;                             // (block-uniform, before any barrier)
+  const TileDesc td = descs[t];
   const long long rs = td.rs, rn = td.rn, last = rn - k;
   const bool dedup = ref >= 0 && ref != td.r && !(dbg & 32);  // block-uniform
   const bool dedup2 = dedup && ref2 >= 0 && ref2 != td.r && !(dbg & 16384);
@@ -757,7 +772,9 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   // alternated between stripes ~150 apart and the hint window missed on
   // 15-24 % of the tiles
   int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
-  const int h1 = dedup ? hx[td.r] : -1, h2 = dedup2 ? hx[nrec + td.r] : -1;   // in flight with staging
+  // (no drift known yet: try delta 0 first, the drift at a record's start)
+  int h1 = dedup ? hx[td.r] : -1, h2 = dedup2 ? hx[nrec + td.r] : -1;   // in flight with staging
+  if (!(dbg & 65536)) { h1 = h1 < 0 ? DRIFT : h1; h2 = h2 < 0 ? DRIFT : h2; }
   const Stage g = stage_of(td, k, dedup, rfs, rfn);
   Stage g2 = g;
   if (dedup2) ref_span(g2, k, r2s, r2n);
@@ -776,7 +793,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   stage2(s_cls, g.a0, g.hi);
   // dev knobs (PG_K3_DBG, timing only): 512 no drift search (delta 0), 1024
   // no segment compare, 2048 no reference staging, 4096 no queue atomic /
-  // writes, 8192 no table clear, 16384 no second reference
+  // writes, 16384 no second reference, 65536 no delta-0 first guess
   if (dedup) {
     if (!(dbg & 2048)) stage2(s_ref, g.ra0, g.rend);
     if (threadIdx.x < NANCH) s_best[threadIdx.x] = (dbg & 512) ? (unsigned)DRIFT : ~0u;
@@ -825,11 +842,6 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
     __syncthreads();
     if (work) queue[sub * qcap + s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
   }
-  if ((dbg & 8192) || zero_n16 == 0) return;           // (the chunked launches clear on the side stream)
-  const uint64_t per = (zero_n16 + gridDim.x - 1) / gridDim.x;
-  const uint64_t z0 = blockIdx.x * per, z1 = z0 + per < zero_n16 ? z0 + per : zero_n16;
-  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-  for (uint64_t i = z0 + threadIdx.x; i < z1; i += IBLOCK) zero[i] = z;
 }
 
 // K3 work pass: one queued segment per thread, every lane busy.  The NQ
@@ -1546,11 +1558,16 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       const char* we = getenv("PG_K3_WGRID");
       const size_t covpad = nch > 1 ? (size_t)(pe ? atoi(pe) : K3_COVPAD) : 0;
       const unsigned wgrid = we ? (unsigned)atoi(we) : (unsigned)c.n_cu * K3_WBLK;
-      uint64_t t0[8], qoff[8], qcapc[8];
+      uint64_t gc[8], qoff[8], qcapc[8];               // per chunk: blocks (8 x the longest XCD part)
       uint64_t items = 0;
-      for (int i = 0; i <= nch; ++i) t0[i] = ntiles * (uint64_t)i / (uint64_t)nch;
       for (int i = 0; i < nch; ++i) {
-        qcapc[i] = (t0[i + 1] - t0[i] + NQ - 1) / NQ * IBLOCK;   // per sub-queue
+        gc[i] = 0;
+        for (int x = 0; x < 8; ++x) {
+          uint64_t t, te;
+          xcd_chunk(ntiles, i, nch, (uint64_t)x, t, te);
+          gc[i] = std::max<uint64_t>(gc[i], 8 * (te - t));
+        }
+        qcapc[i] = (gc[i] + NQ - 1) / NQ * IBLOCK;      // per sub-queue
         qoff[i] = items;
         items += NQ * qcapc[i];
       }
@@ -1572,12 +1589,12 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
                          reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
       PG_HIP(hipGetLastError());
       for (int i = 0; i < nch; ++i) {
-        const uint64_t nt = t0[i + 1] - t0[i];
         auto* qi = q + qoff[i];
         auto* qni = qn + (cbytes / 8) * i;
-        hipLaunchKernelGGL(k_cover, dim3((unsigned)nt), b, covpad, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
-                           c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records,
-                           nullptr, 0ull, (uint64_t)t0[i], dbg);
+        if (gc[i])
+          hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), b, covpad, s0, cls, td, qi, qni,
+                             (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
+                             c.k3_hint.as<int>(), (int)c.n_records, ntiles, i, nch, dbg);
         PG_HIP(hipGetLastError());
         PG_HIP(hipEventRecord(c.ev[1 + i], s0));
         PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: clear, work 0 .. i-1, then this
