@@ -503,6 +503,112 @@ __device__ __forceinline__ void find_drift(const uint8_t* s_cls, long long base,
   }
 }
 
+// find_drift for k_cover's two references at once: stage 1 of all 2 x NANCH
+// (reference, anchor) pairs runs in one round, two pairs per wave (32 lanes
+// each: hint +- HWIN2), then stage 2 for a reference whose stage 1 found
+// nothing.  One barrier instead of four; the hints and drift sets are
+// published by the caller.
+constexpr int HWIN2 = 56;
+struct DriftRef {
+  const uint8_t* s;
+  long long rbase, plo, phi;
+  int hint;
+  unsigned* best;
+};
+__device__ __forceinline__ void find_drift_pair(const uint8_t* s_cls, long long base, long long qt, long long rn,
+                                                const DriftRef& A, const DriftRef& B, bool two,
+                                                unsigned* diag = nullptr) {
+  static_assert(2 * NANCH * 32 <= IBLOCK && (2 * HWIN2) / 4 + 2 <= 32, "two pairs per wave in stage 1");
+  constexpr int NW = (2 * DRIFT + 3) / 4 + 2;
+  auto task = [&](const uint8_t* s_ref, int ia, int ibhi, int lo, int hi, int w, unsigned* best) {
+    const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
+    uint32_t x[2];
+    lds_bytes(s_cls, (uint32_t)ia, x);
+    const uint32_t W0 = rw[w], W1 = rw[w + 1], W2 = rw[w + 2];
+    uint32_t hit = 0;
+#pragma unroll
+    for (int sb = 0; sb < 4; ++sb) {
+      const int ib = 4 * w + sb;
+      const bool h = (ib >= lo) & (ib <= hi) & (__builtin_amdgcn_alignbyte(W1, W0, sb) == x[0]) &
+                     (__builtin_amdgcn_alignbyte(W2, W1, sb) == x[1]);
+      hit |= (uint32_t)h << sb;
+    }
+    if (hit) {
+      uint32_t Aw[ALEN / 4];
+      lds_bytes(s_cls, (uint32_t)ia, Aw);
+      do {
+        const int ib = 4 * w + __builtin_ctz(hit);
+        hit &= hit - 1u;
+        uint32_t Bw[ALEN / 4];
+        lds_bytes(s_ref, (uint32_t)ib, Bw);
+        bool eq = true;
+#pragma unroll
+        for (int i = 0; i < ALEN / 4; ++i) eq &= Bw[i] == Aw[i];
+        const int d = ibhi - ib;
+        const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+        if (eq) atomicMin(best, (ad << 16) | (unsigned)d);
+      } while (hit);
+    }
+  };
+  auto geom = [&](const DriftRef& R, int ai, int& ia, int& ibhi, int& lo, int& hi) {
+    const long long a = qt + 8 + (long long)ai * ASTEP;
+    ia = (int)(base + a);
+    ibhi = (int)(R.rbase + a + DRIFT);
+    lo = max(ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
+    hi = a + ALEN > rn ? -1 : min(ibhi, (int)(R.rbase + R.phi) - ALEN);
+  };
+  {
+    const int pr = (int)threadIdx.x >> 5, m = (int)threadIdx.x & 31;
+    const bool second = pr >= NANCH;
+    if (pr < 2 * NANCH && (!second || two)) {
+      const DriftRef& R = second ? B : A;
+      const int ai = second ? pr - NANCH : pr;
+      if (R.hint >= 0) {
+        int ia, ibhi, lo, hi;
+        geom(R, ai, ia, ibhi, lo, hi);
+        lo = max(lo, ibhi - (R.hint + HWIN2));
+        hi = min(hi, ibhi - (R.hint - HWIN2));
+        const int w = (lo >> 2) + m;
+        if (lo <= hi && 4 * w <= hi) task(R.s, ia, ibhi, lo, hi, w, R.best + ai);
+      }
+    }
+  }
+  __syncthreads();
+  static_assert(NANCH == 3, "any-anchor test");
+  const bool anyA = (A.best[0] & A.best[1] & A.best[2]) != ~0u;            // block-uniform
+  const bool anyB = !two || (B.best[0] & B.best[1] & B.best[2]) != ~0u;
+  if (diag && threadIdx.x == 0) {                             // dev counters: hint stage ran / missed
+    atomicAdd(diag, A.hint >= 0 ? 1u : 0u);
+    atomicAdd(diag + 1, anyA ? 0u : 1u);
+    if (two) {
+      atomicAdd(diag + 2, B.hint >= 0 ? 1u : 0u);
+      atomicAdd(diag + 3, anyB ? 0u : 1u);
+    }
+  }
+  if (anyA && anyB) return;                                   // (the caller's barrier follows)
+#pragma unroll 1
+  for (int ri = 0; ri < 2; ++ri) {
+    const DriftRef& R = ri ? B : A;
+    if (ri ? anyB : anyA) continue;                           // block-uniform
+#pragma unroll 1
+    for (int ai = 0; ai < NANCH; ++ai) {
+      int ia, ibhi, lo, hi;
+      geom(R, ai, ia, ibhi, lo, hi);
+      for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += IBLOCK)
+        task(R.s, ia, ibhi, lo, hi, w, R.best + ai);
+    }
+  }
+  __syncthreads();
+}
+
+// the hint a tile publishes: the drift of its first anchor that matched
+__device__ __forceinline__ void publish_hint(const unsigned* best, int* hint_out) {
+  int h = -1;
+  for (int ai = NANCH - 1; ai >= 0; --ai)
+    if (best[ai] != ~0u) h = (int)(best[ai] & 0xFFFFu);
+  if (h >= 0) *hint_out = h;
+}
+
 // Covered windows of the interior segment q0 .. q0+IW-1 (bit i: window q0+i):
 // its bytes [q-1, q+k] equal the reference's at q - delta for one of the
 // anchors' drifts (reference window interior and staged too).
@@ -773,6 +879,9 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   // 15-24 % of the tiles
   int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
   // (no drift known yet: try delta 0 first, the drift at a record's start)
+  // (plain loads may return a stale line from this CU's L1: device-scope
+  // loads cut the stage-2 searches 14 k -> 0.9 k per build and k_cover alone
+  // 1.56 -> 1.49 ms, yet the whole K3 span measured ~0.5 % slower with them)
   int h1 = dedup ? hx[td.r] : -1, h2 = dedup2 ? hx[nrec + td.r] : -1;   // in flight with staging
   if (!(dbg & 65536)) { h1 = h1 < 0 ? DRIFT : h1; h2 = h2 < 0 ? DRIFT : h2; }
   const Stage g = stage_of(td, k, dedup, rfs, rfn);
@@ -806,18 +915,20 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   const long long base = rs - g.a0, rbase = rfs - g.ra0, rbase2 = r2s - g2.ra0;   // LDS index of position 0
   unsigned* diag = (dbg & 64) ? reinterpret_cast<unsigned*>(hints + 16 * nrec + 2) : nullptr;   // dev counters
   if (dedup && !(dbg & 512))
-    find_drift(s_cls, base, s_ref, rbase, g.qt, rn, g.plo, g.phi, h1, s_best, hx + td.r, diag);
-  if (dedup2 && !(dbg & 512))
-    find_drift(s_cls, base, s_ref2, rbase2, g.qt, rn, g2.plo, g2.phi, h2, s_best2, hx + nrec + td.r,
-               diag ? diag + 2 : nullptr);
+    find_drift_pair(s_cls, base, g.qt, rn, DriftRef{s_ref, rbase, g.plo, g.phi, h1, s_best},
+                    DriftRef{s_ref2, rbase2, g2.plo, g2.phi, h2, s_best2}, dedup2, diag);
   const long long q0 = g.qt + (long long)threadIdx.x * IW;
   constexpr uint32_t ALL = (1u << IW) - 1u;
   uint32_t covered = 0;
-  // the drift sets once per block (one lane's scalar work, read back from
-  // LDS) instead of once per wave
+  // hints and the drift sets once per block (one lane's scalar work, read
+  // back from LDS) instead of once per wave
   __shared__ Drifts s_dr[2];
-  if (dedup && !(dbg & 1024)) {                      // block-uniform
+  if (dedup) {                                       // block-uniform
     if (threadIdx.x == 0) {
+      if (!(dbg & 512)) {
+        publish_hint(s_best, hx + td.r);
+        if (dedup2) publish_hint(s_best2, hx + nrec + td.r);
+      }
       s_dr[0] = drifts_of(s_best, g.qt, base, rbase, rfn, g.plo, g.phi, k);
       if (dedup2) s_dr[1] = drifts_of(s_best2, g.qt, base, rbase2, r2n, g2.plo, g2.phi, k);
     }
