@@ -827,11 +827,12 @@ k_insert(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, in
 }
 
 // tiles [t, te) of XCD x in chunk c of nch (host and device)
-__host__ __device__ __forceinline__ void xcd_chunk(uint64_t ntiles, int c, int nch, uint64_t x, uint64_t& t,
-                                                   uint64_t& te) {
+// (a chunk is the fraction [b0, b1) / bt of every XCD's eighth)
+__host__ __device__ __forceinline__ void xcd_chunk(uint64_t ntiles, uint32_t b0, uint32_t b1, uint32_t bt, uint64_t x,
+                                                   uint64_t& t, uint64_t& te) {
   const uint64_t xs = ntiles * x / 8, xl = ntiles * (x + 1) / 8 - xs;
-  t = xs + xl * (uint64_t)c / (uint64_t)nch;
-  te = xs + xl * (uint64_t)(c + 1) / (uint64_t)nch;
+  t = xs + xl * b0 / bt;
+  te = xs + xl * b1 / bt;
 }
 
 // K3 coverage pass (two-pass form, the default with a lead record).  One
@@ -858,7 +859,7 @@ __global__ void __launch_bounds__(IBLOCK)
 k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
         long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints, int nrec,
-        uint64_t ntiles, int chunk, int nch, int dbg) {
+        uint64_t ntiles, uint32_t b0, uint32_t b1, uint32_t bt, int dbg) {
   __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref2[RSPAN];
@@ -866,7 +867,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   __shared__ uint32_t s_scan[IBLOCK / 64];
   __shared__ unsigned long long s_qbase;
   uint64_t t, te;
-  xcd_chunk(ntiles, chunk, nch, blockIdx.x & 7, t, te);
+  xcd_chunk(ntiles, b0, b1, bt, blockIdx.x & 7, t, te);
   t += blockIdx.x >> 3;
   if (t >= te) return;                             // (block-uniform, before any barrier)
   const TileDesc td = descs[t];
@@ -1661,6 +1662,24 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       int nch = ce ? std::max(1, std::min(6, atoi(ce))) : K3_CHUNKS;
       const char* me = getenv("PG_K3_CHUNK_MIN");              // dev knob (tests): tiles per chunk
       if (ntiles < (uint64_t)nch * (uint64_t)(me ? atoi(me) : 4096)) nch = 1;
+      // chunk sizes (weights; cb = cumulative): the work stream is the
+      // critical path (K3 ~ first coverage pass + all work passes), so the
+      // first chunk is small and the work stream starts early
+      uint32_t cb[8] = {0};
+      {
+        const char* se = getenv("PG_K3_SPLIT");                  // dev knob: "w0,w1,..."
+        int n = 0;
+        if (se && nch > 1) {
+          for (const char* x = se; *x && n < 6; ++n) {
+            cb[n + 1] = cb[n] + (uint32_t)std::max(1, atoi(x));
+            while (*x && *x != ',') ++x;
+            if (*x == ',') ++x;
+          }
+          nch = n;
+        } else {
+          for (int i = 0; i < nch; ++i) cb[i + 1] = cb[i] + 1;
+        }
+      }
       // Overlap needs room on every CU: the coverage blocks are held to ~6 per
       // CU by padding their LDS (covpad bytes of dynamic LDS), which leaves a
       // work block (20 KiB) per CU; the work pass then runs as a persistent
@@ -1675,7 +1694,7 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
         gc[i] = 0;
         for (int x = 0; x < 8; ++x) {
           uint64_t t, te;
-          xcd_chunk(ntiles, i, nch, (uint64_t)x, t, te);
+          xcd_chunk(ntiles, cb[i], cb[i + 1], cb[nch], (uint64_t)x, t, te);
           gc[i] = std::max<uint64_t>(gc[i], 8 * (te - t));
         }
         qcapc[i] = (gc[i] + NQ - 1) / NQ * IBLOCK;      // per sub-queue
@@ -1705,7 +1724,7 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
         if (gc[i])
           hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), b, covpad, s0, cls, td, qi, qni,
                              (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
-                             c.k3_hint.as<int>(), (int)c.n_records, ntiles, i, nch, dbg);
+                             c.k3_hint.as<int>(), (int)c.n_records, ntiles, cb[i], cb[i + 1], cb[nch], dbg);
         PG_HIP(hipGetLastError());
         PG_HIP(hipEventRecord(c.ev[1 + i], s0));
         PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: clear, work 0 .. i-1, then this
