@@ -117,10 +117,10 @@ def main():
     def step():
         ctx.set_fasta_device(d_fasta.data_ptr(), nbytes, keepalive=d_fasta)
         ctx.parse()
+        if world == 1:                      # seq2rdbg + dbg2rdbg in one call (pg_build)
+            st = ctx.build(None, 0, True)
+            return st, st, st.n_dbg, st.n_rdbg, 0
         st_b = ctx.build_dbg(None, 0, True)
-        if world == 1:
-            st = ctx.build_rdbg()
-            return st_b, st, st.n_dbg, st.n_rdbg, 0
         n_dbg, n_rdbg, _, sent = exchange_and_reduce(ctx, world, rank, device, bool(st_b.sentinel))
         return st_b, ctx.stats(), n_dbg, n_rdbg, sent
 

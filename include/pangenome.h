@@ -87,6 +87,12 @@ int pg_build_dbg(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0
  * Marks members in the device table and materialises the rdBG keys. */
 int pg_build_rdbg(pg_ctx* ctx, uint64_t* n_rdbg, pg_stats* stats);
 
+/* seq2rdbg then dbg2rdbg (kmer_numba.py:1234-1268, :1313-1321) in one call:
+ * pg_build_dbg + pg_build_rdbg with the same results, K5 enqueued right
+ * behind K3 (no host round trip between them; its key capacity comes from the
+ * previous build and is re-run if outgrown). */
+int pg_build(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0, uint64_t* n_rdbg, pg_stats* stats);
+
 /* dump()'s keys/values (kmer_numba.py:243-261) of the dBG, unordered.
  * keys == NULL: only *n is set. */
 int pg_dbg_export(pg_ctx* ctx, uint64_t* keys, uint16_t* masks, uint64_t cap, uint64_t* n);

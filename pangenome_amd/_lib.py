@@ -45,6 +45,7 @@ SIGNATURES = {
     "pg_records": (C.c_int, [_P, _P, _P, _P, _P]),
     "pg_build_dbg": (C.c_int, [_P, _P, C.c_int, C.c_int, _SP]),
     "pg_build_rdbg": (C.c_int, [_P, _U64P, _SP]),
+    "pg_build": (C.c_int, [_P, _P, C.c_int, C.c_int, _U64P, _SP]),
     "pg_dbg_export": (C.c_int, [_P, _P, _P, C.c_uint64, _U64P]),
     "pg_rdbg_export": (C.c_int, [_P, _P, C.c_uint64, _U64P]),
     "pg_dbg_partition": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
@@ -162,6 +163,15 @@ class Context:
         st = PgStats()
         n = C.c_uint64()
         check(self.lib.pg_build_rdbg(self.h, C.byref(n), C.byref(st)), "pg_build_rdbg")
+        return st
+
+    def build(self, rec_flags=None, extra_empty: int = 0, rc0: bool = True) -> PgStats:
+        """build_dbg + build_rdbg in one call (pg_build: K5 runs right behind K3)."""
+        st = PgStats()
+        n = C.c_uint64()
+        f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
+        check(self.lib.pg_build(self.h, ptr(f), int(extra_empty), int(bool(rc0)), C.byref(n), C.byref(st)),
+              "pg_build")
         return st
 
     def stats(self) -> PgStats:

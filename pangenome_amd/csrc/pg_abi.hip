@@ -81,8 +81,10 @@ void pg_destroy(pg_ctx* x) {
   for (auto* b : bufs) b->release();
   c.rec_pack.release();
   c.h_pin.release();
+  c.k5_pin.release();
   c.t0.destroy();
   c.t1.destroy();
+  c.t5.destroy();
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c.stream2);
@@ -165,6 +167,24 @@ int pg_build_rdbg(pg_ctx* x, uint64_t* n_rdbg, pg_stats* stats) {
     if (!x) throw pg::Error(PG_EINVAL, "pg_build_rdbg: ctx is NULL");
     PG_HIP(hipSetDevice(x->c.device));
     pg::build_rdbg(x->c);
+    if (n_rdbg) *n_rdbg = x->c.n_rdbg;
+    fill_stats(x->c, stats);
+  });
+}
+
+int pg_build(pg_ctx* x, const uint8_t* rec_flags, int extra_empty, int rc0, uint64_t* n_rdbg, pg_stats* stats) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_build: ctx is NULL");
+    PG_HIP(hipSetDevice(x->c.device));
+    x->c.spec_k5 = true;
+    try {
+      pg::build_dbg(x->c, rec_flags, extra_empty, rc0 != 0);
+    } catch (...) {
+      x->c.spec_k5 = false;
+      throw;
+    }
+    x->c.spec_k5 = false;
+    pg::build_rdbg(x->c);                      // (a no-op when K5 already ran behind K3)
     if (n_rdbg) *n_rdbg = x->c.n_rdbg;
     fill_stats(x->c, stats);
   });

@@ -1751,6 +1751,9 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
   PG_HIP(hipGetLastError());
 }
 
+static void reduce_enqueue(Ctx& c, uint64_t cap_keys);
+static bool reduce_finish(Ctx& c);
+
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   if (!c.parsed) throw Error(-22, "build_dbg: no parsed FASTA (call pg_parse first)");
   const uint64_t R = c.n_records;
@@ -1806,6 +1809,8 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     }
     if (extra_empty) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, flags);
     merge_preload(c, flags);
+    const bool spec = c.spec_k5 && c.rdbg_hint && !dbg;
+    if (spec) reduce_enqueue(c, c.rdbg_hint);
     unsigned sentinel = 0, overflow = 0;
     uint64_t created = 0;
     read_flags(c, sentinel, overflow, created);
@@ -1831,6 +1836,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
       c.cap_hint = std::max<uint64_t>(1024, created + created / 4);
       c.built = true;
       ++c.build_gen;
+      if (spec && !reduce_finish(c)) c.rdbg_hint = 0;   // outgrown: build_rdbg runs K5 again
       return;
     }
     keys = std::max<uint64_t>(keys * 4, created * 2);
@@ -1838,14 +1844,17 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   throw Error(-12, "build_dbg: hash table overflow after resizing");
 }
 
-void build_rdbg(Ctx& c) {
-  if (!c.built) throw Error(-22, "build_rdbg: no dBG (call pg_build_dbg first)");
-  c.rdbg_keys.reserve(8 * (2 * c.n_canon + 2));
+// K5 in two halves, so that pg_build can enqueue it right behind K3 (before
+// build_dbg's flag read-back, with a capacity learned from the last build)
+// and read both back with one synchronisation.
+constexpr size_t K5_CNT_BYTES = 8 * 8 * 65;             // [0] member count, [8 * (1 + i)] dBG size partials
+static void reduce_enqueue(Ctx& c, uint64_t cap_keys) {
+  c.rdbg_keys.reserve(8 * (cap_keys + 1));
   DevBuf& cnt = c.n_sel;
-  constexpr size_t CNT_BYTES = 8 * 8 * 65;              // [0] member count, [8 * (1 + i)] dBG size partials
-  cnt.reserve(CNT_BYTES);
-  PG_HIP(hipMemsetAsync(cnt.p, 0, CNT_BYTES, c.stream));
-  c.t0.start(c.stream);
+  cnt.reserve(K5_CNT_BYTES);
+  PG_HIP(hipMemsetAsync(cnt.p, 0, K5_CNT_BYTES, c.stream));
+  c.t5.init();
+  c.t5.start(c.stream);
   const uint64_t nel = c.cap + c.ovf_cap;               // 16-byte elements: buckets, then overflow slots
   const int ru = getenv("PG_K5_RU") ? atoi(getenv("PG_K5_RU")) : RU_DEF;            // dev knobs
   const unsigned rg = getenv("PG_K5_GRID") ? (unsigned)atoi(getenv("PG_K5_GRID")) : RGRID;
@@ -1859,15 +1868,19 @@ void build_rdbg(Ctx& c) {
                        c.k, rk, 2 * c.n_canon + 1, rc);
   else
     hipLaunchKernelGGL(k_reduce<2>, dim3(grid_for(nel / runit<2>(), 1, rg)), dim3(RT), 0, c.stream, c.tv, c.cap, nel,
-                       c.k, rk, 2 * c.n_canon + 1, rc);
+                       c.k, rk, cap_keys, rc);
   PG_HIP(hipGetLastError());
-  c.t0.stop(c.stream);
-  c.h_pin.reserve(CNT_BYTES);
-  PG_HIP(hipMemcpyAsync(c.h_pin.p, cnt.p, CNT_BYTES, hipMemcpyDeviceToHost, c.stream));
-  c.sync();
-  const unsigned long long* res = c.h_pin.as<unsigned long long>();
-  c.ms_scan = c.t0.ms();
-  if (res[0] > 2 * c.n_canon + 1) throw Error(-5, "build_rdbg: member count exceeds the table's key count");
+  c.t5.stop(c.stream);
+  c.k5_pin.reserve(K5_CNT_BYTES);
+  PG_HIP(hipMemcpyAsync(c.k5_pin.p, cnt.p, K5_CNT_BYTES, hipMemcpyDeviceToHost, c.stream));
+  c.k5_cap = cap_keys;
+}
+
+// after the stream has synchronised; false if the rdBG outgrew k5_cap
+static bool reduce_finish(Ctx& c) {
+  const unsigned long long* res = c.k5_pin.as<unsigned long long>();
+  if (res[0] > c.k5_cap) return false;
+  c.ms_scan = c.t5.ms();
   c.n_rdbg = res[0];
   c.n_dbg = 0;
   for (int i = 0; i < 64; ++i) c.n_dbg += res[8 * (1 + i)];
@@ -1880,6 +1893,16 @@ void build_rdbg(Ctx& c) {
     c.n_dbg += 1;
   }
   c.reduced = true;
+  c.rdbg_hint = c.n_rdbg + c.n_rdbg / 4 + 4096;
+  return true;
+}
+
+void build_rdbg(Ctx& c) {
+  if (!c.built) throw Error(-22, "build_rdbg: no dBG (call pg_build_dbg first)");
+  if (c.reduced) return;                                // K5 already ran behind K3 (pg_build)
+  reduce_enqueue(c, 2 * c.n_canon + 1);
+  c.sync();
+  if (!reduce_finish(c)) throw Error(-5, "build_rdbg: member count exceeds the table's key count");
 }
 
 uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {

@@ -113,6 +113,10 @@ struct Ctx {
   DevBuf scratch;                 // rocPRIM temp storage
   DevBuf rec_pack;                // int64 [5][R]: the record table gathered for one copy
   PinBuf h_pin;                   // pinned staging for small device-to-host reads
+  PinBuf k5_pin;                  // K5's counters (read back together with build_dbg's flags)
+  uint64_t k5_cap = 0;            // rdBG key capacity of the K5 run in flight
+  uint64_t rdbg_hint = 0;         // rdBG keys of the last build (+25 %): speculative K5 capacity
+  bool spec_k5 = false;           // pg_build: K5 is enqueued behind K3, before build_dbg's sync
   uint64_t n_lines = 0, n_records = 0, n_bases = 0, n_nl = 0;
   std::vector<int64_t> h_rec_start, h_rec_len, h_rec_hdr_start, h_rec_hdr_len, h_rec_ptr;
   bool parsed = false;
@@ -171,7 +175,7 @@ struct Ctx {
   uint64_t dump_size = 0, dump_sentinel = 0;
 
   // timings of the last calls (ms, HIP events on `stream`)
-  Timer t0, t1;
+  Timer t0, t1, t5;
   double ms_parse = 0, ms_clear = 0, ms_insert = 0, ms_short = 0, ms_scan = 0;
   double ms_total_build = 0;
 

@@ -259,3 +259,33 @@ def test_k3_chunked_two_references_vs_oracle(oracle_mod, monkeypatch, chunks, c)
     ctx.build_rdbg()
     assert np.array_equal(ctx.rdbg(), ref.rdbg())
     ctx.close()
+
+
+@pytest.mark.gpu
+def test_pg_build_speculative_k5(oracle_mod):
+    """pg_build (K5 enqueued behind K3 with the previous build's rdBG size as
+    its capacity) against the oracle: a first build (no capacity known: K5
+    after the flag read), a repeat (speculative K5), then a larger, more
+    varied input whose rdBG outgrows the learned capacity (K5 re-run)."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    small = synth.pangenome(4, 40_000, snp=1e-4, indel=0.0, seed=5)
+    large = synth.pangenome(10, 120_000, snp=3e-3, indel=5e-4, seed=6)
+    ctx, two = Context(27), Context(27)
+    for fasta in (small, small, large, large):
+        ref = oracle_mod.OracleRun(fasta, 27, 2)
+        ctx.set_fasta(fasta)
+        ctx.parse()
+        st = ctx.build(None, 0, True)
+        two.set_fasta(fasta)                       # the two-call path
+        two.parse()
+        two.build_dbg(None, 0, True)
+        st2 = two.build_rdbg()
+        assert (st.n_dbg, st.n_rdbg) == (st2.n_dbg, st2.n_rdbg)
+        assert np.array_equal(ctx.rdbg(), ref.rdbg())
+        assert st.n_rdbg == len(ref.rdbg())
+        keys, masks = ctx.dbg()
+        rk, rm = ref.dbg()
+        assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
+    ctx.close()
+    two.close()
