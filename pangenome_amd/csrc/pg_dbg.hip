@@ -1467,6 +1467,7 @@ constexpr int N_FLAGS = 16 * (N_CNT + 2) + 16;       // + diagnostic counters
 static void alloc_table(Ctx& c, uint64_t keys) {
   uint64_t buckets = 0, ovf = 0;
   TableView t = make_geometry(c.k, keys, buckets, ovf);
+  if (c.pre_ptr && 16 * buckets > c.table.cap) PG_HIP(hipStreamSynchronize(c.stream2));   // its buffer is freed
   c.table.reserve(16 * buckets);
   c.ovf.reserve(sizeof(Slot) * ovf);
   t.prim = c.table.as<unsigned long long>();
@@ -1484,9 +1485,37 @@ __global__ void __launch_bounds__(256) k_zero16(uint4* __restrict__ p, uint64_t 
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256ull) p[i] = z;
 }
 
-// primary = false: the K3 coverage pass clears the primary buckets itself
+// The next build's table clear, queued on stream2 by pg_parse so that it runs
+// beside the parse instead of beside the first coverage pass (parse
+// invalidates the dBG anyway; a build whose table keeps its place and size
+// skips its own clear).  A narrow grid (PRECLEAR_GRID blocks) trickles the
+// stores out without taking the parse's CUs: C3, per step, K3 1.92 -> 1.73
+// ms for parse 0.45 -> 0.57 ms (8192 blocks: parse 0.66 ms).
+constexpr unsigned PRECLEAR_GRID = 128, K3_ZGRID = 256;
+void preclear_table(Ctx& c) {
+  const char* ge = getenv("PG_PRECLEAR_GRID");            // dev knob (0: no pre-clear)
+  if (!c.table.p || !c.cap || (ge && atoi(ge) == 0)) return;
+  PG_HIP(hipEventRecord(c.ev[14], c.stream));            // after everything queued on the table
+  PG_HIP(hipStreamWaitEvent(c.stream2, c.ev[14], 0));
+  hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, ge ? (unsigned)atoi(ge) : PRECLEAR_GRID)), dim3(256), 0,
+                     c.stream2,
+                     reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
+  PG_HIP(hipGetLastError());
+  c.pre_ptr = c.table.p;
+  c.pre_n16 = c.cap;
+}
+
+// primary = false: the two-pass K3 clears the primary buckets on stream2
+// (launch_insert), unless pg_parse's clear there already covers them
 static void clear_table(Ctx& c, bool primary) {
-  if (primary) {
+  const bool pre = c.pre_ptr && c.pre_ptr == c.table.p && c.pre_n16 >= c.cap;
+  if (c.pre_ptr && primary) {                            // the table is written on stream: wait for it
+    PG_HIP(hipEventRecord(c.ev[14], c.stream2));
+    PG_HIP(hipStreamWaitEvent(c.stream, c.ev[14], 0));
+  }
+  c.pre_ptr = nullptr;
+  c.k3_skip_clear = pre && !primary;                     // (stream2 runs it before the work passes)
+  if (primary && !pre) {
     hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, c.stream,
                        reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
     PG_HIP(hipGetLastError());
@@ -1715,9 +1744,13 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       // the clear on s1, after everything already queued on s0
       PG_HIP(hipEventRecord(c.ev[0], s0));
       PG_HIP(hipStreamWaitEvent(s1, c.ev[0], 0));
-      hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, 8192)), dim3(256), 0, s1,
-                         reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
-      PG_HIP(hipGetLastError());
+      if (!c.k3_skip_clear) {
+        const char* ze = getenv("PG_K3_ZGRID");                  // dev knob
+        hipLaunchKernelGGL(k_zero16, dim3(grid_for(c.cap, 256, ze ? (unsigned)atoi(ze) : K3_ZGRID)), dim3(256), 0, s1,
+                           reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
+        PG_HIP(hipGetLastError());
+      }
+      c.k3_skip_clear = false;
       for (int i = 0; i < nch; ++i) {
         auto* qi = q + qoff[i];
         auto* qni = qn + (cbytes / 8) * i;

@@ -117,6 +117,9 @@ struct Ctx {
   uint64_t k5_cap = 0;            // rdBG key capacity of the K5 run in flight
   uint64_t rdbg_hint = 0;         // rdBG keys of the last build (+25 %): speculative K5 capacity
   bool spec_k5 = false;           // pg_build: K5 is enqueued behind K3, before build_dbg's sync
+  void* pre_ptr = nullptr;        // table clear queued on stream2 by pg_parse (beside the parse)
+  uint64_t pre_n16 = 0;           //   its 16-byte buckets
+  bool k3_skip_clear = false;     // launch_insert: the table is already cleared on stream2
   uint64_t n_lines = 0, n_records = 0, n_bases = 0, n_nl = 0;
   std::vector<int64_t> h_rec_start, h_rec_len, h_rec_hdr_start, h_rec_hdr_len, h_rec_ptr;
   bool parsed = false;
@@ -184,6 +187,7 @@ struct Ctx {
 
 // pg_parse.hip
 void parse_fasta(Ctx& c);
+void preclear_table(Ctx& c);   // pg_dbg.hip: the next build's table clear, on stream2
 // pg_dbg.hip
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0);
 void build_rdbg(Ctx& c);

@@ -355,6 +355,7 @@ __global__ void k_pack_records(uint64_t R, const long long* __restrict__ rs, con
 
 void parse_fasta(Ctx& c) {
   upload_byte_class();
+  preclear_table(c);                                        // beside the parse, on stream2
   hipStream_t st = c.stream;
   const uint64_t n = c.n_bytes;
   c.parsed = false;

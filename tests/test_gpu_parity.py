@@ -262,7 +262,7 @@ def test_k3_chunked_two_references_vs_oracle(oracle_mod, monkeypatch, chunks, c)
 
 
 @pytest.mark.gpu
-def test_pg_build_speculative_k5(oracle_mod):
+def test_pg_build_speculative_k5(oracle_mod, monkeypatch):
     """pg_build (K5 enqueued behind K3 with the previous build's rdBG size as
     its capacity) against the oracle: a first build (no capacity known: K5
     after the flag read), a repeat (speculative K5), then a larger, more
@@ -287,5 +287,16 @@ def test_pg_build_speculative_k5(oracle_mod):
         keys, masks = ctx.dbg()
         rk, rm = ref.dbg()
         assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
+    # the parse queues the next build's table clear on the side stream; a
+    # build that clears on its own stream (group form) waits for it
+    monkeypatch.setenv("PG_K3", "group")
+    ref = oracle_mod.OracleRun(large, 27, 2)
+    ctx.set_fasta(large)
+    ctx.parse()
+    ctx.build(None, 0, True)
+    keys, masks = ctx.dbg()
+    rk, rm = ref.dbg()
+    assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
+    assert np.array_equal(ctx.rdbg(), ref.rdbg())
     ctx.close()
     two.close()
