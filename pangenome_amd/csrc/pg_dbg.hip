@@ -1485,6 +1485,22 @@ __global__ void __launch_bounds__(256) k_zero16(uint4* __restrict__ p, uint64_t 
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * 256ull) p[i] = z;
 }
 
+// Small per-build fills (overflow slots, flags, K3 queue counters, drift
+// hints) in ONE launch, one grid row per region, instead of a
+// hipMemsetAsync each (~5 us of dispatch apiece on the critical stream).
+struct Fill { uint4* p; uint64_t n16; unsigned v; };
+struct Fills { Fill r[4]; };
+__global__ void __launch_bounds__(256) k_fills(Fills f) {
+  const Fill r = f.r[blockIdx.y];
+  const uint4 v = make_uint4(r.v, r.v, r.v, r.v);
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < r.n16; i += (uint64_t)gridDim.x * 256ull) r.p[i] = v;
+}
+static void launch_fills(const Fills& f, int n, uint64_t max_n16, hipStream_t s) {
+  if (!n) return;
+  hipLaunchKernelGGL(k_fills, dim3(grid_for(max_n16, 256, 1024), (unsigned)n), dim3(256), 0, s, f);
+  PG_HIP(hipGetLastError());
+}
+
 // The next build's table clear, queued on stream2 by pg_parse so that it runs
 // beside the parse instead of beside the first coverage pass (parse
 // invalidates the dBG anyway; a build whose table keeps its place and size
@@ -1520,8 +1536,13 @@ static void clear_table(Ctx& c, bool primary) {
                        reinterpret_cast<uint4*>(c.table.p), (uint64_t)c.cap);
     PG_HIP(hipGetLastError());
   }
-  PG_HIP(hipMemsetAsync(c.ovf.p, 0, sizeof(Slot) * c.ovf_cap, c.stream));
-  PG_HIP(hipMemsetAsync(c.flags.p, 0, 4 * N_FLAGS, c.stream));
+  static_assert(sizeof(Slot) == 16 && (4 * N_FLAGS) % 16 == 0, "k_fills works in 16-byte units");
+  c.k3_defer_fill = !primary;                            // the two-pass K3 folds them into its own fill
+  if (!primary) return;
+  Fills f{};
+  f.r[0] = Fill{reinterpret_cast<uint4*>(c.ovf.p), c.ovf_cap, 0u};
+  f.r[1] = Fill{reinterpret_cast<uint4*>(c.flags.p), (uint64_t)(4 * N_FLAGS / 16), 0u};
+  launch_fills(f, 2, std::max<uint64_t>(c.ovf_cap, 4 * N_FLAGS / 16), c.stream);
 }
 
 static uint64_t n_entries(const Ctx& c) { return 2 * c.cap + c.ovf_cap; }
@@ -1717,6 +1738,9 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       const char* we = getenv("PG_K3_WGRID");
       const size_t covpad = nch > 1 ? (size_t)(pe ? atoi(pe) : K3_COVPAD) : 0;
       const unsigned wgrid = we ? (unsigned)atoi(we) : (unsigned)c.n_cu * K3_WBLK;
+      // the last work pass has no coverage pass beside it: more blocks per CU
+      const char* le = getenv("PG_K3_WLAST");                    // dev knob (blocks per CU)
+      const unsigned wlast = le && atoi(le) > 0 ? (unsigned)c.n_cu * (unsigned)atoi(le) : wgrid;
       uint64_t gc[8], qoff[8], qcapc[8];               // per chunk: blocks (8 x the longest XCD part)
       uint64_t items = 0;
       for (int i = 0; i < nch; ++i) {
@@ -1735,8 +1759,21 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       c.k3_queue.reserve(qbytes + cbytes * nch);
       auto* q = c.k3_queue.as<WorkItem>();
       auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
-      PG_HIP(hipMemsetAsync(qn, 0, cbytes * nch, c.stream));
-      PG_HIP(hipMemsetAsync(c.k3_hint.p, 0xFF, 64 * (c.n_records + 1), c.stream));   // no drift known yet
+      {                                                          // counters 0, hints "no drift known yet"
+        static_assert(sizeof(WorkItem) % 16 == 0 && (8 * QSTRIDE * NQ) % 16 == 0, "16-byte fill units");
+        Fills f{};
+        int nf = 0;
+        f.r[nf++] = Fill{reinterpret_cast<uint4*>(qn), cbytes * nch / 16, 0u};
+        f.r[nf++] = Fill{c.k3_hint.as<uint4>(), 4 * (c.n_records + 1), 0xFFFFFFFFu};
+        if (c.k3_defer_fill) {
+          f.r[nf++] = Fill{reinterpret_cast<uint4*>(c.ovf.p), c.ovf_cap, 0u};
+          f.r[nf++] = Fill{reinterpret_cast<uint4*>(c.flags.p), (uint64_t)(4 * N_FLAGS / 16), 0u};
+        }
+        uint64_t mx = 0;
+        for (int j = 0; j < nf; ++j) mx = std::max(mx, f.r[j].n16);
+        launch_fills(f, nf, mx, c.stream);
+        c.k3_defer_fill = false;
+      }
       if (dbg & 64) PG_HIP(hipMemsetAsync(c.k3_hint.as<int>() + 16 * c.n_records + 2, 0, 16, c.stream));
       const long long r2s = c.k3_ref2 >= 0 ? c.h_rec_start[c.k3_ref2] : 0;
       const long long r2n = c.k3_ref2 >= 0 ? c.h_rec_len[c.k3_ref2] : 0;
@@ -1762,7 +1799,7 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
         PG_HIP(hipEventRecord(c.ev[1 + i], s0));
         PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: clear, work 0 .. i-1, then this
         const uint64_t mi = std::min<uint64_t>(NQ * qcapc[i], c.windows_fw / IW + c.n_records + 1);
-        const unsigned gw = nch > 1 ? wgrid : grid_for(mi, IBLOCK, 16384);
+        const unsigned gw = nch > 1 ? (i + 1 == nch ? wlast : wgrid) : grid_for(mi, IBLOCK, 16384);
         if (rc0)
           hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, s1, cls, qi, qni, (unsigned long long)qcapc[i],
                              c.k, shift, c.tv, flags, dbg);

@@ -120,6 +120,7 @@ struct Ctx {
   void* pre_ptr = nullptr;        // table clear queued on stream2 by pg_parse (beside the parse)
   uint64_t pre_n16 = 0;           //   its 16-byte buckets
   bool k3_skip_clear = false;     // launch_insert: the table is already cleared on stream2
+  bool k3_defer_fill = false;     // launch_insert: overflow slots and flags still to be zeroed
   uint64_t n_lines = 0, n_records = 0, n_bases = 0, n_nl = 0;
   std::vector<int64_t> h_rec_start, h_rec_len, h_rec_hdr_start, h_rec_hdr_len, h_rec_ptr;
   bool parsed = false;
