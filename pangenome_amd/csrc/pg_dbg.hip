@@ -1686,7 +1686,17 @@ constexpr int K3_WBLK = 2;                    // work blocks per CU (chunked for
 // the coverage pass + work pass form of k_insert (needs the lead record)
 static bool two_pass(const Ctx& c, uint64_t ntiles, int dbg) { return ntiles && c.k3_ref >= 0 && !(dbg & 256); }
 
-static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t shift, unsigned* flags, int dbg) {
+static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, unsigned* flags) {
+  if (!c.n_records) return;
+  hipLaunchKernelGGL(k_short, dim3(grid_for(c.n_records, IBLOCK, 1024)), dim3(IBLOCK), 0, s, c.cls.as<uint8_t>(),
+                     c.rec_start.as<long long>(), c.rec_len.as<long long>(), c.rec_flag.as<uint8_t>(), c.n_records,
+                     c.k, shift, rc0, c.tv, flags);
+  PG_HIP(hipGetLastError());
+}
+
+// Returns true when it has also queued k_short (records with n <= k+1).
+static bool launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t shift, unsigned* flags, int dbg) {
+  bool short_done = false;
   const dim3 g((unsigned)ntiles), b(IBLOCK);
   const uint8_t* cls = c.cls.as<uint8_t>();
   const auto* tiles = c.tiles.as<unsigned long long>();
@@ -1788,6 +1798,7 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
         PG_HIP(hipGetLastError());
       }
       c.k3_skip_clear = false;
+      PG_HIP(hipEventRecord(c.ev[13], s1));                     // the table is clear from here on
       for (int i = 0; i < nch; ++i) {
         auto* qi = q + qoff[i];
         auto* qni = qn + (cbytes / 8) * i;
@@ -1808,6 +1819,10 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
                              c.k, shift, c.tv, flags, dbg);
         PG_HIP(hipGetLastError());
       }
+      // k_short on s0 beside the last work pass rather than after the join
+      PG_HIP(hipStreamWaitEvent(s0, c.ev[13], 0));
+      launch_short(c, s0, rc0, shift, flags);
+      short_done = true;
       PG_HIP(hipEventRecord(c.ev[15], s1));                     // join: s0 continues after the last work pass
       PG_HIP(hipStreamWaitEvent(s0, c.ev[15], 0));
     } else if (rc0) {
@@ -1819,6 +1834,7 @@ static void launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
     }
   }
   PG_HIP(hipGetLastError());
+  return short_done;
 }
 
 static void reduce_enqueue(Ctx& c, uint64_t cap_keys);
@@ -1869,14 +1885,9 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     c.t0.stop(c.stream);
     unsigned* flags = c.flags.as<unsigned>();
     c.t1.start(c.stream);
-    if (ntiles) launch_insert(c, mode, rc0, ntiles, shift, flags, dbg);
+    const bool short_done = ntiles && launch_insert(c, mode, rc0, ntiles, shift, flags, dbg);
     c.t1.stop(c.stream);
-    if (R) {
-      hipLaunchKernelGGL(k_short, dim3(grid_for(R, IBLOCK, 1024)), dim3(IBLOCK), 0, c.stream,
-                         c.cls.as<uint8_t>(), c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                         c.rec_flag.as<uint8_t>(), R, c.k, shift, rc0, c.tv, flags);
-      PG_HIP(hipGetLastError());
-    }
+    if (!short_done) launch_short(c, c.stream, rc0, shift, flags);
     if (extra_empty) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, flags);
     merge_preload(c, flags);
     const bool spec = c.spec_k5 && c.rdbg_hint && !dbg;
