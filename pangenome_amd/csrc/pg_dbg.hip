@@ -1799,6 +1799,11 @@ static bool launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
       }
       c.k3_skip_clear = false;
       PG_HIP(hipEventRecord(c.ev[13], s1));                     // the table is clear from here on
+      // the last work pass on s0, right behind the last coverage pass and
+      // beside the previous work pass (chunks' inserts commute: atomics), so
+      // that the cross-stream join before K5 waits on s1's shorter tail
+      const char* l0 = getenv("PG_K3_LAST_S0");                  // dev knob
+      const bool last_s0 = nch > 1 && !(l0 && atoi(l0) == 0);
       for (int i = 0; i < nch; ++i) {
         auto* qi = q + qoff[i];
         auto* qni = qn + (cbytes / 8) * i;
@@ -1807,22 +1812,32 @@ static bool launch_insert(Ctx& c, int mode, int rc0, uint64_t ntiles, uint64_t s
                              (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
                              c.k3_hint.as<int>(), (int)c.n_records, ntiles, cb[i], cb[i + 1], cb[nch], dbg);
         PG_HIP(hipGetLastError());
-        PG_HIP(hipEventRecord(c.ev[1 + i], s0));
-        PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: clear, work 0 .. i-1, then this
+        hipStream_t ws = s1;
+        if (last_s0 && i + 1 == nch) {
+          ws = s0;
+          PG_HIP(hipStreamWaitEvent(s0, c.ev[13], 0));
+          launch_short(c, s1, rc0, shift, flags);                // k_short on s1 beside it
+          short_done = true;
+        } else {
+          PG_HIP(hipEventRecord(c.ev[1 + i], s0));
+          PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));      // s1: clear, work 0 .. i-1, then this
+        }
         const uint64_t mi = std::min<uint64_t>(NQ * qcapc[i], c.windows_fw / IW + c.n_records + 1);
         const unsigned gw = nch > 1 ? (i + 1 == nch ? wlast : wgrid) : grid_for(mi, IBLOCK, 16384);
         if (rc0)
-          hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, s1, cls, qi, qni, (unsigned long long)qcapc[i],
+          hipLaunchKernelGGL(k_insert_work<true>, dim3(gw), b, 0, ws, cls, qi, qni, (unsigned long long)qcapc[i],
                              c.k, shift, c.tv, flags, dbg);
         else
-          hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, s1, cls, qi, qni, (unsigned long long)qcapc[i],
+          hipLaunchKernelGGL(k_insert_work<false>, dim3(gw), b, 0, ws, cls, qi, qni, (unsigned long long)qcapc[i],
                              c.k, shift, c.tv, flags, dbg);
         PG_HIP(hipGetLastError());
       }
-      // k_short on s0 beside the last work pass rather than after the join
-      PG_HIP(hipStreamWaitEvent(s0, c.ev[13], 0));
-      launch_short(c, s0, rc0, shift, flags);
-      short_done = true;
+      // k_short beside the last work pass (on whichever stream it is not on), not after the join
+      if (!short_done) {
+        PG_HIP(hipStreamWaitEvent(s0, c.ev[13], 0));
+        launch_short(c, s0, rc0, shift, flags);
+        short_done = true;
+      }
       PG_HIP(hipEventRecord(c.ev[15], s1));                     // join: s0 continues after the last work pass
       PG_HIP(hipStreamWaitEvent(s0, c.ev[15], 0));
     } else if (rc0) {
