@@ -135,6 +135,11 @@ class Context:
         arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
         check(self.lib.pg_set_fasta(self.h, ptr(arr), arr.shape[0]), "pg_set_fasta")
 
+    def set_fasta_host_ptr(self, host_ptr: int, nbytes: int):
+        """Host bytes at a raw address (e.g. a pinned torch tensor's data_ptr():
+        the H2D copy is then plain DMA)."""
+        check(self.lib.pg_set_fasta(self.h, C.c_void_p(host_ptr), nbytes), "pg_set_fasta")
+
     def set_fasta_device(self, dev_ptr: int, nbytes: int, keepalive=None):
         self._keepalive = keepalive
         check(self.lib.pg_set_fasta_device(self.h, C.c_void_p(dev_ptr), nbytes), "pg_set_fasta_device")
