@@ -49,9 +49,9 @@ typedef struct pg_stats {
   uint64_t n_slots;        /* occupied canonical slots                             */
   uint64_t table_capacity; /* slots in the device hash table                       */
   double ms_parse;         /* K1 wall (host-timed, includes its small D2H syncs)  */
-  double ms_clear;         /* table memset                                        */
-  double ms_insert;        /* K3 k_insert                                         */
-  double ms_scan;          /* K5 k_reduce                                         */
+  double ms_clear;         /* (0: the table is written whole, never cleared)      */
+  double ms_insert;        /* K3 stage A: coverage + work passes (record emission)*/
+  double ms_scan;          /* K3 stages B + C: partition merge with the fused K5  */
   uint64_t sentinel;       /* 1 if the n<k key (2^64-1) is in the dBG              */
 } pg_stats;
 
@@ -84,13 +84,13 @@ int pg_records(const pg_ctx* ctx, int64_t* seq_len, int64_t* hdr_start, int64_t*
 int pg_build_dbg(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0, pg_stats* stats);
 
 /* K5: dbg2rdbg (kmer_numba.py:1313-1321 -> build_rdbg_jit_ :1292-1309).
- * Marks members in the device table and materialises the rdBG keys. */
+ * The degree scan runs inside pg_build_dbg (every key's masks are final when
+ * its table partition is merged; the rdBG keys are materialised there), so
+ * this only reports it. */
 int pg_build_rdbg(pg_ctx* ctx, uint64_t* n_rdbg, pg_stats* stats);
 
 /* seq2rdbg then dbg2rdbg (kmer_numba.py:1234-1268, :1313-1321) in one call:
- * pg_build_dbg + pg_build_rdbg with the same results, K5 enqueued right
- * behind K3 (no host round trip between them; its key capacity comes from the
- * previous build and is re-run if outgrown). */
+ * pg_build_dbg + pg_build_rdbg. */
 int pg_build(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0, uint64_t* n_rdbg, pg_stats* stats);
 
 /* dump()'s keys/values (kmer_numba.py:243-261) of the dBG, unordered.
@@ -126,7 +126,8 @@ uint64_t pg_oakht_capacity(uint64_t size);
  * counts[nparts] receives run lengths; d_out == NULL only counts. */
 int pg_dbg_partition(pg_ctx* ctx, int nparts, void* d_out, uint64_t out_cap, uint64_t* counts);
 /* OR-merge received 16-byte records (device pointer) into a fresh owner
- * table; sentinel != 0 adds the n<k key.  Follow with pg_build_rdbg. */
+ * table (the rdBG of the owner's keys is built with it); sentinel != 0 adds
+ * the n<k key.  capacity_hint is ignored (the table is sized exactly). */
 int pg_dbg_merge(pg_ctx* ctx, const void* d_records, uint64_t n, uint64_t capacity_hint, int sentinel);
 
 /* ---- edge pass: rdbg_edge_weight_jit_ (kmer_numba.py:1808-1827) ->
@@ -157,6 +158,20 @@ int pg_rows_export(pg_ctx* ctx, int64_t* rows5, uint64_t cap);
 uint64_t pg_format_xyz(const uint64_t* tuples, const int64_t* counts, uint64_t n, char* out, uint64_t cap);
 uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, const int64_t* name_off, char* out,
                         uint64_t cap);
+
+/* Tuning (tests and experiments; the defaults are the product setting).
+ * PG_TUNE_K3_CHUNKS: chunks of the K3 tile list whose work pass overlaps the
+ * next chunk's coverage pass, 1..6, or 0 = by tile count (4 when the tile
+ * list has >= 16384 tiles, else 1). */
+#define PG_TUNE_K3_CHUNKS 1
+/* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
+ * count asks (0..8): exercises the overflow set, its spill and the re-run
+ * with more buckets (results are unchanged). */
+#define PG_TUNE_BUCKET_SHIFT 2
+/* PG_TUNE_REGION_CAP: first stage A region size in records (0 = estimated):
+ * a small value exercises the stage A re-run (results are unchanged). */
+#define PG_TUNE_REGION_CAP 3
+int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Timings and counters of the last build (see pg_stats). */
 int pg_get_stats(const pg_ctx* ctx, pg_stats* stats);

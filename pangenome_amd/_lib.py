@@ -15,6 +15,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, os.environ.get("PG_LIB_NAME", "libpangenome_hip.so"))   # diag builds only
 
 PG_OK = 0
+PG_TUNE_K3_CHUNKS = 1
+PG_TUNE_BUCKET_SHIFT = 2
+PG_TUNE_REGION_CAP = 3
 
 
 class PgStats(C.Structure):
@@ -56,6 +59,7 @@ SIGNATURES = {
     "pg_rows": (C.c_int, [_P, _P, C.c_int, _U64P]),
     "pg_rows_export": (C.c_int, [_P, _P, C.c_uint64]),
     "pg_get_stats": (C.c_int, [_P, _SP]),
+    "pg_tune": (C.c_int, [_P, C.c_int, C.c_int64]),
     "pg_dbg_dump": (C.c_int, [_P, _U64P, _P, _P, _P, _U64P]),
     "pg_dbg_load": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_oakht_capacity": (C.c_uint64, [C.c_uint64]),
@@ -178,6 +182,9 @@ class Context:
         check(self.lib.pg_build(self.h, ptr(f), int(extra_empty), int(bool(rc0)), C.byref(n), C.byref(st)),
               "pg_build")
         return st
+
+    def tune(self, what: int, value: int):
+        check(self.lib.pg_tune(self.h, int(what), int(value)), "pg_tune")
 
     def stats(self) -> PgStats:
         st = PgStats()

@@ -73,15 +73,17 @@ void pg_destroy(pg_ctx* x) {
   pg::Ctx& c = x->c;
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
-  pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.n_sel, &c.rec_start,
-                        &c.rec_len, &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.ovf,
-                        &c.flags,
-                        &c.rdbg_keys, &c.tiles, &c.groups, &c.tile_desc, &c.k3_queue, &c.k3_hint, &c.part_cnt, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
-                        &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload, &c.dump_cnt};
+  pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.n_sel, &c.rec_start, &c.rec_len,
+                        &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.ovf, &c.flags,
+                        &c.recA_key, &c.recA_mw, &c.ctrA, &c.recS_key[0], &c.recS_key[1], &c.recS_mw[0],
+                        &c.recS_mw[1], &c.ctrS, &c.rseg, &c.k5_ctr, &c.tile_sched, &c.tile_desc, &c.k3_queue,
+                        &c.k3_hint, &c.part_cnt, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
+                        &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload,
+                        &c.dump_cnt};
   for (auto* b : bufs) b->release();
   c.rec_pack.release();
   c.h_pin.release();
-  c.k5_pin.release();
+  c.tile_pin.release();
   c.t0.destroy();
   c.t1.destroy();
   c.t5.destroy();
@@ -176,17 +178,32 @@ int pg_build(pg_ctx* x, const uint8_t* rec_flags, int extra_empty, int rc0, uint
   return guard([&] {
     if (!x) throw pg::Error(PG_EINVAL, "pg_build: ctx is NULL");
     PG_HIP(hipSetDevice(x->c.device));
-    x->c.spec_k5 = true;
-    try {
-      pg::build_dbg(x->c, rec_flags, extra_empty, rc0 != 0);
-    } catch (...) {
-      x->c.spec_k5 = false;
-      throw;
-    }
-    x->c.spec_k5 = false;
-    pg::build_rdbg(x->c);                      // (a no-op when K5 already ran behind K3)
+    pg::build_dbg(x->c, rec_flags, extra_empty, rc0 != 0);
+    pg::build_rdbg(x->c);                      // (the degree scan ran inside the build)
     if (n_rdbg) *n_rdbg = x->c.n_rdbg;
     fill_stats(x->c, stats);
+  });
+}
+
+int pg_tune(pg_ctx* x, int what, int64_t value) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_tune: ctx is NULL");
+    switch (what) {
+      case PG_TUNE_K3_CHUNKS:
+        if (value < 0 || value > 6) throw pg::Error(PG_EINVAL, "pg_tune: K3 chunks must be in [0, 6]");
+        x->c.k3_chunks = (int)value;
+        break;
+      case PG_TUNE_BUCKET_SHIFT:
+        if (value < 0 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: bucket shift must be in [0, 8]");
+        x->c.bb_shift = (int)value;
+        break;
+      case PG_TUNE_REGION_CAP:
+        if (value < 0) throw pg::Error(PG_EINVAL, "pg_tune: region size must be >= 0");
+        x->c.region_cap_force = (uint64_t)value;
+        break;
+      default:
+        throw pg::Error(PG_EINVAL, "pg_tune: unknown parameter " + std::to_string(what));
+    }
   });
 }
 

@@ -97,6 +97,9 @@ struct Ctx {
   hipStream_t stream2 = nullptr;  // side stream: K3 work passes overlap the next coverage pass
   hipEvent_t ev[16] = {};         // ordering events between the two streams
   int n_cu = 256;                 // compute units (persistent-kernel grids)
+  int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
+  int bb_shift = 0;               // pg_tune: table bits below the sized ones (tests of the overflow paths)
+  uint64_t region_cap_force = 0;  // pg_tune: first stage A region size (tests of the re-run path)
 
   // ---- input FASTA (device-resident; either owned or borrowed)
   DevBuf fasta_own;
@@ -113,38 +116,41 @@ struct Ctx {
   DevBuf scratch;                 // rocPRIM temp storage
   DevBuf rec_pack;                // int64 [5][R]: the record table gathered for one copy
   PinBuf h_pin;                   // pinned staging for small device-to-host reads
-  PinBuf k5_pin;                  // K5's counters (read back together with build_dbg's flags)
-  uint64_t k5_cap = 0;            // rdBG key capacity of the K5 run in flight
-  uint64_t rdbg_hint = 0;         // rdBG keys of the last build (+25 %): speculative K5 capacity
-  bool spec_k5 = false;           // pg_build: K5 is enqueued behind K3, before build_dbg's sync
-  void* pre_ptr = nullptr;        // table clear queued on stream2 by pg_parse (beside the parse)
-  uint64_t pre_n16 = 0;           //   its 16-byte buckets
-  bool k3_skip_clear = false;     // launch_insert: the table is already cleared on stream2
-  bool k3_defer_fill = false;     // launch_insert: overflow slots and flags still to be zeroed
   uint64_t n_lines = 0, n_records = 0, n_bases = 0, n_nl = 0;
   std::vector<int64_t> h_rec_start, h_rec_len, h_rec_hdr_start, h_rec_hdr_len, h_rec_ptr;
   bool parsed = false;
 
-  // ---- dBG table (K3) and rdBG (K5)
+  // ---- dBG table (K3 stage C) and rdBG (fused K5)
   DevBuf table;                   // primary buckets (2 x 64-bit words each)
   DevBuf ovf;                     // overflow slots (16 B)
-  TableView tv{};                 // current geometry (pg_common.h)
+  TableView tv{};                 // hash (fixed by k) and current geometry (pg_common.h)
+  int kb = 0, cbits = 0, hash_k = 0, bb = 0;   // key bits, coarse bin bits, k of tv's hash, bucket bits
   uint64_t cap = 0;               // primary buckets (power of two)
   uint64_t ovf_cap = 0;           // overflow slots (power of two)
-  uint64_t cap_hint = 0;          // canonical keys seen by the previous build
-  DevBuf flags;                   // [0] sentinel seen, [1] overflow, [2..] counters
-  DevBuf rdbg_keys;
+  DevBuf flags;                   // [0] sentinel seen, [1] stage A bits, [4] stage B/C bits
   uint64_t n_dbg = 0, n_rdbg = 0, n_canon = 0, sentinel = 0;
   bool built = false, reduced = false;
   int rc0 = 1;
   uint64_t windows_fw = 0, windows_total = 0;
 
-  // ---- walk passes (edges / labels)
-  DevBuf tiles;                   // K3 tile list (record << 32 | stripe), stripe-major
+  // ---- partitioned build (pg_dbg.hip)
+  DevBuf recA_key, recA_mw, ctrA;     // stage A: records per (coarse bin, XCD) region and cursors
+  uint64_t capA = 0;                  // records per stage A region
+  DevBuf recS_key[2], recS_mw[2];     // stage B outputs (ping-pong)
+  DevBuf ctrS;                        // stage B cursors, all levels
+  DevBuf rseg;                        // rdBG keys: NSEG segments of rseg_cap
+  DevBuf k5_ctr;                      // key / dBG counts and rdBG segment cursors
+  uint64_t rseg_cap = 0;
+  uint64_t rseg_cnt[64] = {};
+  uint64_t n_records_a = 0;           // stage A records of the last build
+  double u_ratio = 0, r_ratio = 0;    // last build: records per forward window, rdBG keys per record
+
+  // ---- K3 tiles
+  DevBuf tile_sched;              // per-stripe tile offsets + record order (k_tiles input)
+  PinBuf tile_pin;
   uint64_t n_tiles = 0;
   int tile_k = 0;
-  int tile_mode = 0;              // 0: per-record tiles (k_insert), 1: record groups (k_insert_grp)
-  int k3_ref = -1;                // k_insert's dedup reference record (the lead), -1: none
+  int k3_ref = -1;                // k_cover's dedup reference record (the lead), -1: none
   int k3_ref2 = -1;               // k_cover's second reference record, -1: none
   DevBuf part_cnt;                // multi-GPU partition: owner counts and cursors
   uint64_t part_counts[64] = {};  // counts of the last count pass
@@ -153,11 +159,12 @@ struct Ctx {
   uint64_t part_gen = ~0ull;      // build_gen of the table the counts are for
   uint64_t build_gen = 0;         // bumped by every table build / merge
   DevBuf k3_hint;                 // int32 [8 XCDs][2 references][R]: last drift k_cover found
-  DevBuf tile_desc;               // k_insert tile descriptors (record start / length / index / stripe)
-  DevBuf k3_queue;                // segments left with work after k_insert's coverage pass, + counter
-  DevBuf groups;                  // int32 [n_groups * GG] record ids, -1 padded
+  DevBuf tile_desc;               // tile descriptors (record start / length / index / stripe)
+  DevBuf k3_queue;                // segments left with work after the coverage pass, + counters
   std::vector<int64_t> tile_sig_len;   // record lengths / flags the tile list was built for
   std::vector<uint8_t> tile_sig_flag;
+
+  // ---- walk passes (edges / labels)
   DevBuf tile_cnt, tile_off;      // per tile x strand counts / offsets
   DevBuf occ;                     // member / hit occurrences, walk ordered
   DevBuf edge_tab, pair_tab;      // edge table and (edge, walk) dedup set
@@ -188,7 +195,6 @@ struct Ctx {
 
 // pg_parse.hip
 void parse_fasta(Ctx& c);
-void preclear_table(Ctx& c);   // pg_dbg.hip: the next build's table clear, on stream2
 // pg_dbg.hip
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0);
 void build_rdbg(Ctx& c);
@@ -196,7 +202,6 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap);
 uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap);
 uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts);
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel);
-void merge_preload(Ctx& c, unsigned* flags);
 // pg_persist.hip
 struct PreEnt {                   // one staged oakht slot: oriented key, 12-bit mask, count
   unsigned long long key;
@@ -223,23 +228,19 @@ inline int log2u(uint64_t p) {
   return b;
 }
 
-// Table geometry for k-mers of length k holding about `keys` canonical keys:
-// load <= 0.25 keys per 2-word bucket (C3: 0.5 -> 0.25 took K3 6.31 -> 5.76 ms
-// for +0.2 ms of K5 sweep; 0.125 was slower), quotient <= 38 bits (so that
-// quotient + 26 mask bits fit 64), overflow table ~1/16 of the keys.
-inline TableView make_geometry(int k, uint64_t keys, uint64_t& buckets, uint64_t& ovf_slots) {
+// Bits of a k-mer key: keys < 5^k <= 2^kb.
+inline int key_bits(int k) {
   uint64_t maxkey = 1;
   for (int i = 0; i < k; ++i) maxkey *= 5;
-  const int kb = std::max(1, log2u(maxkey));                 // keys < 5^k <= 2^kb
-  // keys per bucket target (PG_BUCKET_LOAD, development knob)
-  static const double load = getenv("PG_BUCKET_LOAD") ? atof(getenv("PG_BUCKET_LOAD")) : 0.5;
-  const uint64_t want = (uint64_t)((double)keys / (load > 0.05 ? load : 0.5));
-  const int bb = std::max({kb - 38, log2u(std::max<uint64_t>(want, 1)), 11});   // >= 2048 buckets
-  buckets = 1ull << bb;
-  ovf_slots = next_pow2(std::max<uint64_t>(4096, keys / 16));
+  return std::max(1, log2u(maxkey));
+}
+
+// The hash of a table for k-mers of length k (a bijection of kb-bit keys,
+// fixed by k: records carry h = perm(c) before the table is sized) and the
+// reverse-complement constants; the bucket geometry comes from set_geometry.
+inline TableView make_hash(int k, int& kb) {
+  kb = key_bits(k);
   TableView t{};
-  t.bmask = buckets - 1;
-  t.qbits = kb > bb ? (uint32_t)(kb - bb) : 0u;
   t.kmask = kb >= 64 ? ~0ull : ((1ull << kb) - 1ull);
   t.sh1 = std::max(1, kb / 2);
   t.sh2 = std::max(1, kb / 3);
@@ -252,9 +253,15 @@ inline TableView make_geometry(int k, uint64_t keys, uint64_t& buckets, uint64_t
   t.m2 = (0xC2B2AE3D27D4EB4Full & t.kmask) | 1ull;
   t.m1i = inv(t.m1) & t.kmask;
   t.m2i = inv(t.m2) & t.kmask;
-  t.omask = ovf_slots - 1;
   rc_constants(k, t.rc_pad, t.rc_inv);
   return t;
+}
+// 2^bb buckets (kb - 38 <= bb <= kb: the quotient kb - bb plus the 26 mask
+// bits fit one 64-bit word) and `ovf_slots` (a power of two) overflow slots.
+inline void set_geometry(TableView& t, int kb, int bb, uint64_t ovf_slots) {
+  t.bmask = (1ull << bb) - 1ull;
+  t.qbits = (uint32_t)(kb - bb);
+  t.omask = ovf_slots - 1;
 }
 inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65536u) {
   uint64_t g = (n + block - 1) / block;

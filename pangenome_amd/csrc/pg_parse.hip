@@ -26,6 +26,8 @@
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
+#include <mutex>
+
 #include "pg_internal.h"
 
 namespace pg {
@@ -327,9 +329,14 @@ __global__ void k_records(uint64_t R, unsigned long long total, long long last_l
   }
 }
 
-static void upload_byte_class() {
-  static bool done = false;
-  if (done) return;
+// The byte-class table lives in each device's constant memory: upload it once
+// per device (hipMemcpyToSymbol writes the current device only).
+static void upload_byte_class(int device) {
+  static std::mutex mu;
+  static uint64_t done = 0;                                 // one bit per device id < 64
+  std::lock_guard<std::mutex> lock(mu);
+  const uint64_t bit = device < 64 ? 1ull << device : 0ull;
+  if (bit && (done & bit)) return;
   uint8_t t[256];
   for (int i = 0; i < 256; ++i) t[i] = CLS_OTHER;
   const char* s = "ACGTN";
@@ -337,7 +344,7 @@ static void upload_byte_class() {
   for (int i = 0; i < 5; ++i) { t[(uint8_t)s[i]] = c[i]; t[(uint8_t)(s[i] | 0x20)] = c[i]; }
   t[(uint8_t)'$'] = CLS_DOLLAR;
   PG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_byte_class), t, 256));
-  done = true;
+  done |= bit;
 }
 
 // the five per-record arrays side by side, for one device-to-host copy
@@ -354,8 +361,7 @@ __global__ void k_pack_records(uint64_t R, const long long* __restrict__ rs, con
 }
 
 void parse_fasta(Ctx& c) {
-  upload_byte_class();
-  preclear_table(c);                                        // beside the parse, on stream2
+  upload_byte_class(c.device);
   hipStream_t st = c.stream;
   const uint64_t n = c.n_bytes;
   c.parsed = false;

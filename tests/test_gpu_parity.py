@@ -102,20 +102,21 @@ def test_pangenome_vs_oracle(km, oracle_mod, tmp_path, c):
     assert got["rows"] == ref["rows"]
 
 
-@pytest.mark.parametrize("form", ["tile", "group"])
+@pytest.mark.parametrize("chunks", [1, 4])
 @pytest.mark.parametrize("rc0", [True, False])
-def test_k3_forms_vs_oracle(oracle_mod, monkeypatch, form, rc0):
-    """Both K3 kernels (per-record tiles, record groups with the LDS merge) on
-    a pangenome with ragged record lengths, including records shorter than a
-    stripe and records of n <= k+1."""
+def test_k3_ragged_vs_oracle(oracle_mod, chunks, rc0):
+    """The partitioned K3 (coverage + work passes, stage A bins, split, range
+    merge with the fused degree scan) on a pangenome with ragged record
+    lengths, including records shorter than a stripe and records of n <= k+1,
+    with the tile list in one chunk and in four."""
     from pangenome_amd import synth
-    from pangenome_amd._lib import Context
-    monkeypatch.setenv("PG_K3", form)
+    from pangenome_amd._lib import Context, PG_TUNE_K3_CHUNKS
     fasta = synth.pangenome(11, 70_000, snp=0.004, indel=6e-4, seed=31)
     fasta += b">s1\nACGTACGTACGTACGTACGTACGTACGT\n>s2\nACGT\n>s3\n" + b"A" * 700 + b"\n"
     c = 2 if rc0 else 0
     ref = oracle_mod.OracleRun(fasta, 27, c)
     ctx = Context(27)
+    ctx.tune(PG_TUNE_K3_CHUNKS, chunks)
     ctx.set_fasta(fasta)
     ctx.parse()
     ctx.build_dbg(None, 0, rc0)
@@ -128,15 +129,38 @@ def test_k3_forms_vs_oracle(oracle_mod, monkeypatch, form, rc0):
     ctx.close()
 
 
+@pytest.mark.parametrize("k", [15, 27])
+def test_overflow_and_rerun_paths_vs_oracle(oracle_mod, k):
+    """Forced slow paths give the same dBG: a table 8x smaller than sized
+    (LDS overflow sets fill, spill to the HBM overflow table, re-run with
+    more buckets) and tiny stage A regions (records dropped, re-run with the
+    exact region counts)."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context, PG_TUNE_BUCKET_SHIFT, PG_TUNE_REGION_CAP
+    fasta = synth.pangenome(6, 90_000, snp=0.01, indel=1e-3, seed=17)
+    ref = oracle_mod.OracleRun(fasta, k, 2)
+    rk, rm = ref.dbg()
+    for what, val in ((PG_TUNE_BUCKET_SHIFT, 3), (PG_TUNE_BUCKET_SHIFT, 8), (PG_TUNE_REGION_CAP, 64)):
+        ctx = Context(k)
+        ctx.tune(what, val)
+        ctx.set_fasta(fasta)
+        ctx.parse()
+        st = ctx.build(None, 0, True)
+        keys, masks = ctx.dbg()
+        assert np.array_equal(keys, rk) and np.array_equal(masks, rm), (what, val)
+        assert np.array_equal(ctx.rdbg(), ref.rdbg()), (what, val)
+        assert st.n_rdbg == len(ref.rdbg())
+        ctx.close()
+
+
 @pytest.mark.parametrize("c", [0, 2])
-def test_k3_reference_dedup_vs_oracle(oracle_mod, monkeypatch, c):
+def test_k3_reference_dedup_vs_oracle(oracle_mod, c):
     """k_insert skips a follower window whose k+2 context bytes equal the lead
     record's at some drift: copies of the lead with insertions (drift inside
     and beyond the +-512 search), deletions, SNPs, an N run, lowercase bytes,
     shorter copies (reference windows near its ends) and a reverse complement."""
     from pangenome_amd import synth
     from pangenome_amd._lib import Context
-    monkeypatch.delenv("PG_K3", raising=False)
     rng = np.random.default_rng(7 + c)
     acgt = np.frombuffer(b"ACGT", np.uint8)
     lead = acgt[rng.integers(0, 4, 30_000)]
@@ -228,18 +252,15 @@ def test_full_size_properties(km):
     assert ctx.records()["seq_len"].tolist() == lens
 
 
-@pytest.mark.parametrize("chunks", [1, 3])
+@pytest.mark.parametrize("chunks", [1, 3, 4])
 @pytest.mark.parametrize("c", [0, 2])
-def test_k3_chunked_two_references_vs_oracle(oracle_mod, monkeypatch, chunks, c):
+def test_k3_chunked_two_references_vs_oracle(oracle_mod, chunks, c):
     """The two-pass K3 on two streams (coverage of chunk i+1 beside the work
     pass of chunk i), with the lead and a second reference record: genomes
     sharing the lead's variant sites (so ref2 covers them), an N run, a
     lowercase stretch and records shorter than a stripe."""
     from pangenome_amd import synth
-    from pangenome_amd._lib import Context
-    monkeypatch.delenv("PG_K3", raising=False)
-    monkeypatch.setenv("PG_K3_CHUNKS", str(chunks))
-    monkeypatch.setenv("PG_K3_CHUNK_MIN", "1")
+    from pangenome_amd._lib import Context, PG_TUNE_K3_CHUNKS
     fasta = synth.pangenome(12, 150_000, snp=2e-3, indel=3e-4, seed=77 + chunks)
     recs = [b">" + r for r in fasta.split(b">")[1:]]
     body = bytearray(recs[3])
@@ -249,6 +270,7 @@ def test_k3_chunked_two_references_vs_oracle(oracle_mod, monkeypatch, chunks, c)
     fasta = b"".join(recs) + b">short\n" + b"ACGT" * 300 + b"\n"
     ref = oracle_mod.OracleRun(fasta, 27, c)
     ctx = Context(27)
+    ctx.tune(PG_TUNE_K3_CHUNKS, chunks)
     ctx.set_fasta(fasta)
     ctx.parse()
     ctx.build_dbg(None, 0, c == 2)
@@ -261,18 +283,18 @@ def test_k3_chunked_two_references_vs_oracle(oracle_mod, monkeypatch, chunks, c)
     ctx.close()
 
 
-@pytest.mark.gpu
-def test_pg_build_speculative_k5(oracle_mod, monkeypatch):
-    """pg_build (K5 enqueued behind K3 with the previous build's rdBG size as
-    its capacity) against the oracle: a first build (no capacity known: K5
-    after the flag read), a repeat (speculative K5), then a larger, more
-    varied input whose rdBG outgrows the learned capacity (K5 re-run)."""
+def test_pg_build_sequence_vs_oracle(oracle_mod):
+    """One context over inputs of different shape: a first build (no learned
+    stage A size), a repeat, then a larger, more varied input whose records
+    per window outgrow the learned size (stage A re-run), a single record,
+    and back — pg_build and the two-call path against the oracle."""
     from pangenome_amd import synth
     from pangenome_amd._lib import Context
     small = synth.pangenome(4, 40_000, snp=1e-4, indel=0.0, seed=5)
-    large = synth.pangenome(10, 120_000, snp=3e-3, indel=5e-4, seed=6)
+    large = synth.pangenome(10, 120_000, snp=3e-2, indel=5e-3, seed=6)
+    single = synth.ecoli_like(300_000)
     ctx, two = Context(27), Context(27)
-    for fasta in (small, small, large, large):
+    for fasta in (small, small, large, large, single, small):
         ref = oracle_mod.OracleRun(fasta, 27, 2)
         ctx.set_fasta(fasta)
         ctx.parse()
@@ -287,16 +309,5 @@ def test_pg_build_speculative_k5(oracle_mod, monkeypatch):
         keys, masks = ctx.dbg()
         rk, rm = ref.dbg()
         assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
-    # the parse queues the next build's table clear on the side stream; a
-    # build that clears on its own stream (group form) waits for it
-    monkeypatch.setenv("PG_K3", "group")
-    ref = oracle_mod.OracleRun(large, 27, 2)
-    ctx.set_fasta(large)
-    ctx.parse()
-    ctx.build(None, 0, True)
-    keys, masks = ctx.dbg()
-    rk, rm = ref.dbg()
-    assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
-    assert np.array_equal(ctx.rdbg(), ref.rdbg())
     ctx.close()
     two.close()
