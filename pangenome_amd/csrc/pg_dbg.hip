@@ -812,41 +812,40 @@ __device__ __forceinline__ uint64_t part_at(const Recs& I, uint32_t p, const uns
   return ((uint64_t)p * I.nsub + s) * I.cap + (r - s_off[s]);
 }
 
-// Split pass: partition p's records by the next S bits of the bucket index
-// ((h >> shift) & (nb - 1)) into output partitions p * nb + b.  A block takes
-// SCH records, ranks them per bin in LDS, reserves each bin's run with one
-// global atomic, sorts them by bin in LDS and writes the runs coalesced.
-constexpr int SB = 256, SR = 16, SCH = SB * SR;
+// Split pass: the records of input region g (partition p = g / nsub) by the
+// next S bits of the bucket index ((h >> shift) & (nb - 1)) into output
+// partitions p * nb + b.  A block takes SCH consecutive records of one region
+// (bpr blocks per region), ranks them per bin in LDS, reserves each bin's run
+// with one global atomic, sorts them by bin in LDS and writes the runs
+// coalesced.  3 blocks (24 waves) per CU.
+constexpr int SB = 512, SR = 8, SCH = SB * SR;
 constexpr int SMAXB = 128;                    // <= 7 bits per pass
-__global__ void __launch_bounds__(SB)
-k_split(Recs I, Recs O, uint32_t shift, uint32_t nb, uint32_t bpp, unsigned* __restrict__ flags) {
-  __shared__ unsigned long long s_off[9];
+__global__ void __launch_bounds__(SB, 6)
+k_split(Recs I, Recs O, uint32_t shift, uint32_t nb, uint32_t bpr, unsigned* __restrict__ flags) {
   __shared__ uint32_t s_cnt[SMAXB], s_pos[SMAXB];
   __shared__ unsigned long long s_base[SMAXB];
   __shared__ unsigned long long s_key[SCH];
   __shared__ uint32_t s_mw[SCH];
-  __shared__ uint8_t s_bin[SCH];
-  const uint32_t p = blockIdx.x / bpp, j = blockIdx.x % bpp;
-  part_offsets(I, p, s_off);
-  if (threadIdx.x < SMAXB) s_cnt[threadIdx.x] = 0u;
-  __syncthreads();
-  const uint64_t n = s_off[I.nsub], b0 = (uint64_t)j * SCH;
+  const uint32_t g = blockIdx.x / bpr, j = blockIdx.x % bpr, p = g / I.nsub;
+  const unsigned long long nr = I.cursor[CSTRIDE * (uint64_t)g];
+  const uint64_t n = nr < I.cap ? nr : I.cap, b0 = (uint64_t)j * SCH;
   if (b0 >= n) return;                                         // block-uniform
+  if (threadIdx.x < SMAXB) s_cnt[threadIdx.x] = 0u;
   const uint32_t cnt = (uint32_t)(n - b0 < (uint64_t)SCH ? n - b0 : (uint64_t)SCH);
+  const uint64_t in0 = (uint64_t)g * I.cap + b0;
   unsigned long long key[SR];
   uint32_t mw[SR], rk[SR];
 #pragma unroll
   for (int e = 0; e < SR; ++e) {
     const uint32_t i = (uint32_t)e * SB + threadIdx.x;
-    key[e] = 0;
-    mw[e] = 0;
-    rk[e] = 0;
-    if (i < cnt) {
-      const uint64_t at = part_at(I, p, s_off, b0 + i);
-      key[e] = I.key[at];
-      mw[e] = I.mw[at];
-      rk[e] = atomicAdd(&s_cnt[(uint32_t)(key[e] >> shift) & (nb - 1)], 1u);
-    }
+    key[e] = i < cnt ? I.key[in0 + i] : 0ull;
+    mw[e] = i < cnt ? I.mw[in0 + i] : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < SR; ++e) {
+    const uint32_t i = (uint32_t)e * SB + threadIdx.x;
+    rk[e] = i < cnt ? atomicAdd(&s_cnt[(uint32_t)(key[e] >> shift) & (nb - 1)], 1u) : 0u;
   }
   __syncthreads();
   if (threadIdx.x < 64) {                     // exclusive scan of the bin counts, two bins per lane
@@ -876,16 +875,16 @@ k_split(Recs I, Recs O, uint32_t shift, uint32_t nb, uint32_t bpp, unsigned* __r
       const uint32_t d = s_pos[b] + rk[e];
       s_key[d] = key[e];
       s_mw[d] = mw[e];
-      s_bin[d] = (uint8_t)b;
     }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < cnt; i += SB) {
-    const uint32_t b = s_bin[i];
+    const unsigned long long kk = s_key[i];
+    const uint32_t b = (uint32_t)(kk >> shift) & (nb - 1);
     const unsigned long long pos = s_base[b] + (i - s_pos[b]);
     if (pos < O.cap) {
       const uint64_t at = ((uint64_t)p * nb + b) * O.cap + pos;
-      O.key[at] = s_key[i];
+      O.key[at] = kk;
       O.mw[at] = s_mw[i];
     } else {
       atomicOr(flags + 4, F_SPLIT_OVER);
@@ -904,9 +903,10 @@ k_split(Recs I, Recs O, uint32_t shift, uint32_t nb, uint32_t bpp, unsigned* __r
 // its rdBG membership (build_rdbg_jit_ :1300-1305): members go to one of
 // NSEG output segments (one reservation per block), the dBG size and the
 // canonical key count to spread counters.
-constexpr int RB_T = 256;
+constexpr int RB_T = 1024;                    // 2 blocks (32 waves) per CU: 70 KiB of LDS each
+constexpr int RB_R = 4;                       // records in flight per thread
 constexpr int RANGE_BITS = 12;                // <= 4096 buckets (64 KiB of LDS) per partition
-constexpr int OVL = 1024;                     // LDS overflow slots per partition
+constexpr int OVL = 512;                      // LDS overflow slots per partition
 constexpr int NSEG = 64;
 struct RdbgOut {
   unsigned long long* keys;                   // segment s at [s * cap, (s+1) * cap)
@@ -919,7 +919,39 @@ __device__ __forceinline__ uint32_t member_bits(uint32_t m) {   // bit0: A membe
   return (uint32_t)(pa && rdbg_member(m & MASK12)) | ((uint32_t)(pb && rdbg_member((m >> B_SHIFT) & MASK12)) << 1);
 }
 
-__global__ void __launch_bounds__(RB_T)
+// OR one record (h, m) into the LDS range W (bucket lb) or the LDS overflow set
+__device__ __forceinline__ void range_or(unsigned long long* W, unsigned long long* OK, uint32_t* OM,
+                                         const TableView& T, uint64_t h, uint32_t m, uint32_t lb, uint64_t qmask,
+                                         unsigned* flags) {
+  const unsigned long long q = h & qmask, mine = (q << MW_BITS) | m;
+  unsigned long long* w = W + 2 * lb;
+  unsigned long long old = atomicCAS(w, 0ull, mine);
+  if (old == 0ull) return;
+  if ((old >> MW_BITS) == q) {
+    if ((old & m) != m) atomicOr(w, (unsigned long long)m);
+    return;
+  }
+  old = atomicCAS(w + 1, 0ull, mine);
+  if (old == 0ull) return;
+  if ((old >> MW_BITS) == q) {
+    if ((old & m) != m) atomicOr(w + 1, (unsigned long long)m);
+    return;
+  }
+  uint32_t s = (uint32_t)(fmix64(h) >> 40) & (OVL - 1);
+  for (int pr = 0; pr < OVL; ++pr) {
+    const unsigned long long o2 = atomicCAS(&OK[s], 0ull, h + 1ull);
+    if (o2 == 0ull || o2 == h + 1ull) {
+      atomicOr(&OM[s], m);
+      return;
+    }
+    s = (s + 1) & (OVL - 1);
+  }
+  // LDS overflow set full: straight to HBM, membership incomplete (the host re-runs with more buckets)
+  ovf_or(T, T.unperm(h), m, flags + 4);
+  atomicOr(flags + 4, F_LDS_SPILL);
+}
+
+__global__ void __launch_bounds__(RB_T, 8)
 k_build_range(Recs I, TableView T, uint32_t rbits, RdbgOut R, unsigned long long* __restrict__ ctr,
               unsigned* __restrict__ flags) {
   __shared__ unsigned long long W[2 << RANGE_BITS];
@@ -936,40 +968,24 @@ k_build_range(Recs I, TableView T, uint32_t rbits, RdbgOut R, unsigned long long
   __syncthreads();
   const uint64_t n = s_off[I.nsub];
   const uint64_t qmask = (1ull << T.qbits) - 1ull;
-  for (uint64_t r = threadIdx.x; r < n; r += RB_T) {
-    const uint64_t at = part_at(I, f, s_off, r);
-    const unsigned long long h = I.key[at];
-    const uint32_t m = I.mw[at];
-    const uint32_t lb = (uint32_t)(h >> T.qbits) & (rng - 1);
-    const unsigned long long q = h & qmask, mine = (q << MW_BITS) | m;
-    unsigned long long* w = W + 2 * lb;
-    unsigned long long old = atomicCAS(w, 0ull, mine);
-    if (old == 0ull) continue;
-    if ((old >> MW_BITS) == q) {
-      if ((old & m) != m) atomicOr(w, (unsigned long long)m);
-      continue;
-    }
-    old = atomicCAS(w + 1, 0ull, mine);
-    if (old == 0ull) continue;
-    if ((old >> MW_BITS) == q) {
-      if ((old & m) != m) atomicOr(w + 1, (unsigned long long)m);
-      continue;
-    }
-    uint32_t s = (uint32_t)(fmix64(h) >> 40) & (OVL - 1);
-    bool placed = false;
-    for (int pr = 0; pr < OVL; ++pr) {
-      const unsigned long long o2 = atomicCAS(&OK[s], 0ull, h + 1ull);
-      if (o2 == 0ull || o2 == h + 1ull) {
-        atomicOr(&OM[s], m);
-        placed = true;
-        break;
+  // RB_R records per thread loaded before any is merged (the loads overlap)
+  for (uint64_t r0 = 0; r0 < n; r0 += (uint64_t)RB_T * RB_R) {
+    unsigned long long h[RB_R];
+    uint32_t m[RB_R];
+#pragma unroll
+    for (int e = 0; e < RB_R; ++e) {
+      const uint64_t r = r0 + (uint64_t)e * RB_T + threadIdx.x;
+      h[e] = 0ull;
+      m[e] = 0u;
+      if (r < n) {
+        const uint64_t at = I.nsub == 1 ? (uint64_t)f * I.cap + r : part_at(I, f, s_off, r);
+        h[e] = I.key[at];
+        m[e] = I.mw[at];
       }
-      s = (s + 1) & (OVL - 1);
     }
-    if (!placed) {                            // LDS overflow set full: straight to HBM, membership incomplete
-      ovf_or(T, T.unperm(h), m, flags + 4);
-      atomicOr(flags + 4, F_LDS_SPILL);
-    }
+#pragma unroll
+    for (int e = 0; e < RB_R; ++e)
+      if (m[e]) range_or(W, OK, OM, T, h[e], m[e], (uint32_t)(h[e] >> T.qbits) & (rng - 1), qmask, flags);
   }
   __syncthreads();
   // the range, out whole; count keys, dBG entries (present orientations) and members
@@ -1074,29 +1090,47 @@ __global__ void k_tiles(const uint32_t* __restrict__ sched, uint32_t nj, uint32_
   }
 }
 
-// dBG export: (key, 12-bit mask) of both orientations of every entry
-__global__ void k_export_dbg(TableView T, uint64_t nw, uint64_t ntot, int k,
-                             unsigned long long* __restrict__ keys, unsigned short* __restrict__ masks,
-                             uint64_t cap, unsigned long long* __restrict__ counter) {
-  const int lane = threadIdx.x & 63;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntot;
-       i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t m = entry_mask(T, nw, i);
-    const bool pa = m & PRES_A, pb = m & PRES_B;
-    const unsigned long long ba = __ballot(pa), bb = __ballot(pb);
-    const unsigned na = __builtin_popcountll(ba), nbb = __builtin_popcountll(bb);
-    if (na + nbb == 0) continue;
-    const int leader = __builtin_ctzll(ba | bb);
-    unsigned long long base = 0;
-    if (lane == leader) base = atomicAdd(counter, (unsigned long long)(na + nbb));
-    base = __shfl(base, leader, 64);
-    if (!(pa || pb)) continue;
-    const uint64_t c = entry_key(T, nw, i);
+// dBG export: (key, 12-bit mask) of both orientations of every entry.  A
+// block takes EXE entries per thread in a contiguous chunk and reserves its
+// output run with one atomic (one per wave on the single counter serialised
+// ~1 M same-address atomics: 13 ms for a C3 table).
+constexpr int EXE = 8;
+__global__ void __launch_bounds__(256) k_export_dbg(TableView T, uint64_t nw, uint64_t ntot, int k,
+                                                   unsigned long long* __restrict__ keys,
+                                                   unsigned short* __restrict__ masks, uint64_t cap,
+                                                   unsigned long long* __restrict__ counter) {
+  __shared__ uint32_t s_scan[4];
+  __shared__ unsigned long long s_base;
+  for (uint64_t c0 = blockIdx.x * (uint64_t)(256 * EXE); c0 < ntot; c0 += (uint64_t)gridDim.x * 256 * EXE) {
+    uint32_t m[EXE];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < EXE; ++e) {
+      const uint64_t i = c0 + (uint64_t)threadIdx.x * EXE + e;
+      m[e] = i < ntot ? entry_mask(T, nw, i) : 0u;
+      cnt += ((m[e] & PRES_A) ? 1u : 0u) + ((m[e] & PRES_B) ? 1u : 0u);
+    }
+    uint32_t tot;
+    const uint32_t pre = block_excl_scan<256>(cnt, s_scan, tot);
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(counter, (unsigned long long)tot) : 0ull;
+    __syncthreads();
     // writes past cap are dropped; the host rejects a count above cap
-    const uint64_t oa = base + __builtin_popcountll(ba & lt), ob = base + na + __builtin_popcountll(bb & lt);
-    if (pa && oa < cap) { keys[oa] = c; masks[oa] = m & MASK12; }
-    if (pb && ob < cap) { keys[ob] = T.rc(c); masks[ob] = (m >> B_SHIFT) & MASK12; }
+    uint64_t o = s_base + pre;
+#pragma unroll
+    for (int e = 0; e < EXE; ++e) {
+      if (!(m[e] & (PRES_A | PRES_B))) continue;
+      const uint64_t i = c0 + (uint64_t)threadIdx.x * EXE + e;
+      const uint64_t c = entry_key(T, nw, i);
+      if (m[e] & PRES_A) {
+        if (o < cap) { keys[o] = c; masks[o] = m[e] & MASK12; }
+        ++o;
+      }
+      if (m[e] & PRES_B) {
+        if (o < cap) { keys[o] = T.rc(c); masks[o] = (m[e] >> B_SHIFT) & MASK12; }
+        ++o;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1320,16 +1354,18 @@ static void finish_build(Ctx& c, const ACount& a) {
     c.ovf_cap = ovf;
     c.bb = bb;
     // split levels: partition bits cb -> ... -> fp, <= 7 bits a pass
-    struct Lv { int L, S; uint64_t pin, cap, bpp, ctr_off; };
+    // (input regions: stage A's 8 per coarse bin, then one per partition)
+    struct Lv { int L, S; uint64_t pin, cap, nreg, bpr, ctr_off; };
     std::vector<Lv> lv;
-    uint64_t maxin = a.maxbin, ctr_words = 0;
+    uint64_t maxin = a.maxbin, maxreg = a.maxreg, nsub = 8, ctr_words = 0;
     for (int L = cb; L < fp;) {
       const int S = std::min(7, fp - L);
       const uint64_t pin = 1ull << L, nb = 1ull << S;
       const uint64_t capo = (uint64_t)((double)maxin / (double)nb * capx) + 64;
-      lv.push_back(Lv{L, S, pin, capo, (maxin + SCH - 1) / SCH, ctr_words});
+      lv.push_back(Lv{L, S, pin, capo, pin * nsub, (maxreg + SCH - 1) / SCH, ctr_words});
       ctr_words += CSTRIDE * pin * nb;
-      maxin = capo;
+      maxin = maxreg = capo;
+      nsub = 1;
       L += S;
     }
     uint64_t rec_max = 0;
@@ -1357,8 +1393,9 @@ static void finish_build(Ctx& c, const ACount& a) {
       const uint32_t nb = 1u << l.S;
       Recs out{c.recS_key[i & 1].as<unsigned long long>(), c.recS_mw[i & 1].as<uint32_t>(),
                c.ctrS.as<unsigned long long>() + l.ctr_off, l.cap, 1};
-      hipLaunchKernelGGL(k_split, dim3((unsigned)(l.pin * l.bpp)), dim3(SB), 0, c.stream, in, out,
-                         (uint32_t)(kb - l.L - l.S), nb, (uint32_t)l.bpp, c.flags.as<unsigned>());
+      if (l.nreg * l.bpr >= (1ull << 31)) throw Error(-22, "build: split grid too large");
+      hipLaunchKernelGGL(k_split, dim3((unsigned)(l.nreg * l.bpr)), dim3(SB), 0, c.stream, in, out,
+                         (uint32_t)(kb - l.L - l.S), nb, (uint32_t)l.bpr, c.flags.as<unsigned>());
       PG_HIP(hipGetLastError());
       in = out;
     }
@@ -1567,7 +1604,7 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {
   masks.reserve(2 * nmax);
   cnt.reserve(8);
   PG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
-  hipLaunchKernelGGL(k_export_dbg, dim3(grid_for(ntot, 256, 8192)), dim3(256), 0, c.stream, c.tv, 2 * c.cap, ntot,
+  hipLaunchKernelGGL(k_export_dbg, dim3(grid_for(ntot, 256 * EXE, 8192)), dim3(256), 0, c.stream, c.tv, 2 * c.cap, ntot,
                      c.k, keys.as<unsigned long long>(), masks.as<unsigned short>(), nmax, cnt.as<unsigned long long>());
   PG_HIP(hipGetLastError());
   unsigned long long n = 0;
