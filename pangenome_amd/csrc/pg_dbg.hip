@@ -893,30 +893,52 @@ k_split(Recs I, Recs O, uint32_t shift, uint32_t nb, uint32_t bpr, unsigned* __r
 }
 
 // ---------------------------------------------------------------- stage C
-// One block per fine partition f = buckets [f << rbits, (f + 1) << rbits):
-// its records are OR-merged into an LDS copy of the range (one 64-bit LDS CAS
-// creates a key with its masks, as the HBM table's layout has it: a bucket's
-// second word fills after its first; a key whose bucket is full goes to an
-// LDS overflow set and, once final, to the HBM overflow table).  The range is
-// then written out whole with 16-byte stores (every bucket of the table is
-// written by exactly one block: no clear), and every key's final masks give
-// its rdBG membership (build_rdbg_jit_ :1300-1305): members go to one of
-// NSEG output segments (one reservation per block), the dBG size and the
-// canonical key count to spread counters.
-constexpr int RB_T = 1024;                    // 2 blocks (32 waves) per CU: 70 KiB of LDS each
-constexpr int RB_R = 4;                       // records in flight per thread
+// Fine partition f = buckets [f << rbits, (f + 1) << rbits).  Its records are
+// OR-merged into an LDS copy of the range (one 64-bit LDS CAS creates a key
+// with its masks, as the HBM table's layout has it: a bucket's second word
+// fills after its first; a key whose bucket is full goes to an LDS overflow
+// set and, once final, to the HBM overflow table).  One pass over the range
+// then writes it out whole with 16-byte stores (every bucket of the table is
+// written by exactly one block: no clear), applies the rdBG rule
+// (build_rdbg_jit_ :1300-1305) to every key, whose masks are final there, and
+// zeroes the LDS copy for the block's next partition.
+// Persistent: block b takes partitions b, b + G, ...; the records of the next
+// partition are loaded into registers before the current one is merged, so
+// their latency hides behind the merge and the pass.  Each block appends its
+// rdBG members to its own output segment (no global atomics at all) and
+// leaves its key / dBG / member counts in its own counter slot.
+constexpr int RB_T = 512;                     // 2 blocks (16 waves) per CU: 70 KiB of LDS each
+constexpr int RB_R = 8;                       // records per thread and partition held in registers
 constexpr int RANGE_BITS = 12;                // <= 4096 buckets (64 KiB of LDS) per partition
 constexpr int OVL = 512;                      // LDS overflow slots per partition
-constexpr int NSEG = 64;
+constexpr int RB_CTR = 4;                     // per-block counters: keys, dBG entries, members
+constexpr uint32_t MQ = 64;                   // queued rdBG members per wave
 struct RdbgOut {
-  unsigned long long* keys;                   // segment s at [s * cap, (s+1) * cap)
-  unsigned long long* cursor;                 // per segment, CSTRIDE apart
+  unsigned long long* keys;                   // block b's members at [b * cap, (b+1) * cap)
+  unsigned long long* ctr;                    // per block: RB_CTR words
   uint64_t cap;
 };
 
 __device__ __forceinline__ uint32_t member_bits(uint32_t m) {   // bit0: A member, bit1: B member
   const uint32_t pa = (m >> 12) & 1u, pb = (m >> 25) & 1u;
   return (uint32_t)(pa && rdbg_member(m & MASK12)) | ((uint32_t)(pb && rdbg_member((m >> B_SHIFT) & MASK12)) << 1);
+}
+
+// a key whose bucket is full: the LDS overflow set (rare: out of line)
+__device__ __noinline__ void range_or_ovl(unsigned long long* OK, uint32_t* OM, const TableView& T, uint64_t h,
+                                          uint32_t m, unsigned* flags) {
+  uint32_t s = (uint32_t)(fmix64(h) >> 40) & (OVL - 1);
+  for (int pr = 0; pr < OVL; ++pr) {
+    const unsigned long long o2 = atomicCAS(&OK[s], 0ull, h + 1ull);
+    if (o2 == 0ull || o2 == h + 1ull) {
+      atomicOr(&OM[s], m);
+      return;
+    }
+    s = (s + 1) & (OVL - 1);
+  }
+  // LDS overflow set full: straight to HBM, membership incomplete (the host re-runs with more buckets)
+  ovf_or(T, T.unperm(h), m, flags + 4);
+  atomicOr(flags + 4, F_LDS_SPILL);
 }
 
 // OR one record (h, m) into the LDS range W (bucket lb) or the LDS overflow set
@@ -937,123 +959,149 @@ __device__ __forceinline__ void range_or(unsigned long long* W, unsigned long lo
     if ((old & m) != m) atomicOr(w + 1, (unsigned long long)m);
     return;
   }
-  uint32_t s = (uint32_t)(fmix64(h) >> 40) & (OVL - 1);
-  for (int pr = 0; pr < OVL; ++pr) {
-    const unsigned long long o2 = atomicCAS(&OK[s], 0ull, h + 1ull);
-    if (o2 == 0ull || o2 == h + 1ull) {
-      atomicOr(&OM[s], m);
-      return;
-    }
-    s = (s + 1) & (OVL - 1);
-  }
-  // LDS overflow set full: straight to HBM, membership incomplete (the host re-runs with more buckets)
-  ovf_or(T, T.unperm(h), m, flags + 4);
-  atomicOr(flags + 4, F_LDS_SPILL);
+  range_or_ovl(OK, OM, T, h, m, flags);
 }
 
-__global__ void __launch_bounds__(RB_T, 8)
-k_build_range(Recs I, TableView T, uint32_t rbits, RdbgOut R, unsigned long long* __restrict__ ctr,
-              unsigned* __restrict__ flags) {
+// records of partition f (one region of the last split level)
+__device__ __forceinline__ uint64_t part_count(const Recs& I, uint32_t f, uint32_t z) {
+  // z is a zero the compiler cannot see through: a vector load, counted by
+  // vmcnt, so that waiting on the LDS atomics does not wait on it
+  const unsigned long long n = I.cursor[CSTRIDE * (uint64_t)f + z];
+  return n < I.cap ? n : I.cap;
+}
+
+__global__ void __launch_bounds__(RB_T, 4)
+k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, unsigned* __restrict__ flags) {
   __shared__ unsigned long long W[2 << RANGE_BITS];
   __shared__ unsigned long long OK[OVL];      // h + 1, 0 = empty
   __shared__ uint32_t OM[OVL];
-  __shared__ unsigned long long s_off[9];
-  __shared__ uint32_t s_scan[RB_T / 64];
-  __shared__ unsigned long long s_rb;
+  __shared__ unsigned long long s_mcur;       // this block's members so far
+  __shared__ unsigned long long s_mq[RB_T / 64][MQ];   // per-wave member queue
   __shared__ unsigned long long s_red[2][RB_T / 64];
-  const uint32_t f = blockIdx.x, rng = 1u << rbits;
-  part_offsets(I, f, s_off);
+  const uint32_t rng = 1u << rbits, G = gridDim.x;
+  const uint64_t qmask = (1ull << T.qbits) - 1ull;
+  uint32_t z = 0;
+  asm volatile("" : "+v"(z));
   for (uint32_t i = threadIdx.x; i < 2 * rng; i += RB_T) W[i] = 0ull;
   for (uint32_t i = threadIdx.x; i < OVL; i += RB_T) { OK[i] = 0ull; OM[i] = 0u; }
-  __syncthreads();
-  const uint64_t n = s_off[I.nsub];
-  const uint64_t qmask = (1ull << T.qbits) - 1ull;
-  // RB_R records per thread loaded before any is merged (the loads overlap)
-  for (uint64_t r0 = 0; r0 < n; r0 += (uint64_t)RB_T * RB_R) {
-    unsigned long long h[RB_R];
-    uint32_t m[RB_R];
+  if (threadIdx.x == 0) s_mcur = 0ull;
+  uint32_t f = blockIdx.x;
+  unsigned long long ch[RB_R], nh[RB_R];
+  uint32_t cm[RB_R], nm[RB_R];
+  // (uniform base pointers per e, a 32-bit lane offset: one VGPR of address)
+  auto load = [&](uint32_t p, uint64_t n, unsigned long long (&h)[RB_R], uint32_t (&m)[RB_R]) {
+    const uint64_t pb = (uint64_t)(p < nparts ? p : 0) * I.cap;
+    const uint32_t nn = (uint32_t)(p < nparts ? (n < (uint64_t)RB_T * RB_R ? n : (uint64_t)RB_T * RB_R) : 0);
 #pragma unroll
     for (int e = 0; e < RB_R; ++e) {
-      const uint64_t r = r0 + (uint64_t)e * RB_T + threadIdx.x;
-      h[e] = 0ull;
-      m[e] = 0u;
-      if (r < n) {
-        const uint64_t at = I.nsub == 1 ? (uint64_t)f * I.cap + r : part_at(I, f, s_off, r);
-        h[e] = I.key[at];
-        m[e] = I.mw[at];
-      }
+      const unsigned long long* kp = I.key + pb + e * RB_T;
+      const uint32_t* mp = I.mw + pb + e * RB_T;
+      const bool ok = (uint32_t)(e * RB_T) + threadIdx.x < nn;
+      h[e] = ok ? kp[threadIdx.x] : 0ull;
+      m[e] = ok ? mp[threadIdx.x] : 0u;
     }
+  };
+  uint64_t n_cur = f < nparts ? part_count(I, f, z) : 0;
+  uint64_t n_nxt = f + G < nparts ? part_count(I, f + G, z) : 0;
+  load(f, n_cur, ch, cm);
+  uint32_t created = 0, ndbg = 0;
+  const uint64_t mseg = (uint64_t)blockIdx.x * R.cap;
+  // rdBG members: each wave queues h (| 1 << 63 for the rc orientation) in its
+  // own LDS buffer and turns a full buffer into keys with all 64 lanes busy
+  // (unperm + rc cost ~250 VALU per wave: run per bucket, nearly every wave
+  // paid them for a handful of member lanes)
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  uint32_t mp = 0;                                             // queued in this wave's buffer (wave-uniform)
+  auto flush = [&]() {
+    if (!mp) return;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(&s_mcur, (unsigned long long)mp);
+    base = __shfl(base, 0, 64);
+    if (lane < mp) {
+      const unsigned long long e = s_mq[wv][lane];
+      const uint64_t c = T.unperm(e & ~(1ull << 63));
+      const uint64_t o = base + lane;
+      if (o < R.cap) R.keys[mseg + o] = (e >> 63) ? T.rc(c) : c;
+      else atomicOr(flags + 4, F_RSEG_OVER);
+    }
+    mp = 0;
+  };
+  auto push1 = [&](unsigned long long e, bool on) {
+    const unsigned long long bal = __ballot(on);
+    const uint32_t n = (uint32_t)__builtin_popcountll(bal);
+    if (!n) return;
+    if (mp + n > MQ) flush();
+    if (on) s_mq[wv][mp + (uint32_t)__builtin_popcountll(bal & lt)] = e;
+    mp += n;
+  };
+  auto push = [&](uint64_t h, uint32_t mb) {                   // every lane of the wave calls it
+    push1(h, mb & 1u);
+    push1(h | (1ull << 63), mb & 2u);
+  };
+  __syncthreads();
+  for (; f < nparts; f += G) {                                 // block-uniform
+    load(f + G, n_nxt, nh, nm);                                // in flight during this partition
+    const uint64_t n_nn = f + 2 * G < nparts ? part_count(I, f + 2 * G, z) : 0;
 #pragma unroll
     for (int e = 0; e < RB_R; ++e)
-      if (m[e]) range_or(W, OK, OM, T, h[e], m[e], (uint32_t)(h[e] >> T.qbits) & (rng - 1), qmask, flags);
-  }
-  __syncthreads();
-  // the range, out whole; count keys, dBG entries (present orientations) and members
-  const uint64_t b0 = (uint64_t)f << rbits;
-  uint32_t created = 0, ndbg = 0, nmem = 0;
-  for (uint32_t i = threadIdx.x; i < rng; i += RB_T) {
-    const unsigned long long x = W[2 * i], y = W[2 * i + 1];
-    *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
-    if (x) {
-      const uint32_t m = (uint32_t)(x & MW_MASK);
-      ++created;
-      ndbg += ((m >> 12) & 1u) + ((m >> 25) & 1u);
-      nmem += __builtin_popcount(member_bits(m));
+      if (cm[e]) range_or(W, OK, OM, T, ch[e], cm[e], (uint32_t)(ch[e] >> T.qbits) & (rng - 1), qmask, flags);
+    for (uint64_t r = (uint64_t)RB_T * RB_R + threadIdx.x; r < n_cur; r += RB_T) {   // rare: a large partition
+      const unsigned long long h = I.key[(uint64_t)f * I.cap + r];
+      range_or(W, OK, OM, T, h, I.mw[(uint64_t)f * I.cap + r], (uint32_t)(h >> T.qbits) & (rng - 1), qmask, flags);
     }
-    if (y) {
-      const uint32_t m = (uint32_t)(y & MW_MASK);
-      ++created;
-      ndbg += ((m >> 12) & 1u) + ((m >> 25) & 1u);
-      nmem += __builtin_popcount(member_bits(m));
+    __syncthreads();
+    // the range out whole; counts; members queued; LDS zeroed
+    const uint64_t b0 = (uint64_t)f << rbits;
+    for (uint32_t i0 = 0; i0 < rng; i0 += RB_T) {              // every lane runs every trip (wave scans)
+      const uint32_t i = i0 + threadIdx.x;
+      const bool live = i < rng;
+      const unsigned long long x = live ? W[2 * i] : 0ull, y = live ? W[2 * i + 1] : 0ull;
+      if (live) {
+        *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
+        W[2 * i] = 0ull;
+        W[2 * i + 1] = 0ull;
+      }
+      const uint32_t mx = (uint32_t)(x & MW_MASK), my = (uint32_t)(y & MW_MASK);
+      created += (x ? 1u : 0u) + (y ? 1u : 0u);
+      ndbg += ((mx >> 12) & 1u) + ((mx >> 25) & 1u) + ((my >> 12) & 1u) + ((my >> 25) & 1u);
+      const uint32_t bx = x ? member_bits(mx) : 0u, by = y ? member_bits(my) : 0u;
+      push(((b0 + i) << T.qbits) | (x >> MW_BITS), bx);
+      push(((b0 + i) << T.qbits) | (y >> MW_BITS), by);
     }
+    static_assert(OVL % 64 == 0, "whole waves");
+    for (uint32_t i = threadIdx.x; i < OVL; i += RB_T) {
+      const unsigned long long kk = OK[i];
+      const uint32_t m = OM[i];
+      if (kk) {
+        ovf_or(T, T.unperm(kk - 1ull), m, flags + 4);
+        ++created;
+        ndbg += ((m >> 12) & 1u) + ((m >> 25) & 1u);
+        OK[i] = 0ull;
+        OM[i] = 0u;
+      }
+      push(kk - 1ull, kk ? member_bits(m) : 0u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < RB_R; ++e) { ch[e] = nh[e]; cm[e] = nm[e]; }
+    n_cur = n_nxt;
+    n_nxt = n_nn;
   }
-  for (uint32_t i = threadIdx.x; i < OVL; i += RB_T) {
-    if (!OK[i]) continue;
-    const uint32_t m = OM[i];
-    ovf_or(T, T.unperm(OK[i] - 1ull), m, flags + 4);
-    ++created;
-    ndbg += ((m >> 12) & 1u) + ((m >> 25) & 1u);
-    nmem += __builtin_popcount(member_bits(m));
-  }
-  uint32_t tot;
-  const uint32_t pre = block_excl_scan<RB_T>(nmem, s_scan, tot);
-  const uint32_t seg = f % NSEG;
-  if (threadIdx.x == 0) s_rb = tot ? atomicAdd(R.cursor + CSTRIDE * seg, (unsigned long long)tot) : 0ull;
-  {                                           // block sums of created / ndbg
-    unsigned long long a = created, b = ndbg;
-    for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
-    if ((threadIdx.x & 63) == 0) { s_red[0][threadIdx.x >> 6] = a; s_red[1][threadIdx.x >> 6] = b; }
-  }
+  flush();
+  // the block's counters
+  unsigned long long a = created, b = ndbg;
+  for (int o = 32; o > 0; o >>= 1) { a += __shfl_down(a, o, 64); b += __shfl_down(b, o, 64); }
+  if ((threadIdx.x & 63) == 0) { s_red[0][threadIdx.x >> 6] = a; s_red[1][threadIdx.x >> 6] = b; }
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long a = 0, b = 0;
-    for (int w = 0; w < RB_T / 64; ++w) { a += s_red[0][w]; b += s_red[1][w]; }
-    if (a) atomicAdd(ctr + CSTRIDE * (f % 64), a);
-    if (b) atomicAdd(ctr + CSTRIDE * (64 + f % 64), b);
+    unsigned long long sa = 0, sb = 0;
+    for (int w = 0; w < RB_T / 64; ++w) { sa += s_red[0][w]; sb += s_red[1][w]; }
+    unsigned long long* o = R.ctr + (uint64_t)blockIdx.x * RB_CTR;
+    o[0] = sa;
+    o[1] = sb;
+    o[2] = s_mcur;
   }
-  if (!tot) return;                                            // block-uniform
-  // members, in the same order as counted: key c of orientation A, rc(c) of B
-  unsigned long long o = s_rb + pre;
-  const uint64_t sb = (uint64_t)seg * R.cap;
-  auto put = [&](uint64_t key) {
-    if (o < R.cap) R.keys[sb + o] = key;
-    else atomicOr(flags + 4, F_RSEG_OVER);
-    ++o;
-  };
-  auto members = [&](uint64_t h, uint32_t m) {
-    const uint32_t mb = member_bits(m);
-    if (!mb) return;
-    const uint64_t c = T.unperm(h);
-    if (mb & 1u) put(c);
-    if (mb & 2u) put(T.rc(c));
-  };
-  for (uint32_t i = threadIdx.x; i < rng; i += RB_T) {
-    const unsigned long long x = W[2 * i], y = W[2 * i + 1];
-    if (x) members(((b0 + i) << T.qbits) | (x >> MW_BITS), (uint32_t)(x & MW_MASK));
-    if (y) members(((b0 + i) << T.qbits) | (y >> MW_BITS), (uint32_t)(y & MW_MASK));
-  }
-  for (uint32_t i = threadIdx.x; i < OVL; i += RB_T)
-    if (OK[i]) members(OK[i] - 1ull, OM[i]);
 }
 
 // ---------------------------------------------------------------- tiles
@@ -1187,6 +1235,13 @@ k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts, unsigned lon
       if (m[j]) out[s_base[own[j]] + rank[j]] = Slot{key[j] + 1ull, m[j], 0u};
     __syncthreads();
   }
+}
+
+// rdBG export: segment s (off[s+1] - off[s] keys at s * cap) to out + off[s]
+__global__ void k_gather_segs(const unsigned long long* __restrict__ seg, uint64_t cap,
+                              const unsigned long long* __restrict__ off, unsigned long long* __restrict__ out) {
+  const uint64_t s = blockIdx.x, o = off[s], n = off[s + 1] - o;
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) out[o + i] = seg[s * cap + i];
 }
 
 // ------------------------------------------------------------------ host
@@ -1358,11 +1413,12 @@ static void finish_build(Ctx& c, const ACount& a) {
     struct Lv { int L, S; uint64_t pin, cap, nreg, bpr, ctr_off; };
     std::vector<Lv> lv;
     uint64_t maxin = a.maxbin, maxreg = a.maxreg, nsub = 8, ctr_words = 0;
-    for (int L = cb; L < fp;) {
+    // (no split needed: one S = 0 pass still gathers each bin's 8 regions into one)
+    for (int L = cb; L < fp || lv.empty();) {
       const int S = std::min(7, fp - L);
       const uint64_t pin = 1ull << L, nb = 1ull << S;
       const uint64_t capo = (uint64_t)((double)maxin / (double)nb * capx) + 64;
-      lv.push_back(Lv{L, S, pin, capo, pin * nsub, (maxreg + SCH - 1) / SCH, ctr_words});
+      lv.push_back(Lv{L, S, pin, capo, pin * nsub, std::max<uint64_t>(1, (maxreg + SCH - 1) / SCH), ctr_words});
       ctr_words += CSTRIDE * pin * nb;
       maxin = maxreg = capo;
       nsub = 1;
@@ -1375,14 +1431,16 @@ static void finish_build(Ctx& c, const ACount& a) {
       c.recS_mw[i].reserve(4 * rec_max);
     }
     c.ctrS.reserve(8 * std::max<uint64_t>(ctr_words, 1));
-    const uint64_t rcap = (uint64_t)(rseg_frac * (double)a.total / NSEG) + 4096;
-    c.rseg.reserve(8 * NSEG * rcap);
+    const uint64_t nparts = 1ull << fp;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nparts, 2ull * (uint64_t)c.n_cu);   // persistent: 2 per CU
+    const uint64_t rcap = (uint64_t)(rseg_frac * (double)a.total / grid) + 4096;
+    c.rseg.reserve(8 * grid * rcap);
     c.rseg_cap = rcap;
-    c.k5_ctr.reserve(8 * CSTRIDE * (128 + NSEG));
+    c.rseg_nseg = grid;
+    c.k5_ctr.reserve(8 * RB_CTR * grid);
     FillList fl;
     fl.add(c.ovf.p, sizeof(Slot) * ovf);
     fl.add(c.ctrS.p, 8 * ctr_words);
-    fl.add(c.k5_ctr.p, 8 * CSTRIDE * (128 + NSEG));
     fl.add(c.flags.as<unsigned>() + 4, 16);                   // stage B/C bits (not the sentinel)
     c.t5.start(c.stream);
     fl.launch(c.stream);
@@ -1400,12 +1458,12 @@ static void finish_build(Ctx& c, const ACount& a) {
       in = out;
     }
     unsigned long long* k5 = c.k5_ctr.as<unsigned long long>();
-    const RdbgOut ro{c.rseg.as<unsigned long long>(), k5 + CSTRIDE * 128, rcap};
-    hipLaunchKernelGGL(k_build_range, dim3(1u << fp), dim3(RB_T), 0, c.stream, in, c.tv, rbits, ro, k5,
+    const RdbgOut ro{c.rseg.as<unsigned long long>(), k5, rcap};
+    hipLaunchKernelGGL(k_build_range, dim3(grid), dim3(RB_T), 0, c.stream, in, c.tv, rbits, (uint32_t)nparts, ro,
                        c.flags.as<unsigned>());
     PG_HIP(hipGetLastError());
     c.t5.stop(c.stream);
-    const size_t kbytes = 8 * CSTRIDE * (128 + NSEG);
+    const size_t kbytes = 8 * RB_CTR * grid;
     c.h_pin.reserve(kbytes + 4 * N_FLAGS);
     PG_HIP(hipMemcpyAsync(c.h_pin.p, c.k5_ctr.p, kbytes, hipMemcpyDeviceToHost, c.stream));
     PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + kbytes, c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost, c.stream));
@@ -1421,13 +1479,12 @@ static void finish_build(Ctx& c, const ACount& a) {
     if (bits & F_OVF_FULL) { ovf_mult *= 4; continue; }
     if (bits & F_RSEG_OVER) { rseg_frac = 2.0; continue; }
     uint64_t created = 0, ndbg = 0, nr = 0;
-    for (int i = 0; i < 64; ++i) {
-      created += h[CSTRIDE * i];
-      ndbg += h[CSTRIDE * (64 + i)];
-    }
-    for (int s = 0; s < NSEG; ++s) {
-      c.rseg_cnt[s] = h[CSTRIDE * (128 + s)];
-      nr += c.rseg_cnt[s];
+    c.rseg_cnt.resize(grid);
+    for (uint32_t b = 0; b < grid; ++b) {
+      created += h[RB_CTR * b];
+      ndbg += h[RB_CTR * b + 1];
+      c.rseg_cnt[b] = h[RB_CTR * b + 2];
+      nr += c.rseg_cnt[b];
     }
     c.n_canon = created;
     c.n_dbg = ndbg + c.sentinel;
@@ -1628,16 +1685,26 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {
 uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap) {
   if (!c.reduced) throw Error(-22, "export_rdbg: no rdBG (call pg_build_rdbg first)");
   if (h_keys && cap >= c.n_rdbg) {
-    uint64_t o = 0;
-    for (int s = 0; s < NSEG; ++s) {
-      const uint64_t n = c.rseg_cnt[s];
-      if (n)
-        PG_HIP(hipMemcpyAsync(h_keys + o, c.rseg.as<unsigned long long>() + (uint64_t)s * c.rseg_cap, 8 * n,
-                              hipMemcpyDeviceToHost, c.stream));
-      o += n;
+    // the blocks' segments gathered on the device into one run, one copy back
+    const uint64_t nseg = c.rseg_nseg, n = c.n_rdbg - c.sentinel;
+    std::vector<unsigned long long> off(nseg + 1, 0);
+    for (uint64_t s = 0; s < nseg; ++s) off[s + 1] = off[s] + c.rseg_cnt[s];
+    DevBuf d_off, out;
+    d_off.reserve(8 * (nseg + 1));
+    out.reserve(8 * std::max<uint64_t>(n, 1));
+    c.h_pin.reserve(8 * (nseg + 1));
+    std::memcpy(c.h_pin.p, off.data(), 8 * (nseg + 1));
+    PG_HIP(hipMemcpyAsync(d_off.p, c.h_pin.p, 8 * (nseg + 1), hipMemcpyHostToDevice, c.stream));
+    if (n) {
+      hipLaunchKernelGGL(k_gather_segs, dim3((unsigned)nseg), dim3(256), 0, c.stream, c.rseg.as<unsigned long long>(),
+                         c.rseg_cap, d_off.as<unsigned long long>(), out.as<unsigned long long>());
+      PG_HIP(hipGetLastError());
+      PG_HIP(hipMemcpyAsync(h_keys, out.p, 8 * n, hipMemcpyDeviceToHost, c.stream));
     }
     c.sync();
-    if (c.sentinel) h_keys[o] = SENTINEL;
+    d_off.release();
+    out.release();
+    if (c.sentinel) h_keys[n] = SENTINEL;
   }
   return c.n_rdbg;
 }

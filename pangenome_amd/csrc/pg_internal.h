@@ -138,10 +138,10 @@ struct Ctx {
   uint64_t capA = 0;                  // records per stage A region
   DevBuf recS_key[2], recS_mw[2];     // stage B outputs (ping-pong)
   DevBuf ctrS;                        // stage B cursors, all levels
-  DevBuf rseg;                        // rdBG keys: NSEG segments of rseg_cap
-  DevBuf k5_ctr;                      // key / dBG counts and rdBG segment cursors
-  uint64_t rseg_cap = 0;
-  uint64_t rseg_cnt[64] = {};
+  DevBuf rseg;                        // rdBG keys: one segment of rseg_cap per stage C block
+  DevBuf k5_ctr;                      // per stage C block: key / dBG / member counts
+  uint64_t rseg_cap = 0, rseg_nseg = 0;
+  std::vector<uint64_t> rseg_cnt;     // members per segment
   uint64_t n_records_a = 0;           // stage A records of the last build
   double u_ratio = 0, r_ratio = 0;    // last build: records per forward window, rdBG keys per record
 
