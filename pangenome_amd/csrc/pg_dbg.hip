@@ -37,6 +37,12 @@
 
 #include "pg_internal.h"
 
+// Development experiments (tools/exp_build.sh builds variants with
+// -DPG_EXP_BITS=n into separate libraries; the product build has none)
+#ifndef PG_EXP_BITS
+#define PG_EXP_BITS 0
+#endif
+
 namespace pg {
 
 constexpr int IBLOCK = 256;
@@ -925,7 +931,7 @@ __device__ __forceinline__ uint32_t member_bits(uint32_t m) {   // bit0: A membe
 }
 
 // a key whose bucket is full: the LDS overflow set (rare: out of line)
-__device__ __noinline__ void range_or_ovl(unsigned long long* OK, uint32_t* OM, const TableView& T, uint64_t h,
+__device__ __forceinline__ void range_or_ovl(unsigned long long* OK, uint32_t* OM, const TableView& T, uint64_t h,
                                           uint32_t m, unsigned* flags) {
   uint32_t s = (uint32_t)(fmix64(h) >> 40) & (OVL - 1);
   for (int pr = 0; pr < OVL; ++pr) {
@@ -1041,11 +1047,12 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
   };
   __syncthreads();
   for (; f < nparts; f += G) {                                 // block-uniform
-    load(f + G, n_nxt, nh, nm);                                // in flight during this partition
+    if (!(PG_EXP_BITS & 4)) load(f + G, n_nxt, nh, nm);       // in flight during this partition
     const uint64_t n_nn = f + 2 * G < nparts ? part_count(I, f + 2 * G, z) : 0;
 #pragma unroll
     for (int e = 0; e < RB_R; ++e)
-      if (cm[e]) range_or(W, OK, OM, T, ch[e], cm[e], (uint32_t)(ch[e] >> T.qbits) & (rng - 1), qmask, flags);
+      if (cm[e] && !(PG_EXP_BITS & 2))
+        range_or(W, OK, OM, T, ch[e], cm[e], (uint32_t)(ch[e] >> T.qbits) & (rng - 1), qmask, flags);
     for (uint64_t r = (uint64_t)RB_T * RB_R + threadIdx.x; r < n_cur; r += RB_T) {   // rare: a large partition
       const unsigned long long h = I.key[(uint64_t)f * I.cap + r];
       range_or(W, OK, OM, T, h, I.mw[(uint64_t)f * I.cap + r], (uint32_t)(h >> T.qbits) & (rng - 1), qmask, flags);
@@ -1058,7 +1065,7 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       const bool live = i < rng;
       const unsigned long long x = live ? W[2 * i] : 0ull, y = live ? W[2 * i + 1] : 0ull;
       if (live) {
-        *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
+        if (!(PG_EXP_BITS & 1)) *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
         W[2 * i] = 0ull;
         W[2 * i + 1] = 0ull;
       }
@@ -1066,8 +1073,10 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       created += (x ? 1u : 0u) + (y ? 1u : 0u);
       ndbg += ((mx >> 12) & 1u) + ((mx >> 25) & 1u) + ((my >> 12) & 1u) + ((my >> 25) & 1u);
       const uint32_t bx = x ? member_bits(mx) : 0u, by = y ? member_bits(my) : 0u;
-      push(((b0 + i) << T.qbits) | (x >> MW_BITS), bx);
-      push(((b0 + i) << T.qbits) | (y >> MW_BITS), by);
+      if (!(PG_EXP_BITS & 8)) {
+        push(((b0 + i) << T.qbits) | (x >> MW_BITS), bx);
+        push(((b0 + i) << T.qbits) | (y >> MW_BITS), by);
+      }
     }
     static_assert(OVL % 64 == 0, "whole waves");
     for (uint32_t i = threadIdx.x; i < OVL; i += RB_T) {
@@ -1083,6 +1092,7 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       push(kk - 1ull, kk ? member_bits(m) : 0u);
     }
     __syncthreads();
+    if (PG_EXP_BITS & 4) load(f + G, n_nxt, nh, nm);
 #pragma unroll
     for (int e = 0; e < RB_R; ++e) { ch[e] = nh[e]; cm[e] = nm[e]; }
     n_cur = n_nxt;
