@@ -47,7 +47,8 @@ namespace pg {
 
 constexpr int IBLOCK = 256;
 constexpr int IW = 16;                        // windows per thread (one segment)
-constexpr int TILE = IBLOCK * IW;             // windows per tile (one coverage block)
+constexpr int CBLOCK = 256;                   // coverage block (one tile)
+constexpr int TILE = CBLOCK * IW;             // windows per tile (one coverage block)
 constexpr int SPAN = TILE + 64;               // staged bytes (k <= 27: TILE + k + 3 <= SPAN - 16)
 constexpr int CSTRIDE = 8;                    // counter spacing: one 64-byte line (uint64 words)
 
@@ -229,7 +230,7 @@ struct WorkItem {
 // line; a tile appends to sub-queue (its block) % NQ.  One counter shared by
 // all ~120 K tiles of a C3 launch serialises their atomics at the memory side
 // (1.48 ms measured, tools/rates.hip) - as long as the whole coverage pass;
-// 64 counters take 0.045 ms.  A tile appends at most IBLOCK items.
+// 64 counters take 0.045 ms.  A tile appends at most CBLOCK items.
 constexpr int NQ = 64;
 constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long long words)
 
@@ -247,7 +248,7 @@ struct DriftRef {
 };
 __device__ __forceinline__ void find_drift_pair(const uint8_t* s_cls, long long base, long long qt, long long rn,
                                                 const DriftRef& A, const DriftRef& B, bool two) {
-  static_assert(2 * NANCH * 32 <= IBLOCK && (2 * HWIN2) / 4 + 2 <= 32, "two pairs per wave in stage 1");
+  static_assert(2 * NANCH * 32 <= CBLOCK && (2 * HWIN2) / 4 + 2 <= 32, "two pairs per wave in stage 1");
   constexpr int NW = (2 * DRIFT + 3) / 4 + 2;
   auto task = [&](const uint8_t* s_ref, int ia, int ibhi, int lo, int hi, int w, unsigned* best) {
     const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
@@ -315,7 +316,7 @@ __device__ __forceinline__ void find_drift_pair(const uint8_t* s_cls, long long 
     for (int ai = 0; ai < NANCH; ++ai) {
       int ia, ibhi, lo, hi;
       geom(R, ai, ia, ibhi, lo, hi);
-      for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += IBLOCK)
+      for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += CBLOCK)
         task(R.s, ia, ibhi, lo, hi, w, R.best + ai);
     }
   }
@@ -487,8 +488,12 @@ __host__ __device__ __forceinline__ void xcd_chunk(uint64_t ntiles, uint32_t b0,
 // ahead, and the stage-2 search then ran on ~9 % of tiles).  A persistent,
 // software-pipelined form of this kernel (register prefetch of the next
 // tile) measured slower: 1.02 vs 0.76 ms at 64 VGPRs with spills, against
-// one-tile blocks at 8 waves/SIMD.
-__global__ void __launch_bounds__(IBLOCK)
+// one-tile blocks at 8 waves/SIMD; rebuilt without spills (117 VGPRs, 4
+// blocks per CU, descriptor two tiles ahead, hints and staging one tile
+// ahead, the queue reservation consumed a tile later) it ran 909 vs 845 us
+// for all of C3's tiles in one launch: the pass is not bound by its
+// dependent memory round trips.
+__global__ void __launch_bounds__(CBLOCK)
 k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
         long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints, int nrec,
@@ -497,7 +502,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
   __shared__ __attribute__((aligned(16))) uint8_t s_ref2[RSPAN];
   __shared__ unsigned s_best[NANCH], s_best2[NANCH];
-  __shared__ uint32_t s_scan[IBLOCK / 64];
+  __shared__ uint32_t s_scan[CBLOCK / 64];
   __shared__ unsigned long long s_qbase;
   __shared__ Drifts s_dr[2];
   uint64_t t, te;
@@ -524,10 +529,10 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   Stage g2 = g;
   if (dedup2) ref_span(g2, k, r2s, r2n);
   // staging: at most two 16-byte chunks per thread and span, predicated
-  // (the spans are < 2 * IBLOCK * 16 bytes: SPAN, RSPAN)
-  static_assert(SPAN + 16 <= 2 * IBLOCK * 16 && RSPAN <= 2 * IBLOCK * 16, "two chunks per thread");
+  // (the spans are < 2 * CBLOCK * 16 bytes: SPAN, RSPAN)
+  static_assert(SPAN + 16 <= 2 * CBLOCK * 16 && RSPAN <= 2 * CBLOCK * 16, "two chunks per thread");
   auto stage2 = [&](uint8_t* dst, long long from, long long to) {
-    const long long o0 = (long long)threadIdx.x * 16, o1 = o0 + IBLOCK * 16;
+    const long long o0 = (long long)threadIdx.x * 16, o1 = o0 + CBLOCK * 16;
     const bool l0 = from + o0 < to, l1 = from + o1 < to;
     uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
     if (l0) v0 = *reinterpret_cast<const uint4*>(cls + from + o0);
@@ -574,7 +579,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
   }
   const bool work = q0 <= last && covered != ALL;
   uint32_t nwork;
-  const uint32_t pos = block_excl_scan<IBLOCK>(work ? 1u : 0u, s_scan, nwork);
+  const uint32_t pos = block_excl_scan<CBLOCK>(work ? 1u : 0u, s_scan, nwork);
   const unsigned sub = blockIdx.x % NQ;
   if (threadIdx.x == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
   __syncthreads();
@@ -1543,7 +1548,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
       xcd_chunk(ntiles, (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch, (uint64_t)x, t, te);
       gc[i] = std::max<uint64_t>(gc[i], 8 * (te - t));
     }
-    qcapc[i] = (gc[i] + NQ - 1) / NQ * IBLOCK;      // per sub-queue
+    qcapc[i] = (gc[i] + NQ - 1) / NQ * CBLOCK;      // per sub-queue
     qoff[i] = items;
     items += NQ * qcapc[i];
   }
@@ -1571,7 +1576,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     auto* qi = q + qoff[i];
     auto* qni = qn + (cbytes / 8) * i;
     if (gc[i])
-      hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), b, covpad, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
+      hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), dim3(CBLOCK), covpad, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
                          c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
                          (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch);
     PG_HIP(hipGetLastError());
