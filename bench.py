@@ -51,33 +51,44 @@ def workload(config: str, rank: int, world: int):
     raise SystemExit("unknown --config %s" % config)
 
 
-def cpu_baseline(config: str, full: bool = False):
+def cpu_baseline(config: str, sample: bool = False):
     """The oracle's faithful single-core restatement (same oakht hash, probe
-    sequence, growth and 3 probes per occurrence as kmer_numba.py) on a bounded
-    prefix of the same workload (~10-30 s of CPU work), or the whole batch
-    with --cpu-full (C3: a few minutes).  Peak RSS is the process's."""
+    sequence, growth and 3 probes per occurrence as kmer_numba.py) on the
+    whole workload batch (C3 in full, ~2 min on one core), or
+    on its first 12 genomes with --cpu-sample (~12 s).  A heartbeat goes to
+    stderr every 30 s while it runs.  Peak RSS is the process's (it includes
+    the torch/HIP runtime); table_bytes is the oracle's oakht at 11 B/slot."""
     import resource
+    import threading
     from oracle import oracle
     from pangenome_amd import synth
     if config == "c2":
-        fa, sample = synth.ecoli_like(), "whole C2 genome (4.64 Mbp)"
+        fa, desc = synth.ecoli_like(), "whole C2 genome (4.64 Mbp)"
     else:
-        g = 100 if full else 12
+        g = 12 if sample else 100
         fa = synth.pangenome(g, 5_000_000, snp=1e-3, indel=1e-4)
-        sample = ("all 100 C3 genomes (500 Mbp)" if full else "first %d of the C3 genomes (%.0f Mbp)" % (g, g * 5.0)) \
-            + ", dBG + rdBG, k=27, -c 2"
-    r = oracle.OracleRun(fa, K, 2)
+        desc = ("all 100 C3 genomes (500 Mbp, batch c3a)" if not sample else
+                "first %d of the C3 genomes (%.0f Mbp)" % (g, g * 5.0)) + ", dBG + rdBG, k=27, -c 2"
+    done = threading.Event()
+
+    def beat():
+        t0 = time.time()
+        while not done.wait(30):
+            print("cpu_baseline: %.0f s" % (time.time() - t0), file=sys.stderr, flush=True)
+    th = threading.Thread(target=beat, daemon=True)
+    th.start()
+    try:
+        r = oracle.OracleRun(fa, K, 2)
+    finally:
+        done.set()
     t_dbg, t_rdbg = r.timings()
     rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0
+    lib = oracle.lib()
     return {"value": r.n_bases() / (t_dbg + t_rdbg) / 1e9, "unit": "Gbp/s", "cores": 1, "kind": "port",
-            "sample": sample, "t_dbg_s": round(t_dbg, 3), "t_rdbg_s": round(t_rdbg, 3),
-            "n_dbg": int(lib_n(r)), "peak_rss_mb": round(rss, 1),
+            "sample": desc, "t_dbg_s": round(t_dbg, 3), "t_rdbg_s": round(t_rdbg, 3),
+            "n_dbg": int(lib.pgo_n_dbg(r.h)), "n_rdbg": int(lib.pgo_n_rdbg(r.h)),
+            "table_bytes": int(lib.pgo_dbg_capacity(r.h)) * 11, "peak_rss_mb": round(rss, 1),
             "cpu": _cpu_model(), "nproc": os.cpu_count()}
-
-
-def lib_n(r):
-    from oracle import oracle
-    return oracle.lib().pgo_n_dbg(r.h)
 
 
 def _cpu_model():
@@ -116,7 +127,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-full", action="store_true", help="CPU baseline on the whole batch (minutes)")
+    ap.add_argument("--cpu-sample", action="store_true", help="CPU baseline on 12 of the 100 C3 genomes (~12 s)")
     args = ap.parse_args()
 
     import torch
@@ -182,12 +193,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ins_ms, scan_ms, parse_ms, counts = [], [], [], []
+    ins_ms, split_ms, range_ms, parse_ms, counts = [], [], [], [], []
     last = None
     for i in range(args.steps):
         last = step(ctx, args.warmup + i)
         ins_ms.append(last[0].ms_insert)
-        scan_ms.append(last[1].ms_scan)
+        split_ms.append(last[1].ms_split)
+        range_ms.append(last[1].ms_range)
         parse_ms.append(last[0].ms_parse)
         counts.append(((args.warmup + i) % len(d_in), last[2], last[3]))
     torch.cuda.synchronize()
@@ -257,19 +269,41 @@ def main():
     ms_step = 1e3 * elapsed / args.steps
     value = total_bases / elapsed / 1e9
 
-    # roofline of the dominant kernel group, K3 (this rank): the coverage and
-    # work passes of all chunks, bracketed by one HIP-event pair on the
-    # context's stream (the side stream joins it before the stop event);
-    # algorithmic bytes = 1 B class code per base + 20 B per forward window
-    # (8 B key + 2 B mask on each strand); averaged over the
-    # timed steps
-    ins_avg = float(np.mean(ins_ms))
-    ins_bytes = st_b.n_bases + 20 * (st_b.n_windows // 2)
-    achieved = ins_bytes / (ins_avg * 1e-3)
-    traffic = None
+    # ---- roofline.  Per kernel, ALGORITHMIC bytes = what the kernel must read
+    # and write by its own definition, over its HIP-event time
+    # on the context's stream, averaged over the timed steps:
+    #   K1 parse    F FASTA bytes read + B class codes written
+    #   K3 stage A  B class codes read + 12 B per emitted record (8 B h + 4 B mask word)
+    #   K3 stage B  24 B per record (read + write; one split pass at C3)
+    #   K3 stage C  12 B per record read + 16 B per table bucket + 8 B per rdBG key written
+    # The dominant kernel (the longest span) is `roofline`; `traffic` is its
+    # PMC-measured HBM bytes per build (profiles/traffic_<config>.json, from
+    # a separate rocprofv3 run).  SURVEY.md §8(d)'s path model, F + 20 W +
+    # 10 D + 8 R, is `path.alg_bytes_s8d`: it charges every window 20 B that
+    # the coverage pass never moves, so it is an "equivalent" figure.
+    st_b, st_c = last[0], last[1]             # stage A stats; stage B/C (N>1: the owner merge's)
+    nrec_a = st_b.n_records_a
+    spans = {
+        "k1_parse": (float(np.mean(parse_ms)), nbytes[-1] + st_b.n_bases,
+                     "F FASTA bytes read + B class codes written"),
+        "k3a_cover_emit": (float(np.mean(ins_ms)), st_b.n_bases + 12 * nrec_a,
+                           "B class codes read + 12 B per emitted record"),
+        "k3b_split": (float(np.mean(split_ms)), 24 * st_c.n_records_a, "24 B per record (read + write)"),
+        "k3c_range": (float(np.mean(range_ms)), 12 * st_c.n_records_a + 16 * st_c.table_capacity + 8 * st_c.n_rdbg,
+                      "12 B per record + 16 B per bucket + 8 B per rdBG key"),
+    }
+    pmc = {}
     tp = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.isfile(tp):
-        traffic = json.load(open(tp)).get("k_insert_hbm_bytes_per_launch")
+        pmc = json.load(open(tp)).get("hbm_bytes_per_build", {})
+    kernels = {}
+    for name, (ms, ab, model) in spans.items():
+        kernels[name] = {"ms": round(ms, 4), "alg_bytes": int(ab), "alg_model": model,
+                         "frac": round(ab / (ms * 1e-3) / HBM_PEAK, 4) if ms > 0 else None,
+                         "pmc_bytes": pmc.get(name), "pmc_frac": round(pmc[name] / (ms * 1e-3) / HBM_PEAK, 4)
+                         if pmc.get(name) and ms > 0 else None}
+    dom = max(kernels, key=lambda n: kernels[n]["ms"])
+    kd = kernels[dom]
     # whole-path algorithmic fraction, SURVEY.md §8(d): F + 20 W + 10 D + 8 R
     path_bytes = bytes_all + 20 * wfw_all + 10 * n_dbg + 8 * n_rdbg
 
@@ -290,16 +324,16 @@ def main():
                    "bases_per_gpu": st_b.n_bases, "fasta_bytes_per_gpu": nbytes[0],
                    "input": "FASTA resident in HBM when the timed region starts",
                    "parallelism": "record-sharded, owner all-to-all" if world > 1 else "single GPU"},
-        "roofline": {"kernel": "K3 = k_cover + k_insert_work in 4 chunks on 2 streams (one HIP-event span)", "bound": "hbm",
-                     "achieved": round(achieved / 1e9, 2),
-                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
-                     "traffic": traffic, "traffic_source": "profile-derived (profiles/traffic_%s.json)" % args.config,
-                     "alg_bytes_per_launch": ins_bytes,
-                     "avg_launch_ms": round(ins_avg, 4)},
-        "path": {"alg_bytes": path_bytes, "frac_of_hbm": round(path_bytes / (elapsed / args.steps) /
-                                                             (world * HBM_PEAK), 5),
-                 "ms_parse": round(float(np.mean(parse_ms)), 3), "ms_insert": round(ins_avg, 3),
-                 "ms_scan": round(float(np.mean(scan_ms)), 3), "n_dbg": n_dbg, "n_rdbg": n_rdbg,
+        "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(kd["alg_bytes"] / (kd["ms"] * 1e-3) / 1e9, 2),
+                     "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": kd["frac"],
+                     "traffic": kd["pmc_bytes"], "traffic_frac": kd["pmc_frac"],
+                     "traffic_source": "PMC FETCH_SIZE x2 + WRITE_SIZE per build, profiles/traffic_%s.json" % args.config,
+                     "alg_bytes_per_launch": kd["alg_bytes"], "alg_model": kd["alg_model"],
+                     "avg_launch_ms": kd["ms"]},
+        "kernels": kernels,
+        "path": {"alg_bytes_s8d": path_bytes, "frac_of_hbm_s8d": round(path_bytes / (elapsed / args.steps) /
+                                                                         (world * HBM_PEAK), 5),
+                 "n_records_a": nrec_a, "n_dbg": n_dbg, "n_rdbg": n_rdbg,
                  "table_slots": st_b.table_capacity, "exchange_bytes_sent_rank0": sent,
                  "cold_first_build_ms": round(cold_ms, 3),
                  "cold_first_build_gbps": round(cst[0].n_bases / cold_ms / 1e6, 3)},
@@ -311,7 +345,7 @@ def main():
     if parity is not None:
         out["parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_full)
+        out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_sample)
     if rehearse:
         out["data"] += "; REHEARSAL: all ranks on cuda:0 over gloo, not a measurement"
     if rank == 0:

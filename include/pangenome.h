@@ -53,6 +53,9 @@ typedef struct pg_stats {
   double ms_insert;        /* K3 stage A: coverage + work passes (record emission)*/
   double ms_scan;          /* K3 stages B + C: partition merge with the fused K5  */
   uint64_t sentinel;       /* 1 if the n<k key (2^64-1) is in the dBG              */
+  uint64_t n_records_a;    /* K3 stage A records (windows the coverage pass kept)  */
+  double ms_split;         /* K3 stage B: k_split pass(es)                         */
+  double ms_range;         /* K3 stage C: k_build_range (table + fused K5)         */
 } pg_stats;
 
 /* Context on HIP device `device` for k-mer length k (clamped to [1, 27] as

@@ -27,6 +27,7 @@ class PgStats(C.Structure):
         ("n_slots", C.c_uint64), ("table_capacity", C.c_uint64),
         ("ms_parse", C.c_double), ("ms_clear", C.c_double), ("ms_insert", C.c_double),
         ("ms_scan", C.c_double), ("sentinel", C.c_uint64),
+        ("n_records_a", C.c_uint64), ("ms_split", C.c_double), ("ms_range", C.c_double),
     ]
 
     def as_dict(self):

@@ -43,6 +43,9 @@ static void fill_stats(const pg::Ctx& c, pg_stats* s) {
   s->ms_clear = c.ms_clear;
   s->ms_insert = c.ms_insert;
   s->ms_scan = c.ms_scan;
+  s->n_records_a = c.n_records_a;
+  s->ms_split = c.ms_split;
+  s->ms_range = c.ms_range;
   s->sentinel = c.sentinel;
 }
 
@@ -87,6 +90,7 @@ void pg_destroy(pg_ctx* x) {
   c.t0.destroy();
   c.t1.destroy();
   c.t5.destroy();
+  c.t6.destroy();
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c.stream2);

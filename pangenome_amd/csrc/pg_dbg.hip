@@ -1410,6 +1410,7 @@ static void finish_build(Ctx& c, const ACount& a) {
   uint64_t ovf_mult = 1;
   double rseg_frac = c.r_ratio > 0 ? std::min(2.0, 1.5 * c.r_ratio + 0.002) : 2.0;
   c.t5.init();
+  c.t6.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
     const int fp = std::max(cb, bb - RANGE_BITS);
     const uint32_t rbits = (uint32_t)(bb - fp);
@@ -1474,16 +1475,20 @@ static void finish_build(Ctx& c, const ACount& a) {
     }
     unsigned long long* k5 = c.k5_ctr.as<unsigned long long>();
     const RdbgOut ro{c.rseg.as<unsigned long long>(), k5, rcap};
+    c.t6.start(c.stream);
     hipLaunchKernelGGL(k_build_range, dim3(grid), dim3(RB_T), 0, c.stream, in, c.tv, rbits, (uint32_t)nparts, ro,
                        c.flags.as<unsigned>());
     PG_HIP(hipGetLastError());
     c.t5.stop(c.stream);
+    c.t6.stop(c.stream);
     const size_t kbytes = 8 * RB_CTR * grid;
     c.h_pin.reserve(kbytes + 4 * N_FLAGS);
     PG_HIP(hipMemcpyAsync(c.h_pin.p, c.k5_ctr.p, kbytes, hipMemcpyDeviceToHost, c.stream));
     PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + kbytes, c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost, c.stream));
     c.sync();
     c.ms_scan = c.t5.ms();
+    c.ms_range = c.t6.ms();
+    c.ms_split = c.ms_scan - c.ms_range;
     const unsigned long long* h = c.h_pin.as<unsigned long long>();
     const unsigned bits = reinterpret_cast<const unsigned*>(c.h_pin.as<uint8_t>() + kbytes)[4];
     if (bits & F_SPLIT_OVER) { capx *= 1.5; continue; }

@@ -186,8 +186,8 @@ struct Ctx {
   uint64_t dump_size = 0, dump_sentinel = 0;
 
   // timings of the last calls (ms, HIP events on `stream`)
-  Timer t0, t1, t5;
-  double ms_parse = 0, ms_clear = 0, ms_insert = 0, ms_short = 0, ms_scan = 0;
+  Timer t0, t1, t5, t6;
+  double ms_parse = 0, ms_clear = 0, ms_insert = 0, ms_short = 0, ms_scan = 0, ms_split = 0, ms_range = 0;
   double ms_total_build = 0;
 
   void sync() { PG_HIP(hipStreamSynchronize(stream)); }
