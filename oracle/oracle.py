@@ -50,6 +50,7 @@ def lib():
         L.pgo_dbg_capacity.restype = i64
         L.pgo_get_edges.argtypes = [P, P, P]
         L.pgo_get_rows.argtypes = [P, P]
+        L.pgo_set_rdbg.argtypes = [P, P, i64]
         L.pgo_free.argtypes = [P]
         _lib = L
     return _lib
@@ -117,6 +118,11 @@ class OracleRun:
         keys = np.empty(n, np.uint64)
         lib().pgo_get_rdbg(self.h, keys.ctypes.data)
         return np.sort(keys)
+
+    def set_rdbg(self, keys):
+        """Replace the rdBG key set the edge and row passes query (-D)."""
+        keys = np.ascontiguousarray(keys, dtype=np.uint64)
+        lib().pgo_set_rdbg(self.h, keys.ctypes.data, keys.shape[0])
 
     def timings(self):
         return lib().pgo_seconds_dbg(self.h), lib().pgo_seconds_rdbg(self.h)

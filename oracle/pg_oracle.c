@@ -580,6 +580,12 @@ void pgo_get_rows(const pgo_result* r, int64_t* out) {
         out[6 * i + 3] = w->end; out[6 * i + 4] = w->strand; out[6 * i + 5] = w->label;
     }
 }
+void pgo_set_rdbg(pgo_result* r, const uint64_t* keys, int64_t n) {
+    if (r->has_rdbg) oak_free(&r->rdbg);
+    oak_init(&r->rdbg, 1 << 20); r->has_rdbg = 1;            /* init_dict, then __setitem__ per key */
+    for (int64_t i = 0; i < n; i++) oak_push(&r->rdbg, keys[i], 0);
+}
+
 void pgo_free(pgo_result* r) {
     if (!r) return;
     if (r->has_dbg) oak_free(&r->dbg);

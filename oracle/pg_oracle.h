@@ -68,6 +68,12 @@ void pgo_get_edges(const pgo_result* r, uint64_t* tuples, int64_t* counts);
  * header bytes are buf[header_start : header_start+header_len] and include '>'. */
 void pgo_get_rows(const pgo_result* r, int64_t* rows6);
 
+/* Replace the rdBG key set (what load_on_disk of a -D file gives seq2graph,
+ * :2093): the edge and row passes then query exactly these keys.  Used by the
+ * multi-GPU tests, where every rank walks its records against the rdBG
+ * gathered from all owners. */
+void pgo_set_rdbg(pgo_result* r, const uint64_t* keys, int64_t n);
+
 void pgo_free(pgo_result* r);
 
 #ifdef __cplusplus

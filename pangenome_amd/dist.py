@@ -1,22 +1,71 @@
-"""Multi-GPU dBG -> rdBG: one process per GPU, input sharded by record.
+"""Multi-GPU k-mer -> dBG -> rdBG -> region table: one process per GPU.
 
-Every rank builds the OR-table of its own records (K1 + K3), owner-partitions
-its entries (16-byte records: key+1, the 26-bit mask word of both
-orientations) and sends each run to its owner with one all-to-all (RCCL over
-xGMI; gloo in the CPU tests).  Owners OR-merge what they receive into a fresh
-table and run the degree scan (K5) on their partition only.  A k-mer's mask
-needs every occurrence, so this exchange is the path's one real collective;
-RCCL has no bitwise-OR reduction and slot layouts differ per GPU, so an
-all-reduce of "the count table" would not be exact — the all-to-all is
-(SURVEY.md §8e).
+SURVEY.md §8(e).  The reference runs seq2rdbg / dbg2rdbg / seq2graph
+(kmer_numba.py:1234-1268, :1313-1321, :1853-1951) in one process; here the
+input FASTA is sharded by bases across ranks at record boundaries, and the
+per-base work of every pass runs on each rank's own GPU over its own records:
 
-The orchestration takes a `table` object (the GPU Context, or a CPU stand-in
-in tests) with: partition(nparts) -> counts, partition(nparts, ptr, cap),
-merge(ptr, n, sentinel=...), build_rdbg() -> stats (n_dbg, n_rdbg).
+1. shard     every rank memory-maps the file and takes the byte range
+             [bounds[r], bounds[r+1]) (split just before a header line, so
+             each shard parses exactly as those records do in the whole file);
+             the record tables are all-gathered, and the pass plans (-n
+             limits, 2**33-base checkpoints, -r/-R resume) are computed over
+             the global record list exactly as host.plan_* does on one GPU.
+2. dBG       each rank builds the OR-table of its records (K1 + K3).
+3. dump      `<in>_db.npz` needs the occurrence counts of the whole input:
+             every rank counts its own records' occurrences per oriented key
+             (saturating at 255, so summing saturated counts and saturating
+             again is exact), rank 0 gathers them and places the union in the
+             reference's oakht slot layout (pg_dbg_load + pg_dbg_dump).
+4. rdBG      owner exchange: entries are owner-partitioned by key hash and
+             moved with one all-to-all (RCCL over xGMI); owners OR-merge and
+             apply the rdBG rule to their partition (exchange_and_reduce).
+             The owners' rdBG keys are all-gathered (C3: 1.9 M keys, 15 MB),
+             and every rank loads them as its walk membership table (the
+             `-D` path, :2093).
+5. edges     every rank walks its records (rdbg_edge_weight :1446-1518);
+             rank 0 gathers the edge lists in rank order — records are
+             contiguous per rank, so first-occurrence order across ranks is
+             rank order — and reduces them by edge (walk counts add, the first
+             occurrence wins), then applies the checkpoint reversals
+             (host.edge_order / host.merge_edges for -R).
+6. labels    rank 0 writes `.xyz`, runs `mcl` (or reuses `.mcl`) and builds
+             the label table (:1893-1944); it is broadcast to every rank.
+7. rows      every rank computes and formats its records' region rows
+             (seqs2path_jit_ :1830-1849); rank 0 gathers the text in rank
+             (= record) order and prints it.
+
+Collectives: one all-to-all (the only data-path exchange), all-gathers of the
+record tables and of the rdBG keys, point-to-point gathers to rank 0 of the
+dump counts, edges and row text, one broadcast of the label table.  RCCL has
+no bitwise-OR reduction and slot layouts differ per GPU, so an all-reduce of
+"the count table" would not be exact — the owner all-to-all is.
+
+The orchestration talks to a per-rank *shard backend* (GpuShard here; the CPU
+tests use an oracle-backed stand-in with the same methods):
+  load(data) -> records dict (seq_len, hdr_start, hdr_len, ptr), shard-relative
+  stage(keys, masks, counts)        stage npz slots into the next build (-r/-d/-D)
+  build(flags, extra, rc0) -> bool  the local dBG; returns the n<k sentinel flag
+  counts() -> (keys, masks, counts) oriented entries of the local build with
+                                    their occurrence counts
+  partition / merge / build_rdbg    the exchange (exchange_and_reduce)
+  owner_rdbg() -> keys              the owner partition's rdBG keys
+  members(keys, n_records, rc0)     the global rdBG as walk membership
+  edges(flags, rc1) -> (tuples, counts, walk)   first-occurrence order
+  rows_text(labels, flags, rc1, names) -> bytes
+  dump_global(keys, masks, counts) -> (capacity, size, keys, values, counts)
 """
 from __future__ import annotations
 
+import os
+import sys
+from time import time
+
 import numpy as np
+
+from . import host
+
+SENTINEL = 2 ** 64 - 1
 
 
 def _is_cuda(device) -> bool:
@@ -24,7 +73,8 @@ def _is_cuda(device) -> bool:
 
 
 def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bool, group=None):
-    """Returns (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent)."""
+    """Owner all-to-all + OR-merge + rdBG rule on the owner partition.
+    Returns (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent)."""
     import torch
     import torch.distributed as dist
 
@@ -57,3 +107,445 @@ def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bo
     sums = torch.tensor([st.n_dbg, st.n_rdbg], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
     return int(sums[0].item()), int(sums[1].item()), int(st.n_rdbg), 16 * (total - int(counts[rank]))
+
+
+# ------------------------------------------------------------------ sharding
+def _find_header_after(buf, pos: int, step: int = 1 << 22) -> int:
+    """Smallest p >= pos with buf[p] == '>' and buf[p-1] == '\\n' (a header
+    line start other than byte 0), or len(buf)."""
+    n = len(buf)
+    p = max(pos, 1)
+    while p < n:
+        a = np.asarray(buf[p - 1:min(n, p + step)])
+        hit = np.flatnonzero((a[:-1] == 10) & (a[1:] == 62))
+        if hit.shape[0]:
+            return p + int(hit[0])
+        p += step
+    return n
+
+
+def shard_bounds(buf, world: int) -> list:
+    """Byte bounds of the world shards of a FASTA: about len/world bytes each,
+    split just before a header line, so a shard starts in the line state
+    seqio_jit_ (:135-172) is in at that header in the whole file.  A split that
+    would leave the last shard without any '\\n' is not taken: readline_jit_'s
+    final unterminated line is yielded only when it does not start at byte 0
+    (`end > start > 0`, :130), which differs between a shard and the file."""
+    n = len(buf)
+    b = [0]
+    for r in range(1, world):
+        p = _find_header_after(buf, max(b[-1], r * n // world))
+        b.append(max(p, b[-1]))
+    b.append(n)
+    # the last non-empty shard must hold a newline unless it starts at byte 0
+    # (the shard before it then ends with the '\n' before its header)
+    s = max((x for x in b[1:world] if x < n), default=0)
+    if s > 0 and not np.any(np.asarray(buf[s:n]) == 10):
+        b = [x if j == 0 or x < s else n for j, x in enumerate(b)]
+    return b
+
+
+class Shards:
+    """The global record table assembled from every rank's shard-relative one."""
+
+    def __init__(self, metas: list, bounds: list, n_bytes: int):
+        self.bounds = bounds
+        self.R = [int(m["seq_len"].shape[0]) for m in metas]
+        self.off = np.concatenate([[0], np.cumsum(self.R)]).astype(np.int64)
+        cat = lambda k, add: np.concatenate([m[k].astype(np.int64) + (bounds[i] if add else 0)
+                                             for i, m in enumerate(metas)]) if metas else np.zeros(0, np.int64)
+        self.seq_len = cat("seq_len", False)
+        self.hdr_start = cat("hdr_start", True)
+        self.hdr_len = cat("hdr_len", False)
+        ptr = cat("ptr", True)
+        # a shard's last record is yielded, in the whole file, when seqio reads
+        # the next shard's first header line: its ptr is that line's start
+        for i in range(len(metas)):
+            if self.R[i] and bounds[i + 1] < n_bytes:
+                ptr[self.off[i + 1] - 1] = bounds[i + 1]
+        self.ptr = ptr
+
+    def local(self, arr, rank: int):
+        return arr[self.off[rank]:self.off[rank + 1]]
+
+
+# ------------------------------------------------------------- communication
+class Comm:
+    """The few collectives the pipeline needs, on torch.distributed (RCCL over
+    xGMI when the backend is nccl; gloo moves host tensors)."""
+
+    def __init__(self, device, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.dev = torch.device("cpu") if dist.get_backend(group) == "gloo" else device
+
+    def allgather_obj(self, obj):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj, group=self.group)
+        return out
+
+    def _sizes(self, n: int):
+        t = self.torch.tensor([n], dtype=self.torch.int64, device=self.dev)
+        out = [self.torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return [int(x.item()) for x in out]
+
+    def gather_bytes(self, payload: np.ndarray, dst: int = 0):
+        """Variable-size uint8 payloads to rank dst (point to point), in rank order."""
+        torch = self.torch
+        payload = np.ascontiguousarray(payload, dtype=np.uint8).reshape(-1)
+        sizes = self._sizes(payload.shape[0])
+        if self.rank != dst:
+            if payload.shape[0]:
+                self.dist.send(torch.from_numpy(payload).to(self.dev), dst, group=self.group)
+            return None
+        out = []
+        for r in range(self.world):
+            if r == dst:
+                out.append(payload)
+            elif sizes[r]:
+                t = torch.empty(sizes[r], dtype=torch.uint8, device=self.dev)
+                self.dist.recv(t, r, group=self.group)
+                out.append(t.cpu().numpy())
+            else:
+                out.append(np.zeros(0, np.uint8))
+        return out
+
+    def allgather_bytes(self, payload: np.ndarray):
+        torch = self.torch
+        payload = np.ascontiguousarray(payload, dtype=np.uint8).reshape(-1)
+        sizes = self._sizes(payload.shape[0])
+        m = max(max(sizes), 1)
+        t = torch.zeros(m, dtype=torch.uint8, device=self.dev)
+        if payload.shape[0]:
+            t[:payload.shape[0]] = torch.from_numpy(payload).to(self.dev)
+        out = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(out, t, group=self.group)
+        return [o[:s].cpu().numpy() for o, s in zip(out, sizes)]
+
+    def bcast_bytes(self, payload, src: int = 0) -> np.ndarray:
+        torch = self.torch
+        n = self.torch.tensor([payload.shape[0] if self.rank == src else 0], dtype=torch.int64, device=self.dev)
+        self.dist.broadcast(n, src, group=self.group)
+        t = torch.empty(int(n.item()), dtype=torch.uint8, device=self.dev)
+        if self.rank == src and payload.shape[0]:
+            t.copy_(torch.from_numpy(np.ascontiguousarray(payload, dtype=np.uint8)).to(self.dev))
+        if t.numel():
+            self.dist.broadcast(t, src, group=self.group)
+        return t.cpu().numpy()
+
+    def barrier(self):
+        self.dist.barrier(group=self.group)
+
+
+def _pack(*arrs) -> np.ndarray:
+    """Arrays of 8-byte elements -> one uint8 payload (a header of lengths)."""
+    hdr = np.array([len(arrs)] + [a.shape[0] if a.ndim == 1 else a.size for a in arrs], np.int64)
+    return np.concatenate([hdr.view(np.uint8)] + [np.ascontiguousarray(a).reshape(-1).view(np.uint8)
+                                                  for a in arrs])
+
+
+def _unpack(buf: np.ndarray, dtypes):
+    hdr = buf[:8].view(np.int64)
+    k = int(hdr[0])
+    lens = buf[8:8 * (k + 1)].view(np.int64)
+    out, o = [], 8 * (k + 1)
+    for n, dt in zip(lens.tolist(), dtypes):
+        nb = n * np.dtype(dt).itemsize
+        out.append(buf[o:o + nb].view(dt))
+        o += nb
+    return out
+
+
+# ------------------------------------------------------------ shard backend
+class GpuShard:
+    """This rank's records on its GPU (a pg_ctx through the C ABI)."""
+
+    def __init__(self, k: int, device: int):
+        from ._lib import Context
+        self.ctx = Context(k, device)
+
+    def load(self, data):
+        self.ctx.set_fasta(data)
+        self.ctx.parse()
+        return self.ctx.records()
+
+    def stage(self, keys, masks=None, counts=None):
+        self.ctx.dbg_load(keys, masks, counts)
+
+    def build(self, flags, extra, rc0):
+        return bool(self.ctx.build_dbg(flags, int(extra), bool(rc0)).sentinel)
+
+    def counts(self):
+        _, _, keys, values, counts = self.ctx.dbg_dump()
+        sel = counts > 0
+        return keys[sel], values[sel], counts[sel]
+
+    # the exchange (exchange_and_reduce)
+    def partition(self, nparts, ptr=None, cap=0):
+        return self.ctx.partition(nparts, ptr, cap)
+
+    def merge(self, ptr, n, sentinel=False):
+        self.ctx.merge(ptr, n, 0, sentinel)
+
+    def build_rdbg(self):
+        return self.ctx.build_rdbg()
+
+    def owner_rdbg(self):
+        return self.ctx.rdbg()
+
+    def members(self, keys, n_records, rc0):
+        self.ctx.dbg_load(keys, None, None)
+        self.ctx.build_dbg(np.zeros(n_records, np.uint8), 0, bool(rc0))
+        self.ctx.build_rdbg()
+
+    def edges(self, flags, rc1):
+        return self.ctx.edges(flags, bool(rc1))
+
+    def rows_text(self, labels, flags, rc1, names):
+        from ._lib import format_rows
+        self.ctx.set_labels(*labels)
+        return format_rows(self.ctx.rows(flags, bool(rc1)), names)
+
+    def dump_global(self, keys, masks, counts, k, device):
+        from ._lib import Context
+        d = Context(k, device)
+        try:
+            d.set_fasta(np.zeros(0, np.uint8))
+            d.parse()
+            d.dbg_load(keys, masks, counts)
+            d.build_dbg(np.zeros(0, np.uint8), 0, True)
+            return d.dbg_dump()
+        finally:
+            d.close()
+
+
+# ------------------------------------------------------------------ pipeline
+class DistRun:
+    """The CLI stages of entry_point (:2073-2146) over world shards."""
+
+    def __init__(self, qry: str, k: int, shard, comm: Comm, device=None, out=None, dev_index: int = 0,
+                 edge_chunk: int = host.CHUNK):
+        self.qry, self.k, self.sh, self.comm = qry, min(max(1, int(k)), 27), shard, comm
+        self.edge_chunk = int(edge_chunk)                  # seq2graph's checkpoint size (:2073; tests vary it)
+        self.device, self.dev_index = device, dev_index
+        self.rank, self.world = comm.rank, comm.world
+        self.out = out or sys.stdout
+        self.buf = np.memmap(qry, mode="r", dtype=np.uint8) if os.path.getsize(qry) else np.zeros(0, np.uint8)
+        self.bounds = shard_bounds(self.buf, self.world)
+        lo, hi = self.bounds[self.rank], self.bounds[self.rank + 1]
+        self.data = np.ascontiguousarray(self.buf[lo:hi])
+        meta = self.sh.load(self.data)
+        metas = comm.allgather_obj({k_: np.asarray(v, np.int64) for k_, v in meta.items()})
+        self.S = Shards(metas, self.bounds, len(self.buf))
+        self.R_local = self.S.R[self.rank]
+        self.shape = host.FileShape.from_bytes(self.buf, self.S.hdr_start, self.S.hdr_len)
+
+    def say(self, *a):
+        if self.rank == 0:
+            print(*a, file=self.out)
+
+    def names(self):
+        hs, hl = self.S.local(self.S.hdr_start, self.rank), self.S.local(self.S.hdr_len, self.rank)
+        lo = self.bounds[self.rank]
+        return [bytes(self.data[int(s) - lo + 1:int(s) - lo + int(n)]) for s, n in zip(hs, hl)]
+
+    # ---------------------------------------------------------------- dBG
+    def build_dbg(self, Ns, rc0, brkpt=""):
+        """seq2rdbg (:1234-1268) over the shards; -r stages the checkpoint on rank 0."""
+        resume = None
+        if brkpt and os.path.isfile(brkpt):
+            offset, keys, values, counts = host.read_db_npz(brkpt)
+            if self.rank == 0:
+                self.sh.stage(keys, values, counts)
+            resume = host.resume_position(offset, self.S.ptr)
+        flags, extra = host.plan_dbg(self.S.seq_len, self.shape, bool(rc0), int(Ns), host.CHUNK, resume=resume)
+        self.sentinel = self.sh.build(self.S.local(flags, self.rank), extra if self.rank == 0 else 0, rc0)
+
+    def load_dbg(self, fn, rdbg: bool, rc0):
+        """load_on_disk (:289-335) of a -d / -D file: staged on rank 0 (-d: the
+        exchange sends every entry to its owner) or, for -D, on every rank as
+        the membership table itself."""
+        _, keys, values, counts = host.read_db_npz(fn)
+        zeros = np.zeros(self.R_local, np.uint8)
+        if rdbg:
+            self.sh.members(keys, self.R_local, rc0)
+            self.reduced = True
+            return
+        if self.rank == 0:
+            self.sh.stage(keys, values, counts)
+        self.sentinel = self.sh.build(zeros, 0, rc0)
+
+    def dump(self, fn):
+        """dump() (:243-261) of the global dBG, written by rank 0."""
+        keys, masks, counts = self.sh.counts()
+        parts = self.comm.gather_bytes(_pack(keys.astype(np.uint64), masks.astype(np.uint16).astype(np.int64),
+                                             counts.astype(np.int64)))
+        if self.rank == 0:
+            ks, ms, cs = [], [], []
+            for p in parts:
+                k_, m_, c_ = _unpack(p, (np.uint64, np.int64, np.int64))
+                ks.append(k_); ms.append(m_); cs.append(c_)
+            cap, size, K, V, C = self.sh.dump_global(np.concatenate(ks), np.concatenate(ms).astype(np.uint16),
+                                                     np.minimum(np.concatenate(cs), 255).astype(np.uint8),
+                                                     self.k, self.dev_index)
+            host.write_db_npz(fn, cap, size, K, V, C)
+        self.comm.barrier()
+
+    # --------------------------------------------------------------- rdBG
+    def reduce(self, rc0):
+        """dbg2rdbg (:1313-1321): owner exchange, then every rank's walk
+        membership = the union of the owners' rdBG keys."""
+        if getattr(self, "reduced", False):
+            return
+        n_dbg, n_rdbg, _, _ = exchange_and_reduce(self.sh, self.world, self.rank, self.device, self.sentinel,
+                                                  self.comm.group)
+        own = np.ascontiguousarray(self.sh.owner_rdbg(), dtype=np.uint64)
+        allk = np.sort(np.concatenate([p.view(np.uint64) for p in self.comm.allgather_bytes(own.view(np.uint8))]))
+        if allk.shape[0] != n_rdbg:
+            raise RuntimeError("rdBG all-gather: %d keys, owners reported %d" % (allk.shape[0], n_rdbg))
+        self.n_dbg, self.n_rdbg = n_dbg, n_rdbg
+        self.sh.members(allk, self.R_local, rc0)
+        self.reduced = True
+
+    # -------------------------------------------------------------- graph
+    def graph(self, Ns, rc1, brkpt="", cluster=True):
+        """seq2graph (:1853-1951) over the shards."""
+        loaded, resume = None, None
+        if brkpt and os.path.isfile(brkpt):
+            offset, lt, lc = host.read_edge_npz(brkpt)
+            loaded, resume = (lt, lc), host.resume_position(offset, self.S.ptr)
+        eflags, segment, ncp = host.plan_edges(self.S.seq_len, self.shape, int(Ns), self.edge_chunk, resume=resume)
+        t, c, w = self.sh.edges(self.S.local(eflags, self.rank), rc1)
+        w = np.asarray(w, np.int64) + 2 * int(self.S.off[self.rank])
+        parts = self.comm.gather_bytes(_pack(np.ascontiguousarray(t, np.uint64), np.asarray(c, np.int64), w))
+        oname = self.qry + "_rdbg_weight.xyz"
+        payload = np.zeros(0, np.uint8)
+        if self.rank == 0:
+            tuples, counts, walk = reduce_edges([_unpack(p, (np.uint64, np.int64, np.int64)) for p in parts])
+            if loaded is not None:
+                tuples, counts = host.merge_edges(loaded[0], loaded[1], tuples, counts, walk, segment, ncp)
+            else:
+                o = host.edge_order(walk, segment, ncp)
+                tuples, counts = tuples[o], counts[o]
+            from ._lib import format_xyz
+            with open(oname, "wb") as f:                       # :1893-1904
+                f.write(format_xyz(tuples, counts))
+            if cluster:
+                if os.path.isfile("%s.mcl" % oname):
+                    self.say("# the mcl has been ran")
+                else:
+                    self.out.flush()
+                    os.system("mcl %s --abc -I 1.5 -te 8 -o %s.mcl -q x -V all" % (oname, oname))
+            with open(oname + ".mcl", "r") as f:
+                mcl_text = f.read()
+            keys, vals, ids = host.label_table(mcl_text, tuples)      # :1918-1944
+            payload = _pack(keys, vals, ids)
+        keys, vals, ids = _unpack(self.comm.bcast_bytes(payload), (np.int64, np.int64, np.int64))
+        rflags = host.plan_rows(self.S.seq_len, self.shape, self.buf, int(Ns))
+        text = self.sh.rows_text((keys, vals, ids), self.S.local(rflags, self.rank), rc1, self.names())
+        parts = self.comm.gather_bytes(np.frombuffer(text, np.uint8) if text else np.zeros(0, np.uint8))
+        if self.rank == 0:
+            body = b"".join(p.tobytes() for p in parts)
+            if body:
+                if hasattr(self.out, "buffer"):
+                    self.out.flush()
+                    self.out.buffer.write(body)
+                    self.out.buffer.flush()
+                else:
+                    self.out.write(body.decode())
+        self.comm.barrier()
+
+
+def reduce_edges(parts):
+    """Edge lists of the ranks (each in its own first-occurrence order, ranks
+    in record order) -> one list in global first-occurrence order: walk counts
+    add, the first occurrence's walk index is kept (rdbg_edge_weight :1476-1484
+    per walk, the typed Dict's insertion order across walks)."""
+    t = np.concatenate([p[0].reshape(-1, 4) for p in parts]) if parts else np.zeros((0, 4), np.uint64)
+    c = np.concatenate([p[1] for p in parts]) if parts else np.zeros(0, np.int64)
+    w = np.concatenate([p[2] for p in parts]) if parts else np.zeros(0, np.int64)
+    if t.shape[0] == 0:
+        return t, c, w
+    v = np.ascontiguousarray(t).view(np.dtype((np.void, 32))).ravel()
+    _, first, inv = np.unique(v, return_index=True, return_inverse=True)
+    tot = np.zeros(first.shape[0], np.int64)
+    np.add.at(tot, inv.ravel(), c)
+    o = np.argsort(first, kind="stable")
+    return t[first[o]], tot[o], w[first[o]]
+
+
+def entry_point(argv, out=None, shard_factory=None, device=None, dev_index: int = 0, edge_chunk: int = host.CHUNK):
+    """kmer.entry_point (:1971-2146) on every rank of an initialised process
+    group; rank 0 prints.  `shard_factory(k)` makes the rank's backend
+    (default: GpuShard on dev_index)."""
+    import torch.distributed as dist
+    from .kmer import manual_print, parse_args
+    out = out or sys.stdout
+    args = parse_args(argv)
+    qry, kmer, Ns = args["-i"], int(args["-k"]), host.eval_number(args["-n"])
+    bkt, dbs, rbk, rc, rdb = args["-r"], args["-d"], args["-R"], int(args["-c"]), args["-D"]
+    if not qry:
+        if dist.get_rank() == 0:
+            manual_print(out)
+        raise SystemExit()
+    rc0, rc1 = (rc >> 1) == 1, (rc & 1) == 1
+    k = min(max(1, kmer), 27)
+    shard = shard_factory(k) if shard_factory else GpuShard(k, dev_index)
+    comm = Comm(device)
+    run = DistRun(qry, k, shard, comm, device=device, out=out, dev_index=dev_index, edge_chunk=edge_chunk)
+    if dbs or rdb:                                      # :2073-2101
+        if not rdb:
+            run.say("load dBG from disk")
+            run.load_dbg(dbs, False, rc0)
+            run.say("# build the reduced dBG")
+            run.reduce(rc0)
+        else:
+            run.load_dbg(rdb, True, rc0)
+        run.say("# find fr")
+        run.graph(Ns, rc1, brkpt=rbk)
+        return 0
+    run.say("# build the dBG")
+    st = time()
+    run.build_dbg(Ns, rc0, brkpt=bkt)
+    run.say("# finished in", time() - st, "seconds")
+    run.say("# save dBG to disk")
+    st = time()
+    run.dump(qry + "_db")
+    run.say("# finished in", time() - st, "seconds")
+    run.say("# load dBG from disk")
+    st = time()
+    run.say("# finished in", time() - st, "seconds")
+    run.say("# build the reduced dBG")
+    st = time()
+    run.reduce(rc0)
+    run.say("# finished in", time() - st, "seconds")
+    run.say("# find fr")
+    st = time()
+    run.graph(Ns, rc1, brkpt=rbk)
+    run.say("# finished in", time() - st, "seconds")
+    return 0
+
+
+def main():
+    """`python -m torch.distributed.run --nproc-per-node N -m pangenome_amd -i in.fa -k 27`:
+    one rank per GPU over RCCL.  PG_DIST_BACKEND=gloo with PG_DIST_ONE_GPU=1
+    puts every rank on cuda:0 (tests on a one-GPU box)."""
+    import torch
+    import torch.distributed as dist
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("PG_DIST_BACKEND", "nccl")
+    dev_index = 0 if os.environ.get("PG_DIST_ONE_GPU") == "1" else local
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=device)
+    else:
+        dist.init_process_group(backend)
+    try:
+        return entry_point(sys.argv, device=device, dev_index=dev_index)
+    finally:
+        dist.destroy_process_group()

@@ -6,7 +6,6 @@ the oracle, in the same 16-byte canonical record format the GPU exchanges
 the GPU table's partition / merge / degree scan.  The sharded totals must equal
 the single-process build over all records.
 """
-import ctypes
 import os
 import socket
 
@@ -14,85 +13,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PRES_A, B_SHIFT = 1 << 12, 13
-
-
-def rc_key_np(x: np.ndarray, k: int) -> np.ndarray:
-    x = x.astype(np.uint64).copy()
-    r = np.zeros_like(x)
-    for _ in range(k):
-        d = x % np.uint64(5)
-        x //= np.uint64(5)
-        rd = np.where(d < 4, np.uint64(3) - d, np.uint64(4))
-        r = r * np.uint64(5) + rd
-    return r
-
-
-def popcount6(m):
-    return np.array([bin(i).count("1") for i in range(64)])[m & 63]
-
-
-class NumpyTable:
-    """CPU stand-in for the GPU table (test infrastructure)."""
-
-    def __init__(self, k):
-        self.k = k
-        self.c = np.zeros(0, np.uint64)
-        self.mw = np.zeros(0, np.uint64)
-
-    def load_dbg(self, keys, masks):
-        keys = keys.astype(np.uint64)
-        sent = keys == np.uint64(2 ** 64 - 1)
-        self.sentinel = bool(sent.any())
-        keys, masks = keys[~sent], masks[~sent].astype(np.uint64)
-        rc = rc_key_np(keys, self.k)
-        c = np.minimum(keys, rc)
-        word = np.where(keys == c, masks | PRES_A, (masks | PRES_A) << np.uint64(B_SHIFT))
-        self._set(c, word)
-
-    def _set(self, c, word):
-        order = np.argsort(c, kind="stable")
-        c, word = c[order], word[order]
-        uniq, start = np.unique(c, return_index=True)
-        self.c, self.mw = uniq, np.bitwise_or.reduceat(word, start) if c.size else word
-
-    def _owner(self, nparts):
-        z = self.c * np.uint64(0x9E3779B97F4A7C15)
-        return ((z >> np.uint64(40)) % np.uint64(nparts)).astype(np.int64)
-
-    def partition(self, nparts, ptr=None, cap=0):
-        own = self._owner(nparts)
-        counts = np.bincount(own, minlength=nparts).astype(np.uint64)
-        if ptr is not None:
-            buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * cap)).from_address(ptr)).reshape(cap, 2)
-            order = np.argsort(own, kind="stable")
-            buf[:, 0] = (self.c[order] + np.uint64(1)).view(np.int64)
-            buf[:, 1] = self.mw[order].view(np.int64)
-        return counts
-
-    def merge(self, ptr, n, sentinel=False):
-        if n:
-            buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * n)).from_address(ptr)).reshape(n, 2)
-            self._set(buf[:, 0].view(np.uint64) - np.uint64(1), buf[:, 1].view(np.uint64))
-        else:
-            self.c, self.mw = np.zeros(0, np.uint64), np.zeros(0, np.uint64)
-        self.sentinel = sentinel
-
-    def build_rdbg(self):
-        a = (self.mw & np.uint64(0xFFF)).astype(np.int64)
-        b = ((self.mw >> np.uint64(B_SHIFT)) & np.uint64(0xFFF)).astype(np.int64)
-        pa = (self.mw & np.uint64(PRES_A)) != 0
-        pb = (self.mw & np.uint64(PRES_A << B_SHIFT)) != 0
-        ma = pa & ~((popcount6(a >> 6) == 1) & (popcount6(a) == 1))
-        mb = pb & ~((popcount6(b >> 6) == 1) & (popcount6(b) == 1))
-
-        class St:
-            pass
-        st = St()
-        st.n_dbg = int(pa.sum() + pb.sum()) + int(self.sentinel)
-        st.n_rdbg = int(ma.sum() + mb.sum()) + int(self.sentinel)
-        return st
+from dist_util import ROOT, NumpyTable
 
 
 def _records(fasta: bytes):
@@ -103,6 +24,7 @@ def _records(fasta: bytes):
 def _worker(rank, world, port, fasta, k, q):
     import sys
     sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
     from oracle import oracle
     from pangenome_amd.dist import exchange_and_reduce

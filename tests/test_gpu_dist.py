@@ -1,20 +1,29 @@
-"""The multi-GPU path's kernels (pg_dbg_partition / pg_dbg_merge / K5 on the
-owner partition) with 2 ranks sharing one MI355X; the collective is gloo with
-host staging (RCCL needs one GPU per rank; the bench uses it).  The union of
-the owners' rdBG keys must equal the single-process build exactly."""
+"""The multi-GPU path (pangenome_amd/dist.py) through the HIP library, with
+2-3 ranks sharing one MI355X; the collectives run on gloo with host staging
+(RCCL needs one GPU per rank — the 8-GPU bench uses it).
+
+* the exchange kernels (pg_dbg_partition / pg_dbg_merge / the rdBG rule on the
+  owner partition) against the C oracle's dBG / rdBG of the whole input;
+* the whole CLI (`python -m torch.distributed.run ... -m pangenome_amd`) against
+  what the reference itself produced (tests/golden): `.xyz` in edge order,
+  region rows, the `<in>_db.npz` dump, with -n limits, checkpoint chunks,
+  -r / -R resumes from the reference's own checkpoints, -d and -D reloads, and
+  a rank whose shard holds no record.
+"""
+import io
 import os
-import socket
+import sys
 
 import numpy as np
 import pytest
-import torch.multiprocessing as mp
+
+from dist_util import ROOT, spawn_ranks
+from golden_util import Fixture, ResumeFixture
 
 pytestmark = pytest.mark.gpu
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _worker(rank, world, port, shard, q):
-    import sys
+def _exchange_rank(rank, world, port, q, shard):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -22,46 +31,148 @@ def _worker(rank, world, port, shard, q):
     from pangenome_amd.dist import exchange_and_reduce
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    dev = torch.device("cuda", 0)
     ctx = Context(27, 0)
     ctx.set_fasta(shard)
     ctx.parse()
     st = ctx.build_dbg(None, 0, True)
-    res = exchange_and_reduce(ctx, world, rank, dev, bool(st.sentinel))
-    q.put((rank, res, ctx.rdbg()))
+    res = exchange_and_reduce(ctx, world, rank, torch.device("cuda", 0), bool(st.sentinel))
+    q.put((rank, (res, ctx.rdbg())))
     dist.destroy_process_group()
 
 
-def test_two_rank_exchange_on_one_gpu():
+def test_two_rank_exchange_vs_oracle(oracle_mod):
     from pangenome_amd import synth
-    from pangenome_amd._lib import Context
     fasta = synth.pangenome(8, 200_000, snp=0.005, indel=5e-4, seed=99)
     recs = [b">" + r for r in fasta.split(b">")[1:]]
     shards = [b"".join(recs[0::2]), b"".join(recs[1::2]) + b">short\nACGTA\n"]
-    whole = shards[0] + shards[1]
-    ctx = Context(27, 0)
-    ctx.set_fasta(whole)
-    ctx.parse()
-    ctx.build_dbg(None, 0, True)
-    st = ctx.build_rdbg()
-    ref_keys = ctx.rdbg()
-    ctx.close()
-
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    mpc = mp.get_context("spawn")
-    q = mpc.Queue()
-    procs = [mpc.Process(target=_worker, args=(r, 2, port, shards[r], q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    out = dict((r, (res, keys)) for r, res, keys in (q.get(timeout=300) for _ in range(2)))
-    for p in procs:
-        p.join(timeout=120)
-        assert p.exitcode == 0
+    ref = oracle_mod.OracleRun(shards[0] + shards[1], 27, 2)
+    ref_dbg, ref_rdbg = ref.dbg()[0].shape[0], ref.rdbg()
+    res = spawn_ranks(2, _exchange_rank_sharded, (shards,))
     for r in range(2):
-        n_dbg, n_rdbg, _, _ = out[r][0]
-        assert n_dbg == st.n_dbg and n_rdbg == st.n_rdbg
-    union = np.sort(np.concatenate([out[0][1], out[1][1]]))
-    assert np.array_equal(union, ref_keys)
+        n_dbg, n_rdbg, _, _ = res[r][0]
+        assert n_dbg == ref_dbg and n_rdbg == ref_rdbg.shape[0]
+    union = np.sort(np.concatenate([res[0][1], res[1][1]]))
+    assert np.array_equal(union, ref_rdbg)
+
+
+def _exchange_rank_sharded(rank, world, port, q, shards):
+    _exchange_rank(rank, world, port, q, shards[rank])
+
+
+def _cli_rank(rank, world, port, q, argv, chunk, cwd):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from pangenome_amd import dist as pdist
+    os.chdir(cwd)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = io.StringIO()
+    try:
+        pdist.entry_point(argv, out=out, device=torch.device("cuda", 0), dev_index=0, edge_chunk=chunk)
+    finally:
+        dist.destroy_process_group()
+    q.put((rank, out.getvalue()))
+
+
+def rows_of(text):
+    return [ln for ln in text.split("\n") if len(ln.split("\t")) == 5 and ln.split("\t")[3] in ("+", "-")]
+
+
+def _run(tmp_path, world, argv, chunk=2 ** 33):
+    outs = spawn_ranks(world, _cli_rank, (argv, chunk, str(tmp_path)))
+    assert all(rows_of(outs[r]) == [] for r in range(1, world))
+    return outs[0]
+
+
+def _check_dump(path, dbg_keys, dbg_masks, dbg_counts, params=None):
+    z = np.load(path)
+    sel = z["counts"] > 0
+    o = np.argsort(z["keys"][sel], kind="stable")
+    assert np.array_equal(z["keys"][sel][o], dbg_keys)
+    assert np.array_equal(z["values"][sel][o], dbg_masks)
+    assert np.array_equal(z["counts"][sel][o], dbg_counts)
+    if params is not None:
+        assert z["parameters"].tolist() == params.tolist()
+
+
+@pytest.mark.parametrize("name,world", [("pan8_k27_c3", 2), ("pan8_k27_n", 3), ("pan8_k27_chunk", 2),
+                                        ("edge_k27", 3), ("pan8_k27_mcl", 2)])
+def test_dist_cli_vs_reference(name, world, tmp_path):
+    fx = Fixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text(fx.mcl)
+    argv = ["kmer_numba.py", "-i", str(q), "-k", str(fx.k), "-c", str(fx.c)]
+    if fx.ns is not None:
+        argv += ["-n", str(fx.meta["n"])]
+    text = _run(tmp_path, world, argv, fx.edge_chunk)
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
+    assert rows_of(text) == fx.rows
+    _check_dump(str(q) + "_db.npz", fx.dbg_keys, fx.dbg_masks, fx.dbg_counts, fx.db_params)
+
+
+def test_dist_cli_reload_d_and_D(tmp_path):
+    """-d reloads the dump the distributed run wrote; -D an rdBG key file."""
+    from dist_util import oak_place
+    from pangenome_amd import host
+    fx = Fixture("pan8_k27_c3")
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    base = ["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "3"]
+    assert rows_of(_run(tmp_path, 2, base)) == fx.rows
+    text = _run(tmp_path, 2, base + ["-d", str(q) + "_db.npz"])
+    assert "load dBG from disk" in text.split("\n") and rows_of(text) == fx.rows
+    keys = fx.rdbg_keys
+    M = 1048583
+    kk, vv, cc = oak_place(keys, np.full(keys.shape[0], 7, np.uint16), np.ones(keys.shape[0], np.uint8), M)
+    host.write_db_npz(str(tmp_path / "rdbg"), M, keys.shape[0], kk, vv, cc)
+    assert rows_of(_run(tmp_path, 3, base + ["-D", str(tmp_path / "rdbg.npz")])) == fx.rows
+
+
+@pytest.mark.parametrize("name", __import__("golden_util").resume_names())
+def test_dist_cli_resumes_reference_checkpoint(name, tmp_path):
+    fx = ResumeFixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    text = _run(tmp_path, 2, ["kmer_numba.py", "-i", str(q), "-k", str(fx.k), "-c", str(fx.c), fx.flag, fx.brkpt])
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
+    assert rows_of(text) == fx.rows
+    if fx.graph is not None:
+        _check_dump(str(q) + "_db.npz", fx.graph["dbg_keys"], fx.graph["dbg_masks"], fx.graph["dbg_counts"])
+
+
+def test_dist_cli_empty_shard_vs_oracle(oracle_mod, tmp_path):
+    """Two records over three ranks: one rank's shard is empty."""
+    from oracle import oracle
+    from pangenome_amd import synth
+    fasta = synth.pangenome(2, 5000, snp=0.01, seed=3)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    text = _run(tmp_path, 3, ["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "3"])
+    ref = oracle.run_pipeline(fasta, 27, 3)
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == ref["xyz"]
+    assert rows_of(text) == ref["rows"]
+
+
+def test_torchrun_launch(tmp_path):
+    """The launch line itself: `python -m torch.distributed.run --nproc-per-node 2
+    -m pangenome_amd ...` (gloo, both ranks on cuda:0 for this one-GPU box)."""
+    import subprocess
+    fx = Fixture("pan8_k27_c2")
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    from dist_util import free_port
+    env = dict(os.environ, PG_DIST_BACKEND="gloo", PG_DIST_ONE_GPU="1", PYTHONPATH=ROOT)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           "-m", "pangenome_amd", "-i", str(q), "-k", "27", "-c", "2"]
+    p = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert rows_of(p.stdout) == fx.rows
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz

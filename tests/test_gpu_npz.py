@@ -13,43 +13,10 @@ import os
 import numpy as np
 import pytest
 
+from dist_util import oak_place, oak_slot
 from golden_util import Fixture, fixture_names
 
 pytestmark = pytest.mark.gpu
-M64 = (1 << 64) - 1
-
-
-def oak_fnv(x):
-    a = 0xCBF29CE484222325
-    for i in range(4):
-        a ^= (x >> (8 * i)) & 0xFF
-        a = (a * 0x100000001B3) & M64
-    return a
-
-
-def oak_slot(keys, counts, x):
-    """oakht.pointer (:521-538): j, j, j+1, j+4, ... until the key or an empty slot."""
-    M = keys.shape[0]
-    j0 = oak_fnv(x) % M
-    j = j0
-    for k in range(M):
-        if int(keys[j]) == x or counts[j] == 0:
-            break
-        j = (j0 + k * k) % M
-    return j
-
-
-def oak_place(keys_in, vals_in, cnts_in, M):
-    """A valid oakht layout built the way __setitem__ does (test helper)."""
-    keys = np.zeros(M, np.uint64)
-    vals = np.zeros(M, np.uint16)
-    cnts = np.zeros(M, np.uint8)
-    for x, v, c in zip(keys_in.tolist(), vals_in.tolist(), cnts_in.tolist()):
-        j = oak_slot(keys, cnts, x)
-        keys[j], vals[j], cnts[j] = x, v, c
-    return keys, vals, cnts
-
-
 def rows_of(text):
     return [ln for ln in text.split("\n") if len(ln.split("\t")) == 5 and ln.split("\t")[3] in ("+", "-")]
 

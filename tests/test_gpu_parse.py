@@ -11,33 +11,9 @@ headers longer than the kernel's 16 KiB wave span, and random byte soup.
 import numpy as np
 import pytest
 
+from dist_util import seqio_records
+
 pytestmark = pytest.mark.gpu
-
-
-def seqio_records(buf: bytes):
-    """readline_jit_ (:122-132) + seqio_jit_ (:135-172), isfasta, offset 0."""
-    a = np.frombuffer(buf, dtype=np.uint8)
-    n = a.shape[0]
-    nl = np.flatnonzero(a == 10)
-    starts = np.concatenate([[0], nl + 1])[: nl.shape[0]]
-    ends = nl + 1
-    if n and nl.shape[0]:
-        st = int(nl[-1]) + 1
-        if n - 1 > st > 0:                                   # end > start > 0
-            starts = np.append(starts, st)
-            ends = np.append(ends, n)
-    recs = []                                                # (seq_len, hdr_start, hdr_len, ptr)
-    cur = None
-    for st, ed in zip(starts.tolist(), ends.tolist()):
-        if a[st] == 62:
-            if cur is not None:
-                recs.append((cur[0], cur[1], cur[2], st))
-            cur = [0, st, ed - 1 - st]
-        elif cur is not None:
-            cur[0] += ed - st - 1
-    if cur is not None:
-        recs.append((cur[0], cur[1], cur[2], int(starts[-1])))
-    return recs
 
 
 CASES = {
