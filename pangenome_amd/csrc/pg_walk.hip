@@ -563,7 +563,10 @@ uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1) {
     cnt.release();
   }
   unsigned e = 0;
-  PG_HIP(hipMemcpy(&e, err.p, 4, hipMemcpyDeviceToHost));
+  // (c.stream is non-blocking: a null-stream hipMemcpy would not wait for the
+  // memset above when m <= 1 queued nothing that synced)
+  PG_HIP(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
   err.release();
   if (e) throw Error(-5, "pg_edges: edge table error " + std::to_string(e));
   c.n_edges = n_out;
@@ -573,7 +576,10 @@ uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1) {
 void export_edges(Ctx& c, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap) {
   const uint64_t n = std::min<uint64_t>(cap, c.n_edges);
   std::vector<EdgeOut> h(n);
-  if (n) PG_HIP(hipMemcpy(h.data(), c.edge_out.p, sizeof(EdgeOut) * n, hipMemcpyDeviceToHost));
+  if (n) {
+    PG_HIP(hipMemcpyAsync(h.data(), c.edge_out.p, sizeof(EdgeOut) * n, hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+  }
   // order by first occurrence (typed-Dict insertion order, :1479-1484)
   std::vector<uint64_t> idx(n);
   for (uint64_t i = 0; i < n; ++i) idx[i] = i;

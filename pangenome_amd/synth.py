@@ -122,7 +122,34 @@ CONFIGS = {
     "c3": dict(kind="pan", n_genomes=100, genome_len=5_000_000, snp=1e-3, indel=1e-4),
     # C4: 1000 x 5 Mbp (5 Gbp), sharded 125 genomes per GPU at 8 GPUs.
     "c4": dict(kind="pan", n_genomes=1000, genome_len=5_000_000, snp=1e-3, indel=1e-4),
+    # C5: 10 x 3 Gbp variants, 1% SNP, 0.1% indels, each genome split into 24
+    # records of 125 Mbp (30 Gbp, 240 records): generated record by record
+    # (c5_record / write_c5), never held whole.
+    "c5": dict(kind="pan_records", n_genomes=10, records=24, record_len=125_000_000, snp=1e-2, indel=1e-3),
 }
+
+
+def c5_record(genome: int, record: int, record_len: int = 125_000_000, snp: float = 1e-2,
+              indel: float = 1e-3, seed: int = DEFAULT_SEED) -> bytes:
+    """Record `record` of genome `genome` of C5: a variant of base segment
+    `record` (each 125 Mbp segment of the 3 Gbp base genome has its own
+    splitmix64 stream, so any record is generated alone in ~1 GB of memory)."""
+    base = base_genome(record_len, seed ^ (0xC5 << 40) ^ (record * 0x100000001B3))
+    v = variant(base, genome, snp, indel, seed ^ (0xC5C5 << 32) ^ record)
+    return to_fasta_lines(b"g%d_c%d" % (genome, record), v)
+
+
+def write_c5(path: str, n_genomes: int = 10, records: int = 24, record_len: int = 125_000_000,
+             genomes=None) -> int:
+    """Stream C5 (or the genomes listed) to `path`; returns the bytes written."""
+    n = 0
+    with open(path, "wb") as f:
+        for g in (range(n_genomes) if genomes is None else genomes):
+            for r in range(records):
+                b = c5_record(g, r, record_len)
+                f.write(b)
+                n += len(b)
+    return n
 
 
 def ecoli_like(length: int = 4_641_652, seed: int = DEFAULT_SEED, repeats: int = 7,
