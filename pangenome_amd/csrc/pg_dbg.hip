@@ -234,90 +234,95 @@ struct WorkItem {
 constexpr int NQ = 64;
 constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long long words)
 
-// find_drift for k_cover's two references at once: stage 1 of all 2 x NANCH
-// (reference, anchor) pairs runs in one round, two pairs per wave (32 lanes
-// each: hint +- HWIN2), then stage 2 for a reference whose stage 1 found
-// nothing.  One barrier instead of four; the hints and drift sets are
-// published by the caller.
+// Drift search of a coverage block: QM member tiles (one stripe) x 2
+// references x NANCH anchors.  Stage 1: every (member, reference, anchor)
+// triple searches hint +- HWIN2 with 32 lanes, 8 triples per round of the
+// block; stage 2, for a (member, reference) whose anchors all missed, searches
+// the full +-DRIFT with the whole block (rare: ~1 % of tiles).  best[] gets
+// (|delta| << 16 | drift) of every matching candidate (atomicMin: the
+// smallest drift wins).  The hints and drift sets are published by the caller.
 constexpr int HWIN2 = 56;
-struct DriftRef {
-  const uint8_t* s;
-  long long rbase, plo, phi;
-  int hint;
-  unsigned* best;
+constexpr int QM = 4;                         // member tiles per coverage block (one stripe)
+struct MemGeo {                               // a member tile: record, staging window, hints
+  long long rs, rn, a0, hi;
+  int r, h[2];                                // h: the XCD's last drift per reference (DRIFT: none)
 };
-__device__ __forceinline__ void find_drift_pair(const uint8_t* s_cls, long long base, long long qt, long long rn,
-                                                const DriftRef& A, const DriftRef& B, bool two) {
-  static_assert(2 * NANCH * 32 <= CBLOCK && (2 * HWIN2) / 4 + 2 <= 32, "two pairs per wave in stage 1");
+struct RefGeo {                               // a reference record's staged span (same for all members)
+  long long rbase, plo, phi, rfn;             // rbase: LDS index of the record's position 0
+};
+__device__ __forceinline__ void drift_task(const uint8_t* s_cls, const uint8_t* s_ref, int ia, int ibhi, int lo,
+                                           int hi, int w, unsigned* best) {
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
+  uint32_t x[2];
+  lds_bytes(s_cls, (uint32_t)ia, x);
+  const uint32_t W0 = rw[w], W1 = rw[w + 1], W2 = rw[w + 2];
+  uint32_t hit = 0;
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) {
+    const int ib = 4 * w + sb;
+    const bool h = (ib >= lo) & (ib <= hi) & (__builtin_amdgcn_alignbyte(W1, W0, sb) == x[0]) &
+                   (__builtin_amdgcn_alignbyte(W2, W1, sb) == x[1]);
+    hit |= (uint32_t)h << sb;
+  }
+  if (hit) {
+    uint32_t Aw[ALEN / 4];
+    lds_bytes(s_cls, (uint32_t)ia, Aw);
+    do {
+      const int ib = 4 * w + __builtin_ctz(hit);
+      hit &= hit - 1u;
+      uint32_t Bw[ALEN / 4];
+      lds_bytes(s_ref, (uint32_t)ib, Bw);
+      bool eq = true;
+#pragma unroll
+      for (int i = 0; i < ALEN / 4; ++i) eq &= Bw[i] == Aw[i];
+      const int d = ibhi - ib;
+      const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+      if (eq) atomicMin(best, (ad << 16) | (unsigned)d);
+    } while (hit);
+  }
+}
+// anchor ai of a member (LDS base `base`, record length rn) against reference R
+__device__ __forceinline__ void drift_geom(const RefGeo& R, long long qt, long long base, long long rn, int ai,
+                                           int& ia, int& ibhi, int& lo, int& hi) {
+  const long long a = qt + 8 + (long long)ai * ASTEP;
+  ia = (int)(base + a);
+  ibhi = (int)(R.rbase + a + DRIFT);
+  lo = max(ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
+  hi = a + ALEN > rn ? -1 : min(ibhi, (int)(R.rbase + R.phi) - ALEN);
+}
+__device__ __forceinline__ void cover_search(uint8_t (*s_cls)[SPAN + 16], uint8_t (*s_ref)[RSPAN],
+                                             const MemGeo* geo, const RefGeo& R0, const RefGeo& R1,
+                                             unsigned (*best)[2][NANCH], long long qt, uint32_t dm0, uint32_t dm1) {
+  static_assert((2 * HWIN2) / 4 + 2 <= 32, "32 lanes per triple in stage 1");
+  constexpr int NT = QM * 2 * NANCH, PER = CBLOCK / 32;
   constexpr int NW = (2 * DRIFT + 3) / 4 + 2;
-  auto task = [&](const uint8_t* s_ref, int ia, int ibhi, int lo, int hi, int w, unsigned* best) {
-    const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
-    uint32_t x[2];
-    lds_bytes(s_cls, (uint32_t)ia, x);
-    const uint32_t W0 = rw[w], W1 = rw[w + 1], W2 = rw[w + 2];
-    uint32_t hit = 0;
-#pragma unroll
-    for (int sb = 0; sb < 4; ++sb) {
-      const int ib = 4 * w + sb;
-      const bool h = (ib >= lo) & (ib <= hi) & (__builtin_amdgcn_alignbyte(W1, W0, sb) == x[0]) &
-                     (__builtin_amdgcn_alignbyte(W2, W1, sb) == x[1]);
-      hit |= (uint32_t)h << sb;
-    }
-    if (hit) {
-      uint32_t Aw[ALEN / 4];
-      lds_bytes(s_cls, (uint32_t)ia, Aw);
-      do {
-        const int ib = 4 * w + __builtin_ctz(hit);
-        hit &= hit - 1u;
-        uint32_t Bw[ALEN / 4];
-        lds_bytes(s_ref, (uint32_t)ib, Bw);
-        bool eq = true;
-#pragma unroll
-        for (int i = 0; i < ALEN / 4; ++i) eq &= Bw[i] == Aw[i];
-        const int d = ibhi - ib;
-        const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
-        if (eq) atomicMin(best, (ad << 16) | (unsigned)d);
-      } while (hit);
-    }
-  };
-  auto geom = [&](const DriftRef& R, int ai, int& ia, int& ibhi, int& lo, int& hi) {
-    const long long a = qt + 8 + (long long)ai * ASTEP;
-    ia = (int)(base + a);
-    ibhi = (int)(R.rbase + a + DRIFT);
-    lo = max(ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
-    hi = a + ALEN > rn ? -1 : min(ibhi, (int)(R.rbase + R.phi) - ALEN);
-  };
-  {
-    const int pr = (int)threadIdx.x >> 5, m = (int)threadIdx.x & 31;
-    const bool second = pr >= NANCH;
-    if (pr < 2 * NANCH && (!second || two)) {
-      const DriftRef& R = second ? B : A;
-      const int ai = second ? pr - NANCH : pr;
-      if (R.hint >= 0) {
-        int ia, ibhi, lo, hi;
-        geom(R, ai, ia, ibhi, lo, hi);
-        lo = max(lo, ibhi - (R.hint + HWIN2));
-        hi = min(hi, ibhi - (R.hint - HWIN2));
-        const int w = (lo >> 2) + m;
-        if (lo <= hi && 4 * w <= hi) task(R.s, ia, ibhi, lo, hi, w, R.best + ai);
-      }
+#pragma unroll 1
+  for (int t0 = 0; t0 < NT; t0 += PER) {
+    const int t = t0 + ((int)threadIdx.x >> 5), l = (int)threadIdx.x & 31;
+    const int m = t / (2 * NANCH), ri = (t / NANCH) & 1, ai = t % NANCH;
+    if (t < NT && (((ri ? dm1 : dm0) >> m) & 1u)) {
+      const MemGeo& G = geo[m];
+      int ia, ibhi, lo, hi;
+      drift_geom(ri ? R1 : R0, qt, G.rs - G.a0, G.rn, ai, ia, ibhi, lo, hi);
+      lo = max(lo, ibhi - (G.h[ri] + HWIN2));
+      hi = min(hi, ibhi - (G.h[ri] - HWIN2));
+      const int w = (lo >> 2) + l;
+      if (lo <= hi && 4 * w <= hi) drift_task(s_cls[m], s_ref[ri], ia, ibhi, lo, hi, w, &best[m][ri][ai]);
     }
   }
   __syncthreads();
   static_assert(NANCH == 3, "any-anchor test");
-  const bool anyA = (A.best[0] & A.best[1] & A.best[2]) != ~0u;            // block-uniform
-  const bool anyB = !two || (B.best[0] & B.best[1] & B.best[2]) != ~0u;
-  if (anyA && anyB) return;                                   // (the caller's barrier follows)
 #pragma unroll 1
-  for (int ri = 0; ri < 2; ++ri) {
-    const DriftRef& R = ri ? B : A;
-    if (ri ? anyB : anyA) continue;                           // block-uniform
+  for (int p = 0; p < 2 * QM; ++p) {                          // block-uniform
+    const int m = p >> 1, ri = p & 1;
+    if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
+    const MemGeo& G = geo[m];
 #pragma unroll 1
     for (int ai = 0; ai < NANCH; ++ai) {
       int ia, ibhi, lo, hi;
-      geom(R, ai, ia, ibhi, lo, hi);
+      drift_geom(ri ? R1 : R0, qt, G.rs - G.a0, G.rn, ai, ia, ibhi, lo, hi);
       for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += CBLOCK)
-        task(R.s, ia, ibhi, lo, hi, w, R.best + ai);
+        drift_task(s_cls[m], s_ref[ri], ia, ibhi, lo, hi, w, &best[m][ri][ai]);
     }
   }
   __syncthreads();
@@ -467,11 +472,17 @@ __host__ __device__ __forceinline__ void xcd_chunk(uint64_t ntiles, uint32_t b0,
   te = xs + xl * b1 / bt;
 }
 
-// K3 coverage pass.  One block per tile (record, stripe): the drift against
-// the lead record and a second reference (find_drift_pair), each segment's
-// covered windows (segment_cover), and the segments left with work appended
-// to the queue for k_emit_work.  With no reference (a single long record, or
-// the lead's own tiles) every segment is queued with nothing covered.
+// K3 coverage pass.  One block per coverage group: QM tiles of one stripe of
+// QM follower records (the lead's own tiles form groups of one).  The
+// members share one staging of the two references' spans, so a CU keeps ~4x
+// the windows in flight of a one-tile block at the same LDS (the pass is
+// latency-bound: SQ_WAIT_ANY was 58 % of wave cycles with one tile per block,
+// ~9 us per block for three dependent memory round trips and six barriers).
+// Per member: the drift against the lead record and a second reference
+// (cover_search), each segment's covered windows (segment_cover), and the
+// segments left with work appended to the queue for k_emit_work.  A member
+// with no reference (a single long record, or the lead's own tiles) queues
+// every segment with nothing covered.
 // Second reference.  Every follower also differs from the lead at the lead's
 // own variant sites, where all followers share the other allele: with the
 // lead alone those windows were emitted once per follower (C3: ~14 M of 51 M
@@ -480,110 +491,150 @@ __host__ __device__ __forceinline__ void xcd_chunk(uint64_t ntiles, uint32_t b0,
 // own windows are deduped against the lead only; a window it leaves to the
 // lead has the lead's context, key and masks, so "covered by ref2" still
 // means "inserted".
-// Chunks and XCDs: each XCD owns a contiguous eighth of the tile list
+// Chunks and XCDs: each XCD owns a contiguous eighth of the group list
 // (stripe-major, so its blocks share reference spans in its own L2), and
 // chunk c of nch launches takes the c-th part of every XCD's eighth, so an
 // XCD's drift hints carry over from the end of its previous chunk to the
-// start of the next (a contiguous chunk jumped each XCD a quarter genome
-// ahead, and the stage-2 search then ran on ~9 % of tiles).  A persistent,
-// software-pipelined form of this kernel (register prefetch of the next
-// tile) measured slower: 1.02 vs 0.76 ms at 64 VGPRs with spills, against
-// one-tile blocks at 8 waves/SIMD; rebuilt without spills (117 VGPRs, 4
-// blocks per CU, descriptor two tiles ahead, hints and staging one tile
-// ahead, the queue reservation consumed a tile later) it ran 909 vs 845 us
-// for all of C3's tiles in one launch: the pass is not bound by its
-// dependent memory round trips.
+// start of the next.  (A persistent, software-pipelined one-tile form of this
+// kernel measured slower: 909 vs 845 us for all of C3's tiles.)
 __global__ void __launch_bounds__(CBLOCK)
 k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
         long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints, int nrec,
-        uint64_t ntiles, uint32_t b0, uint32_t b1, uint32_t bt) {
-  __shared__ __attribute__((aligned(16))) uint8_t s_cls[SPAN + 16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_ref[RSPAN];
-  __shared__ __attribute__((aligned(16))) uint8_t s_ref2[RSPAN];
-  __shared__ unsigned s_best[NANCH], s_best2[NANCH];
+        uint64_t ngroups, uint32_t b0, uint32_t b1, uint32_t bt) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_cls[QM][SPAN + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_ref[2][RSPAN];
+  __shared__ unsigned s_best[QM][2][NANCH];
   __shared__ uint32_t s_scan[CBLOCK / 64];
   __shared__ unsigned long long s_qbase;
-  __shared__ Drifts s_dr[2];
-  uint64_t t, te;
-  xcd_chunk(ntiles, b0, b1, bt, blockIdx.x & 7, t, te);
-  t += blockIdx.x >> 3;
-  if (t >= te) return;                             // (block-uniform, before any barrier)
-  const TileDesc td = descs[t];
-  const long long rs = td.rs, rn = td.rn, last = rn - k;
-  const bool dedup = ref >= 0 && ref != td.r;                  // block-uniform
-  const bool dedup2 = dedup && ref2 >= 0 && ref2 != td.r;
-  // hints per (XCD, reference, record): the XCD swizzle gives each XCD its
-  // own contiguous eighth of the tile list, so one shared hint per record
-  // alternated between stripes ~150 apart and the hint window missed on
-  // 15-24 % of the tiles
-  int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
-  // (no drift known yet: try delta 0 first, the drift at a record's start)
-  // (plain loads may return a stale line from this CU's L1: device-scope
-  // loads cut the stage-2 searches 14 k -> 0.9 k per build and k_cover alone
-  // 1.56 -> 1.49 ms, yet the whole K3 span measured ~0.5 % slower with them)
-  int h1 = dedup ? hx[td.r] : -1, h2 = dedup2 ? hx[nrec + td.r] : -1;   // in flight with staging
-  h1 = h1 < 0 ? DRIFT : h1;
-  h2 = h2 < 0 ? DRIFT : h2;
-  const Stage g = stage_of(td, k, dedup, rfs, rfn);
-  Stage g2 = g;
-  if (dedup2) ref_span(g2, k, r2s, r2n);
-  // staging: at most two 16-byte chunks per thread and span, predicated
-  // (the spans are < 2 * CBLOCK * 16 bytes: SPAN, RSPAN)
-  static_assert(SPAN + 16 <= 2 * CBLOCK * 16 && RSPAN <= 2 * CBLOCK * 16, "two chunks per thread");
-  auto stage2 = [&](uint8_t* dst, long long from, long long to) {
-    const long long o0 = (long long)threadIdx.x * 16, o1 = o0 + CBLOCK * 16;
-    const bool l0 = from + o0 < to, l1 = from + o1 < to;
-    uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
-    if (l0) v0 = *reinterpret_cast<const uint4*>(cls + from + o0);
-    if (l1) v1 = *reinterpret_cast<const uint4*>(cls + from + o1);
-    if (l0) *reinterpret_cast<uint4*>(dst + o0) = v0;
-    if (l1) *reinterpret_cast<uint4*>(dst + o1) = v1;
-  };
-  stage2(s_cls, g.a0, g.hi);
-  if (dedup) {
-    stage2(s_ref, g.ra0, g.rend);
-    if (threadIdx.x < NANCH) s_best[threadIdx.x] = ~0u;
+  __shared__ MemGeo s_geo[QM];
+  __shared__ Drifts s_dr[QM][2];
+  uint64_t g, ge;
+  xcd_chunk(ngroups, b0, b1, bt, blockIdx.x & 7, g, ge);
+  g += blockIdx.x >> 3;
+  if (g >= ge) return;                             // (block-uniform, before any barrier)
+  // the members' descriptors (uniform loads) -> which members dedup
+  const long long qt = (long long)descs[QM * g].stripe * TILE;
+  uint32_t dm0 = 0, dm1 = 0;
+#pragma unroll
+  for (int m = 0; m < QM; ++m) {
+    const int r = descs[QM * g + m].r;
+    const bool d0 = r >= 0 && ref >= 0 && ref != r;
+    dm0 |= (uint32_t)d0 << m;
+    dm1 |= (uint32_t)(d0 && ref2 >= 0 && ref2 != r) << m;
   }
-  if (dedup2) {
-    stage2(s_ref2, g2.ra0, g2.rend);
-    if (threadIdx.x < NANCH) s_best2[threadIdx.x] = ~0u;
+  // per member: staging window and hints (hints per XCD, reference and
+  // record: the XCD swizzle gives each XCD its own eighth of the group list,
+  // so one shared hint per record alternated between stripes ~150 apart)
+  int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
+  if (threadIdx.x < QM) {
+    const TileDesc td = descs[QM * g + threadIdx.x];
+    MemGeo G;
+    G.r = td.r;
+    G.rs = td.rs;
+    G.rn = td.rn;
+    const long long lo = td.rs + (qt >= 2 ? qt - 2 : 0);
+    G.hi = td.rs + (qt + TILE + k + 2 < td.rn ? qt + TILE + k + 2 : td.rn);
+    G.a0 = lo & ~15ll;
+    if (td.r < 0) G.a0 = G.hi = 0;                 // an empty slot stages nothing
+    // (no drift known yet: try delta 0 first, the drift at a record's start)
+    const int h0 = ((dm0 >> threadIdx.x) & 1u) ? hx[td.r] : -1;
+    const int h1 = ((dm1 >> threadIdx.x) & 1u) ? hx[nrec + td.r] : -1;
+    G.h[0] = h0 < 0 ? DRIFT : h0;
+    G.h[1] = h1 < 0 ? DRIFT : h1;
+    s_geo[threadIdx.x] = G;
+  }
+  if (threadIdx.x < QM * 2 * NANCH) (&s_best[0][0][0])[threadIdx.x] = ~0u;
+  // the references' spans of this stripe: [qt-1-DRIFT, qt+TILE+k+1+DRIFT) clipped
+  RefGeo rg[2];
+  long long ra0[2], rend[2];
+#pragma unroll
+  for (int ri = 0; ri < 2; ++ri) {
+    const long long s = ri ? r2s : rfs, n = ri ? r2n : rfn;
+    rg[ri].plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
+    rg[ri].phi = qt + TILE + k + 1 + DRIFT < n ? qt + TILE + k + 1 + DRIFT : n;
+    rg[ri].rfn = n;
+    ra0[ri] = (s + rg[ri].plo) & ~15ll;
+    rend[ri] = s + rg[ri].phi;
+    rg[ri].rbase = s - ra0[ri];
   }
   __syncthreads();
-  const long long base = rs - g.a0, rbase = rfs - g.ra0, rbase2 = r2s - g2.ra0;   // LDS index of position 0
-  if (dedup)
-    find_drift_pair(s_cls, base, g.qt, rn, DriftRef{s_ref, rbase, g.plo, g.phi, h1, s_best},
-                    DriftRef{s_ref2, rbase2, g2.plo, g2.phi, h2, s_best2}, dedup2);
-  const long long q0 = g.qt + (long long)threadIdx.x * IW;
-  constexpr uint32_t ALL = (1u << IW) - 1u;
-  uint32_t covered = 0;
-  // hints and the drift sets once per block (one lane's scalar work, read
-  // back from LDS) instead of once per wave
-  if (dedup) {                                       // block-uniform
-    if (threadIdx.x == 0) {
-      publish_hint(s_best, hx + td.r);
-      if (dedup2) publish_hint(s_best2, hx + nrec + td.r);
-      s_dr[0] = drifts_of(s_best, g.qt, base, rbase, rfn, g.plo, g.phi, k);
-      if (dedup2) s_dr[1] = drifts_of(s_best2, g.qt, base, rbase2, r2n, g2.plo, g2.phi, k);
+  // staging: every span's loads in flight before the first LDS store (at most
+  // two 16-byte chunks per thread and span: SPAN, RSPAN < 2 * CBLOCK * 16)
+  static_assert(SPAN + 16 <= 2 * CBLOCK * 16 && RSPAN <= 2 * CBLOCK * 16, "two chunks per thread");
+  {
+    constexpr int NS = QM + 2;
+    uint4 v[NS][2];
+    bool lv[NS][2];
+    const long long o0 = (long long)threadIdx.x * 16, o1 = o0 + CBLOCK * 16;
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      long long from, to;
+      if (s < QM) { from = s_geo[s].a0; to = s_geo[s].hi; }
+      else {
+        const int ri = s - QM;
+        const bool use = ri ? dm1 != 0 : dm0 != 0;
+        from = ra0[ri];
+        to = use ? rend[ri] : from;
+      }
+      lv[s][0] = from + o0 < to;
+      lv[s][1] = from + o1 < to;
+      v[s][0] = lv[s][0] ? *reinterpret_cast<const uint4*>(cls + from + o0) : make_uint4(0u, 0u, 0u, 0u);
+      v[s][1] = lv[s][1] ? *reinterpret_cast<const uint4*>(cls + from + o1) : make_uint4(0u, 0u, 0u, 0u);
     }
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      uint8_t* dst = s < QM ? s_cls[s] : s_ref[s - QM];
+      if (lv[s][0]) *reinterpret_cast<uint4*>(dst + o0) = v[s][0];
+      if (lv[s][1]) *reinterpret_cast<uint4*>(dst + o1) = v[s][1];
+    }
   }
-  if (dedup && q0 > 0 && q0 + IW <= last) {
-    constexpr int NB = (IW + 27 + 1 + 3) / 4;                // bytes q0-1 .. q0+IW+k-1, k <= 27
-    const uint32_t o = (uint32_t)(base + q0 - 1);
-    const int rel = (int)threadIdx.x * IW;
-    uint32_t G[NB];
-    lds_bytes16(s_cls, o, G);
-    covered = segment_cover(s_cls, s_ref, o, rel, G, s_dr[0], k);
-    if (dedup2 && covered != ALL) covered |= segment_cover(s_cls, s_ref2, o, rel, G, s_dr[1], k);
+  __syncthreads();
+  if (dm0) cover_search(s_cls, s_ref, s_geo, rg[0], rg[1], s_best, qt, dm0, dm1);     // (block-uniform)
+  // hints and drift sets: one lane per (member, reference)
+  if (threadIdx.x < 2 * QM) {
+    const int m = threadIdx.x >> 1, ri = threadIdx.x & 1;
+    if ((((ri ? dm1 : dm0) >> m) & 1u)) {
+      const MemGeo& G = s_geo[m];
+      publish_hint(s_best[m][ri], hx + (ri ? nrec : 0) + G.r);
+      const RefGeo R = ri ? rg[1] : rg[0];
+      s_dr[m][ri] = drifts_of(s_best[m][ri], qt, G.rs - G.a0, R.rbase, R.rfn, R.plo, R.phi, k);
+    }
   }
-  const bool work = q0 <= last && covered != ALL;
+  __syncthreads();
+  constexpr uint32_t ALL = (1u << IW) - 1u;
+  constexpr int NB = (IW + 27 + 1 + 3) / 4;                  // bytes q0-1 .. q0+IW+k-1, k <= 27
+  const long long q0 = qt + (long long)threadIdx.x * IW;
+  const int rel = (int)threadIdx.x * IW;
+  uint32_t cov[QM], nwk = 0, wmask = 0;
+#pragma unroll
+  for (int m = 0; m < QM; ++m) {
+    const MemGeo& G = s_geo[m];
+    const long long last = G.rn - k;
+    uint32_t covered = 0;
+    if (((dm0 >> m) & 1u) && q0 > 0 && q0 + IW <= last) {
+      const uint32_t o = (uint32_t)(G.rs - G.a0 + q0 - 1);
+      uint32_t Gb[NB];
+      lds_bytes16(s_cls[m], o, Gb);
+      covered = segment_cover(s_cls[m], s_ref[0], o, rel, Gb, s_dr[m][0], k);
+      if (((dm1 >> m) & 1u) && covered != ALL) covered |= segment_cover(s_cls[m], s_ref[1], o, rel, Gb, s_dr[m][1], k);
+    }
+    cov[m] = covered;
+    const bool work = G.r >= 0 && q0 <= last && covered != ALL;
+    wmask |= (uint32_t)work << m;
+    nwk += work ? 1u : 0u;
+  }
   uint32_t nwork;
-  const uint32_t pos = block_excl_scan<CBLOCK>(work ? 1u : 0u, s_scan, nwork);
+  uint32_t pos = block_excl_scan<CBLOCK>(nwk, s_scan, nwork);
   const unsigned sub = blockIdx.x % NQ;
   if (threadIdx.x == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
   __syncthreads();
-  if (work) queue[sub * qcap + s_qbase + pos] = WorkItem{rs, last, q0, covered, 0u};
+#pragma unroll
+  for (int m = 0; m < QM; ++m)
+    if ((wmask >> m) & 1u) {
+      const MemGeo& G = s_geo[m];
+      queue[sub * qcap + s_qbase + pos++] = WorkItem{G.rs, G.rn - k, q0, cov[m], 0u};
+    }
 }
 
 // ---------------------------------------------------------------- stage A
@@ -1120,36 +1171,42 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
 }
 
 // ---------------------------------------------------------------- tiles
-// The K3 tile list, expanded on the device from the host's compact schedule
-// (sched = off[0 .. nj] then ord[0 .. nord)): stripe j holds tiles
-// [off[j], off[j+1]); while j < lead_stripes its first tile is the lead's
-// (record ord[0], stripe j), the others are followers ord[1 + i] at stripe
-// j - LEAD (the lead runs LEAD stripes ahead).
+// The K3 coverage groups, expanded on the device from the host's compact
+// schedule (sched = off[0 .. nj], nf[0 .. nj), ord[0 .. nord)): stripe group
+// j holds coverage groups [off[j], off[j+1]); while j < lead_stripes its first
+// group is the lead's tile (record ord[0], stripe j) alone, the others hold QM
+// followers each, ord[1 + f] for f < nf[j], at stripe j - LEAD (the lead runs
+// LEAD stripes ahead).  Group g's members are descs[QM*g .. QM*g + QM); an
+// empty slot has r = -1 and the group's stripe.
 constexpr uint32_t LEAD = 4;
 __global__ void k_tiles(const uint32_t* __restrict__ sched, uint32_t nj, uint32_t lead_stripes,
                         const long long* __restrict__ rec_start, const long long* __restrict__ rec_len,
-                        TileDesc* __restrict__ out, uint64_t ntiles) {
+                        TileDesc* __restrict__ out, uint64_t ngroups) {
   const uint32_t* off = sched;
-  const uint32_t* ord = sched + nj + 1;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < ntiles;
+  const uint32_t* nf = sched + nj + 1;
+  const uint32_t* ord = nf + nj;
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < ngroups * QM;
        t += (uint64_t)gridDim.x * blockDim.x) {
-    uint32_t lo = 0, hi = nj;                                  // off[lo] <= t < off[hi]
+    const uint64_t g = t / QM;
+    const uint32_t m = (uint32_t)(t % QM);
+    uint32_t lo = 0, hi = nj;                                  // off[lo] <= g < off[hi]
     while (hi - lo > 1) {
       const uint32_t mid = (lo + hi) >> 1;
-      if (off[mid] <= t) lo = mid; else hi = mid;
+      if (off[mid] <= g) lo = mid; else hi = mid;
     }
-    uint32_t i = (uint32_t)(t - off[lo]);
-    int r;
-    int stripe;
-    if (lo < lead_stripes && i == 0) {
-      r = (int)ord[0];
+    uint32_t i = (uint32_t)(g - off[lo]);
+    const bool lead = lo < lead_stripes;
+    int r = -1, stripe;
+    if (lead && i == 0) {
       stripe = (int)lo;
+      if (m == 0) r = (int)ord[0];
     } else {
-      if (lo < lead_stripes) --i;
-      r = (int)ord[1 + i];
+      if (lead) --i;
       stripe = (int)(lo - LEAD);
+      const uint32_t f = i * QM + m;
+      if (f < nf[lo]) r = (int)ord[1 + f];
     }
-    out[t] = TileDesc{rec_start[r], rec_len[r], r, stripe, 0};
+    out[t] = r >= 0 ? TileDesc{rec_start[r], rec_len[r], r, stripe, 0} : TileDesc{0, 0, -1, stripe, 0};
   }
 }
 
@@ -1297,13 +1354,14 @@ static void init_hash(Ctx& c) {
   c.hash_k = c.k;
 }
 
-// The tile list (records with n >= k+2), stripe-major: stripe 0 of every
-// record, then stripe 1, ... (records with more stripes first within a
-// stripe).  One lead record runs LEAD stripes ahead of the others, so that
-// the coverage pass finds the lead's windows staged before its followers
-// compare against them in the same L2.  The host sorts the records and sends
-// the per-stripe tile counts; k_tiles expands the descriptors on the device.
-// Cached while the record table and flags repeat.
+// The coverage groups (records with n >= k+2), stripe-major: stripe 0 of
+// every record, then stripe 1, ... (records with more stripes first within a
+// stripe), QM followers of a stripe per group.  One lead record runs LEAD
+// stripes ahead of the others, so that the coverage pass finds the lead's
+// windows staged before its followers compare against them in the same L2.
+// The host sorts the records and sends the per-stripe group offsets and
+// follower counts; k_tiles expands the descriptors on the device.  Cached
+// while the record table and flags repeat.  Returns the number of groups.
 static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   const uint64_t R = c.n_records;
   if (c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k) return c.n_tiles;
@@ -1319,31 +1377,33 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
   c.k3_hint.reserve(64 * (R + 1) + 64);               // drift hints per XCD, reference, record
   const uint64_t lead_s = nt.empty() ? 0 : nt[0].first;
   const uint32_t nj = nt.empty() ? 0u : (uint32_t)(lead_s + LEAD);
-  std::vector<uint32_t> sched(nj + 1 + nt.size());
+  std::vector<uint32_t> sched(2 * nj + 1 + nt.size());
   uint64_t total = 0;
   size_t live = nt.size();
   for (uint32_t j = 0; j < nj; ++j) {
     sched[j] = (uint32_t)total;
-    uint64_t cnt = j < lead_s ? 1 : 0;
+    uint64_t cnt = j < lead_s ? 1 : 0, nfol = 0;
     if (j >= LEAD) {
       const uint64_t jf = j - LEAD;                   // the followers' stripe
       while (live && nt[live - 1].first <= jf) --live;
-      cnt += live > 1 ? live - 1 : 0;
+      nfol = live > 1 ? live - 1 : 0;
+      cnt += (nfol + QM - 1) / QM;
     }
+    sched[nj + 1 + j] = (uint32_t)nfol;
     total += cnt;
   }
   sched[nj] = (uint32_t)total;
-  for (size_t i = 0; i < nt.size(); ++i) sched[nj + 1 + i] = (uint32_t)nt[i].second;
-  if (total >= (1ull << 32)) throw Error(-22, "make_tiles: too many tiles");
-  c.tile_desc.reserve(sizeof(TileDesc) * (total + 1));
+  for (size_t i = 0; i < nt.size(); ++i) sched[2 * nj + 1 + i] = (uint32_t)nt[i].second;
+  if (total * QM >= (1ull << 32)) throw Error(-22, "make_tiles: too many tiles");
+  c.tile_desc.reserve(sizeof(TileDesc) * (QM * total + 1));
   if (total) {
     c.tile_pin.reserve(4 * sched.size());
     c.tile_sched.reserve(4 * sched.size());
     std::memcpy(c.tile_pin.p, sched.data(), 4 * sched.size());
     PG_HIP(hipMemcpyAsync(c.tile_sched.p, c.tile_pin.p, 4 * sched.size(), hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_tiles, dim3(grid_for(total, 256, 2048)), dim3(256), 0, c.stream, c.tile_sched.as<uint32_t>(),
-                       nj, (uint32_t)lead_s, c.rec_start.as<long long>(), c.rec_len.as<long long>(),
-                       c.tile_desc.as<TileDesc>(), total);
+    hipLaunchKernelGGL(k_tiles, dim3(grid_for(QM * total, 256, 2048)), dim3(256), 0, c.stream,
+                       c.tile_sched.as<uint32_t>(), nj, (uint32_t)lead_s, c.rec_start.as<long long>(),
+                       c.rec_len.as<long long>(), c.tile_desc.as<TileDesc>(), total);
     PG_HIP(hipGetLastError());
   }
   c.tile_sig_len = c.h_rec_len;
@@ -1519,9 +1579,8 @@ static void finish_build(Ctx& c, const ACount& a) {
 
 // chunks of the tile list whose work pass overlaps the next coverage pass
 constexpr int K3_CHUNKS = 4;
-constexpr int K3_COVPAD = 8 * 1024;           // dynamic LDS pad per coverage block (chunked form)
 constexpr int K3_WBLK = 2;                    // work blocks per CU (chunked form)
-constexpr uint64_t K3_CHUNK_MIN = 4096;       // tiles per chunk below which one chunk runs
+constexpr uint64_t K3_CHUNK_MIN = 1024;       // coverage groups per chunk below which one chunk runs
 
 static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, const BinOut& O) {
   if (!c.n_records) return;
@@ -1553,7 +1612,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
       xcd_chunk(ntiles, (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch, (uint64_t)x, t, te);
       gc[i] = std::max<uint64_t>(gc[i], 8 * (te - t));
     }
-    qcapc[i] = (gc[i] + NQ - 1) / NQ * CBLOCK;      // per sub-queue
+    qcapc[i] = (gc[i] + NQ - 1) / NQ * (QM * CBLOCK);   // per sub-queue: a block queues <= QM * CBLOCK
     qoff[i] = items;
     items += NQ * qcapc[i];
   }
@@ -1566,7 +1625,6 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   c.t1.init();
   c.t1.start(s0);
   fl.launch(s0);
-  const size_t covpad = nch > 1 ? (size_t)K3_COVPAD : 0;
   const unsigned wgrid = (unsigned)c.n_cu * K3_WBLK;
   auto* q = c.k3_queue.as<WorkItem>();
   auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
@@ -1581,7 +1639,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     auto* qi = q + qoff[i];
     auto* qni = qn + (cbytes / 8) * i;
     if (gc[i])
-      hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), dim3(CBLOCK), covpad, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
+      hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
                          c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
                          (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch);
     PG_HIP(hipGetLastError());
