@@ -55,6 +55,46 @@ __device__ __forceinline__ uint32_t eq4(uint32_t w, uint32_t pat) {
 __device__ __forceinline__ uint32_t eq16(const uint4& v, uint32_t pat) {
   return eq4(v.x, pat) | eq4(v.y, pat) << 4 | eq4(v.z, pat) << 8 | eq4(v.w, pat) << 12;
 }
+// bit 7 of every byte of w that equals the replicated byte in pat
+__device__ __forceinline__ uint32_t zmatch(uint32_t w, uint32_t pat) {
+  const uint32_t x = w ^ pat;
+  return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
+// zmatch's byte bits (7, 15, 23, 31) packed into bits 0..3: the four
+// partial products land on distinct bit positions, so nothing carries
+__device__ __forceinline__ uint32_t pack4(uint32_t z) { return (z * 0x00204081u) >> 28; }
+
+// Fast-path view of one lane's 16 bytes: the '\n' mask, whether a '>' is
+// among them, and the class codes of the bytes when every byte but '\n' is
+// one of ACGTacgt (`acgt`).  u = the byte with bit 5 cleared (a -> A ...);
+// t = (u >> 1) & 3 maps A C T G to 0 1 2 3, so u is ACGT iff the byte of
+// "ACTG" at t equals u, and the class (A0 C1 G2 T3) is t ^ (t >> 1).
+// '\n' bytes are checked as 'A' (they are dropped anyway).
+struct FastLane {
+  uint32_t nlm, cls[4];
+  bool gt, acgt;
+};
+__device__ __forceinline__ FastLane fast_lane(const uint4& v) {
+  static_assert(CLS_A == 0 && CLS_C == 1 && CLS_G == 2 && CLS_T == 3, "class codes of ACGT");
+  FastLane f;
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t gt = 0, bad = 0;
+  f.nlm = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t zn = zmatch(w[d], 0x0A0A0A0Au);
+    gt |= zmatch(w[d], 0x3E3E3E3Eu);
+    f.nlm |= pack4(zn) << (4 * d);
+    const uint32_t bm = zn | (zn - (zn >> 7));                 // 0xFF on the '\n' bytes
+    const uint32_t u = ((w[d] & ~bm) | (0x41414141u & bm)) & 0xDFDFDFDFu;
+    const uint32_t t = (u >> 1) & 0x03030303u;
+    bad |= __builtin_amdgcn_perm(0u, 0x47544341u, t) ^ u;
+    f.cls[d] = t ^ ((t >> 1) & 0x01010101u);
+  }
+  f.gt = gt != 0u;
+  f.acgt = bad == 0u;
+  return f;
+}
 
 // bits of the lane's 16 positions below `lim`
 __device__ __forceinline__ uint32_t below_mask(uint64_t p, uint64_t lim) {
@@ -174,10 +214,40 @@ __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__
   uint32_t c0 = 0, c1 = 0, fo = 2u;                           // identity: out(s) = s
   uint32_t nl = 0, hdr = 0;
   int top = -1, second = -1;
+  auto last_two = [&](uint32_t nlm, uint64_t p) {             // the span's last two '\n'
+    if (nlm) {
+      const int rel = (int)(p - p0);
+      const int t = 31 - __builtin_clz(nlm);
+      const uint32_t rest = nlm & ~(1u << t);
+      second = rest ? rel + 31 - __builtin_clz(rest) : top;
+      top = rel + t;
+    }
+  };
 #pragma unroll
   for (int s = 0; s < WSTEPS; ++s) {
     if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
     const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
+    // Fast step (wave-uniform): every byte below n - 1, no '>' in the step,
+    // and the span-so-far sends either in-state to out-state 0 - then no
+    // header line is open or starts, and every byte but '\n' is content
+    if (fo == 0u && p0 + (uint64_t)(s + 1) * WSTEP < n) {
+      uint32_t gt = 0, nlm = 0;
+      const uint32_t w[4] = {v[s].x, v[s].y, v[s].z, v[s].w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        gt |= zmatch(w[d], 0x3E3E3E3Eu);
+        nlm |= pack4(zmatch(w[d], 0x0A0A0A0Au)) << (4 * d);
+      }
+      if (!__ballot(gt != 0u)) {
+        carry = (uint32_t)(__ballot((nlm >> 15) & 1u) >> 63) & 1u;
+        const uint32_t cnt = (uint32_t)__builtin_popcount(nlm);
+        c0 += 16u - cnt;
+        c1 += 16u - cnt;
+        nl += cnt;
+        last_two(nlm, p);
+        continue;
+      }
+    }
     const LaneStep ls = lane_step(v[s], p, n, lane, carry);
     // lane-local counts for span in-state 0 / 1: a lane's in-state is fixed by
     // a line start in a lower lane, else it is the step's in-state fo(s)
@@ -190,13 +260,7 @@ __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__
     fo = step_out(ls, f0) | step_out(ls, f1) << 1;
     nl += __builtin_popcount(ls.nlm);
     hdr += __builtin_popcount(ls.hs);
-    if (ls.nlm) {
-      const int rel = (int)(p - p0);
-      const int t = 31 - __builtin_clz(ls.nlm);
-      const uint32_t rest = ls.nlm & ~(1u << t);
-      second = rest ? rel + 31 - __builtin_clz(rest) : top;
-      top = rel + t;
-    }
+    last_two(ls.nlm, p);
   }
   // per lane: c0, c1 <= 256 and nl, hdr <= 256, so the packed sums stay in 16 bits
   const uint32_t cs = __builtin_amdgcn_readlane(wave_incl_sum(c0 | c1 << 16), 63);
@@ -216,7 +280,8 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
                                                  const Fn* __restrict__ incl,
                                                  uint8_t* __restrict__ out, long long* __restrict__ rec_start,
                                                  long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
-  constexpr int STAGE = WSTEP + 32;
+  // pending bytes (< 32) + one step's (<= WSTEP) + the fast step's fifth dword
+  constexpr int STAGE = WSTEP + 48;
   __shared__ uint8_t lut[256];
   __shared__ __attribute__((aligned(16))) uint8_t stage_all[WAVES][STAGE];
   lut[threadIdx.x] = c_byte_class[threadIdx.x];
@@ -225,6 +290,15 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
   const uint64_t span = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
   if (span >= nspan) return;                                  // wave-uniform, after the only barrier
   uint8_t* stage = stage_all[threadIdx.x >> 6];
+  auto wave_sync = []() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+  // Invariant at every step start: the stage is zero past its pending bytes
+  // (the fast step ORs whole dwords in; the general step stores bytes).
+  for (int z = 16 * lane; z < STAGE; z += 16 * 64) *reinterpret_cast<uint4*>(stage + z) = make_uint4(0, 0, 0, 0);
+  wave_sync();
   const uint64_t p0 = span * WSPAN;
   // the prefix function evaluated at the file's in-state (0; byte 0 starts a line)
   const Fn pre = span ? incl[span - 1] : fn_identity();
@@ -242,42 +316,76 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
     if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
     const uint64_t pn = p + WSTEP;
     const uint4 vn = (s + 1 < WSTEPS && pn < n) ? load16(buf, pn, n) : make_uint4(0, 0, 0, 0);
-    const LaneStep ls = lane_step(v, p, n, lane, carry);
-    const uint32_t region = lane_region(ls, lane_in(ls, state));
-    const uint32_t cm = lane_content(ls, region);
-    const uint32_t mine = (uint32_t)__builtin_popcount(cm) | (uint32_t)__builtin_popcount(ls.hs) << 16;
-    const uint32_t incl = wave_incl_sum(mine);
-    const uint32_t excl = incl - mine;
-    const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
-    const unsigned long long lane_off = off + (excl & 0xFFFFu);
-    const unsigned long long lane_rec = rec + (excl >> 16);
-    // header lines: start (record begins at the next base) and terminator
-    const uint32_t term = region & (ls.nlm | (~ls.vn1 & below_mask(p, n) & (ls.vn1 + 1u)));
-    if (ls.hs | term) {
-      for (uint32_t m = ls.hs; m; m &= m - 1) {
-        const int j = __builtin_ctz(m);
-        const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((1u << j) - 1u));
-        hdr_start[r] = (long long)(p + j);
-        rec_start[r] = (long long)(lane_off + __builtin_popcount(cm & ((1u << j) - 1u)));
+    uint32_t ctot, hcnt = 0;
+    // Fast step (wave-uniform): in-state 0, every byte below n - 1, no '>',
+    // at most one '\n' per lane and every other byte one of ACGTacgt - the
+    // lane's bases are its 16 bytes minus the '\n', classed in registers and
+    // ORed into the zeroed stage as 5 dwords (no per-byte LDS traffic)
+    const FastLane fl = fast_lane(v);
+    const bool fast = state == 0u && p0 + (uint64_t)(s + 1) * WSTEP < n &&
+                      !__ballot(fl.gt || !fl.acgt || (fl.nlm & (fl.nlm - 1u)) != 0u);
+    if (fast) {
+      carry = (uint32_t)(__ballot((fl.nlm >> 15) & 1u) >> 63) & 1u;
+      const uint32_t mine = 16u - (uint32_t)__builtin_popcount(fl.nlm);
+      const uint32_t incl = wave_incl_sum(mine);
+      const uint32_t excl = incl - mine;
+      ctot = __builtin_amdgcn_readlane(incl, 63);
+      // drop the '\n' at byte j (j = 16: none): bytes past it move down by one
+      const uint32_t j = fl.nlm ? (uint32_t)__builtin_ctz(fl.nlm) : 16u;
+      uint32_t y[4];
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const uint32_t down = d < 3 ? __builtin_amdgcn_alignbyte(fl.cls[d + 1], fl.cls[d], 1) : fl.cls[3] >> 8;
+        const int lo = (int)j - 4 * d;                        // bytes of dword d below j
+        const uint32_t keep = lo >= 4 ? 0xFFFFFFFFu : lo <= 0 ? 0u : (1u << (8 * lo)) - 1u;
+        y[d] = (fl.cls[d] & keep) | (down & ~keep);
       }
-      for (uint32_t m = term; m; m &= m - 1) {
-        const int j = __builtin_ctz(m);
-        const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((2u << j) - 1u)) - 1;
-        hdr_end[r] = (long long)(p + j);
+      const uint32_t w = (uint32_t)(off - cb) + excl;
+      uint32_t* s32 = reinterpret_cast<uint32_t*>(stage) + (w >> 2);
+      const uint32_t sh = 32u - 8u * (w & 3u);
+      uint32_t prev = 0;
+#pragma unroll
+      for (int d = 0; d < 5; ++d) {
+        const uint32_t cur = d < 4 ? y[d] : 0u;
+        atomicOr(s32 + d, (uint32_t)((((uint64_t)cur << 32) | prev) >> sh));
+        prev = cur;
       }
-    }
-    // stage this step's bases after the pending bytes of chunk `cb`
-    {
+    } else {
+      const LaneStep ls = lane_step(v, p, n, lane, carry);
+      const uint32_t region = lane_region(ls, lane_in(ls, state));
+      const uint32_t cm = lane_content(ls, region);
+      const uint32_t mine = (uint32_t)__builtin_popcount(cm) | (uint32_t)__builtin_popcount(ls.hs) << 16;
+      const uint32_t incl = wave_incl_sum(mine);
+      const uint32_t excl = incl - mine;
+      const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+      const unsigned long long lane_off = off + (excl & 0xFFFFu);
+      const unsigned long long lane_rec = rec + (excl >> 16);
+      // header lines: start (record begins at the next base) and terminator
+      const uint32_t term = region & (ls.nlm | (~ls.vn1 & below_mask(p, n) & (ls.vn1 + 1u)));
+      if (ls.hs | term) {
+        for (uint32_t m = ls.hs; m; m &= m - 1) {
+          const int jj = __builtin_ctz(m);
+          const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((1u << jj) - 1u));
+          hdr_start[r] = (long long)(p + jj);
+          rec_start[r] = (long long)(lane_off + __builtin_popcount(cm & ((1u << jj) - 1u)));
+        }
+        for (uint32_t m = term; m; m &= m - 1) {
+          const int jj = __builtin_ctz(m);
+          const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((2u << jj) - 1u)) - 1;
+          hdr_end[r] = (long long)(p + jj);
+        }
+      }
+      // stage this step's bases after the pending bytes of chunk `cb`
       uint32_t w = (uint32_t)(off - cb) + (excl & 0xFFFFu);
       const uint32_t words[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-      for (int j = 0; j < 16; ++j)
-        if ((cm >> j) & 1u) stage[w++] = lut[(words[j >> 2] >> (8 * (j & 3))) & 0xFFu];
+      for (int jj = 0; jj < 16; ++jj)
+        if ((cm >> jj) & 1u) stage[w++] = lut[(words[jj >> 2] >> (8 * (jj & 3))) & 0xFFu];
+      ctot = tot & 0xFFFFu;
+      hcnt = tot >> 16;
+      state = step_out(ls, state);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t ctot = tot & 0xFFFFu;
+    wave_sync();
     // write every completed 16-byte chunk; the partial one stays staged.  Only
     // the span's first chunk can hold bytes of the previous span (< own).
     const unsigned long long full = (off + ctot) & ~15ull;
@@ -287,23 +395,22 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
         if (g >= own) {
           *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(src);
         } else {
-          for (int j = 0; j < 16; ++j)
-            if (g + j >= own) out[g + j] = src[j];
+          for (int jj = 0; jj < 16; ++jj)
+            if (g + jj >= own) out[g + jj] = src[jj];
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_sync();
+      // (the bytes past the pending ones in that chunk are zero: invariant)
       if (lane == 0)
         *reinterpret_cast<uint4*>(stage) = *reinterpret_cast<const uint4*>(stage + (full - cb));
       cb = full;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      wave_sync();
+      for (int z = 16 + 16 * lane; z < STAGE; z += 16 * 64)
+        *reinterpret_cast<uint4*>(stage + z) = make_uint4(0, 0, 0, 0);
+      wave_sync();
     }
     off += ctot;
-    rec += tot >> 16;
-    state = step_out(ls, state);
+    rec += hcnt;
     v = vn;
     p = pn;
   }

@@ -111,3 +111,34 @@ def test_parse_span_boundaries(oracle_mod):
         body = b"A" * (span + shift - 4)
         _check(b">a\n" + body + b"\n>b\nCC\n", oracle_mod)
         _check(b">a\nC\n" + b"G" * (span + shift - 6) + b">c\nAC\n", oracle_mod)
+
+
+def _mixed_fasta(seed, widths, nrec=12, reclen=40_000):
+    """Records of ACGT with lowercase stretches, N runs and a rare '$', wrapped
+    at the given line widths: most 1 KiB wave steps take K1's fast step (no
+    '>', at most one '\\n' per 16 bytes, ACGTacgt only), the rest its general
+    step, switching at every kind of boundary."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    out = []
+    for r in range(nrec):
+        s = acgt[rng.integers(0, 4, reclen)].copy()
+        for _ in range(6):                                   # lowercase stretches
+            a = int(rng.integers(0, reclen - 500))
+            s[a:a + int(rng.integers(1, 500))] |= 0x20
+        if r % 3 == 0:                                       # an N run (general steps)
+            a = int(rng.integers(0, reclen - 100))
+            s[a:a + int(rng.integers(1, 100))] = ord("N")
+        if r % 5 == 1:
+            s[int(rng.integers(0, reclen))] = ord("$")
+        w = int(widths[r % len(widths)])
+        body = b"\n".join(s[i:i + w].tobytes() for i in range(0, reclen, w))
+        out.append(b">rec%d some description\n" % r + body + b"\n")
+    return b"".join(out)
+
+
+@pytest.mark.parametrize("widths", [(60,), (15, 16, 17), (61, 80, 1000), (16, 7, 60, 33)])
+def test_parse_fast_steps(oracle_mod, widths):
+    _check(_mixed_fasta(sum(widths), widths), oracle_mod)
+    # unterminated last line, and a record longer than a 16 KiB span
+    _check(_mixed_fasta(7, widths, nrec=3, reclen=50_000)[:-1], oracle_mod)
