@@ -1431,15 +1431,8 @@ struct ACount {
   uint64_t total = 0, maxreg = 0, maxbin = 0;
   unsigned sentinel = 0, bits = 0;
 };
-// sync #1: the stage A region counts and flags
-static ACount stageA_read(Ctx& c) {
-  const size_t cb = 8 * CSTRIDE * NREG;
-  c.h_pin.reserve(cb + 4 * N_FLAGS);
-  PG_HIP(hipMemcpyAsync(c.h_pin.p, c.ctrA.p, cb, hipMemcpyDeviceToHost, c.stream));
-  PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + cb, c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost, c.stream));
-  c.sync();
-  const unsigned long long* h = c.h_pin.as<unsigned long long>();
-  const unsigned* fl = reinterpret_cast<const unsigned*>(c.h_pin.as<uint8_t>() + cb);
+// stage A's counts and flags from a pinned copy of ctrA and the flags
+static ACount stageA_counts(const unsigned long long* h, const unsigned* fl) {
   ACount a;
   for (int p = 0; p < NBIN; ++p) {
     uint64_t bin = 0;
@@ -1456,13 +1449,31 @@ static ACount stageA_read(Ctx& c) {
   return a;
 }
 
+// sync #1: the stage A region counts and flags
+static ACount stageA_read(Ctx& c) {
+  const size_t cb = 8 * CSTRIDE * NREG;
+  c.h_pin.reserve(cb + 4 * N_FLAGS);
+  PG_HIP(hipMemcpyAsync(c.h_pin.p, c.ctrA.p, cb, hipMemcpyDeviceToHost, c.stream));
+  PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + cb, c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  return stageA_counts(c.h_pin.as<unsigned long long>(),
+                       reinterpret_cast<const unsigned*>(c.h_pin.as<uint8_t>() + cb));
+}
+
 // stage A region size for about `est` records (10 % + 512 per region of slack)
 static uint64_t region_cap(uint64_t est) { return est / NREG + est / (NREG * 10) + 512; }
 
-// ---- stages B and C over stage A's records, and sync #2.  The table gets
-// 2^bb buckets with 2^bb >= the record count (>= the key count: at most one
-// key per 2-word bucket on average), kb - 38 <= bb <= kb.
-static void finish_build(Ctx& c, const ACount& a) {
+// ---- stages B and C over stage A's records, and the build's last sync.  The
+// table gets 2^bb buckets with 2^bb >= the record count (>= the key count: at
+// most one key per 2-word bucket on average), kb - 38 <= bb <= kb.
+// spec: stage A is still in flight on the stream and `a` is a plan (region
+// capacity as the largest region, 8 regions' worth as the largest bin, the
+// last build's records-per-window ratio as the total), so stages B and C
+// are queued right behind it with no host round trip in between; stage A's
+// counts and flags come back with the same sync.  Returns false (with the
+// exact counts in `a`) if stage A overflowed a region; a B/C flag re-runs B/C
+// with the exact counts.
+static bool finish_build(Ctx& c, ACount& a, bool spec) {
   const int kb = c.kb, cb = c.cbits;
   int bb = std::max(1, log2u(std::max<uint64_t>(a.total, 1)));
   bb = std::min(std::max({bb - c.bb_shift, cb, kb - 38}), kb);
@@ -1541,16 +1552,26 @@ static void finish_build(Ctx& c, const ACount& a) {
     PG_HIP(hipGetLastError());
     c.t5.stop(c.stream);
     c.t6.stop(c.stream);
-    const size_t kbytes = 8 * RB_CTR * grid;
-    c.h_pin.reserve(kbytes + 4 * N_FLAGS);
+    const size_t kbytes = 8 * RB_CTR * grid, abytes = spec ? 8 * CSTRIDE * NREG : 0;
+    c.h_pin.reserve(kbytes + 4 * N_FLAGS + abytes);
     PG_HIP(hipMemcpyAsync(c.h_pin.p, c.k5_ctr.p, kbytes, hipMemcpyDeviceToHost, c.stream));
     PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + kbytes, c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost, c.stream));
+    if (spec)
+      PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + kbytes + 4 * N_FLAGS, c.ctrA.p, abytes, hipMemcpyDeviceToHost,
+                            c.stream));
     c.sync();
     c.ms_scan = c.t5.ms();
     c.ms_range = c.t6.ms();
     c.ms_split = c.ms_scan - c.ms_range;
     const unsigned long long* h = c.h_pin.as<unsigned long long>();
-    const unsigned bits = reinterpret_cast<const unsigned*>(c.h_pin.as<uint8_t>() + kbytes)[4];
+    const unsigned* hf = reinterpret_cast<const unsigned*>(c.h_pin.as<uint8_t>() + kbytes);
+    if (spec) {                                // stage A's exact counts, and whether it fit
+      a = stageA_counts(reinterpret_cast<const unsigned long long*>(c.h_pin.as<uint8_t>() + kbytes + 4 * N_FLAGS), hf);
+      c.sentinel = a.sentinel ? 1 : 0;
+      spec = false;
+      if (a.bits & F_A_OVER) return false;
+    }
+    const unsigned bits = hf[4];
     if (bits & F_SPLIT_OVER) { capx *= 1.5; continue; }
     if (bits & F_LDS_SPILL) {
       if (bb < kb) { ++bb; continue; }
@@ -1572,7 +1593,7 @@ static void finish_build(Ctx& c, const ACount& a) {
     c.r_ratio = a.total ? (double)nr / (double)a.total : 0.0;
     c.built = c.reduced = true;
     ++c.build_gen;
-    return;
+    return true;
   }
   throw Error(-12, "build: table overflow after resizing");
 }
@@ -1709,19 +1730,36 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   uint64_t est = c.u_ratio > 0 ? (uint64_t)(c.u_ratio * 1.25 * (double)c.windows_fw) : c.windows_fw / redund;
   est = std::min(est, c.windows_fw) + extra;
   uint64_t cap = c.region_cap_force ? c.region_cap_force : region_cap(est);
+  c.ms_clear = 0;
   ACount a;
+  // after a first build the whole build is queued at once (finish_build's
+  // spec form: one host round trip instead of two); the table is then sized
+  // from the last build's records per window, 5 % up
+  if (c.u_ratio > 0 && !c.region_cap_force) {
+    enqueue_stageA(c, cap, ntiles, rc0, extra_empty);
+    a.total = (uint64_t)(c.u_ratio * 1.05 * (double)c.windows_fw) + extra;
+    a.maxreg = cap;
+    a.maxbin = 8 * cap;
+    const bool ok = finish_build(c, a, true);
+    c.ms_insert = c.t1.ms();
+    c.n_records_a = a.total;
+    if (ok) {
+      if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
+      return;
+    }
+    cap = a.maxreg + a.maxreg / 8 + 512;           // every region's exact count is known now
+  }
   for (int attempt = 0; attempt < 3; ++attempt) {
     enqueue_stageA(c, cap, ntiles, rc0, extra_empty);
     a = stageA_read(c);
     if (!(a.bits & F_A_OVER)) break;
-    cap = a.maxreg + a.maxreg / 8 + 512;           // every region's exact count is known now
+    cap = a.maxreg + a.maxreg / 8 + 512;
   }
   if (a.bits & F_A_OVER) throw Error(-12, "build_dbg: stage A regions overflowed");
   c.ms_insert = c.t1.ms();
-  c.ms_clear = 0;
   c.sentinel = a.sentinel ? 1 : 0;
   c.n_records_a = a.total;
-  finish_build(c, a);
+  finish_build(c, a, false);
   if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
 }
 
@@ -1854,7 +1892,7 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
   c.ms_insert = c.t1.ms();
   c.sentinel = a.sentinel ? 1 : 0;
   c.n_records_a = a.total;
-  finish_build(c, a);
+  finish_build(c, a, false);
 }
 
 }  // namespace pg

@@ -114,7 +114,8 @@ struct Ctx {
   DevBuf rec_flag;                // uint8 per record: take part in the current pass
   DevBuf cls;                     // uint8 per base: class code (records concatenated)
   DevBuf scratch;                 // rocPRIM temp storage
-  DevBuf rec_pack;                // int64 [5][R]: the record table gathered for one copy
+  DevBuf rec_pack;                // the scan total + int64 [5][rec_cap]: the record table for one copy
+  uint64_t rec_cap = 0;           // record arrays sized for the last parse's record count
   PinBuf h_pin;                   // pinned staging for small device-to-host reads
   uint64_t n_lines = 0, n_records = 0, n_bases = 0, n_nl = 0;
   std::vector<int64_t> h_rec_start, h_rec_len, h_rec_hdr_start, h_rec_hdr_len, h_rec_ptr;

@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__
 __constant__ uint8_t c_byte_class[256];
 
 __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf, uint64_t n, uint64_t nspan,
-                                                 const Fn* __restrict__ incl,
+                                                 const Fn* __restrict__ incl, uint64_t rcap,
                                                  uint8_t* __restrict__ out, long long* __restrict__ rec_start,
                                                  long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
   // pending bytes (< 32) + one step's (<= WSTEP) + the fast step's fifth dword
@@ -366,13 +366,14 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
         for (uint32_t m = ls.hs; m; m &= m - 1) {
           const int jj = __builtin_ctz(m);
           const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((1u << jj) - 1u));
+          if (r >= rcap) continue;                            // the host re-runs with the exact count
           hdr_start[r] = (long long)(p + jj);
           rec_start[r] = (long long)(lane_off + __builtin_popcount(cm & ((1u << jj) - 1u)));
         }
         for (uint32_t m = term; m; m &= m - 1) {
           const int jj = __builtin_ctz(m);
           const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((2u << jj) - 1u)) - 1;
-          hdr_end[r] = (long long)(p + jj);
+          if (r < rcap) hdr_end[r] = (long long)(p + jj);
         }
       }
       // stage this step's bases after the pending bytes of chunk `cb`
@@ -421,18 +422,35 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
   }
 }
 
-__global__ void k_records(uint64_t R, unsigned long long total, long long last_line_start,
-                          long long* __restrict__ rec_start, long long* __restrict__ rec_len,
-                          long long* __restrict__ hdr, long long* __restrict__ rec_ptr) {
-  // hdr: [0, R) header start, [R, 2R) header terminator -> header length
+// The record table from the scan's total (read on the device: no host round
+// trip between the scan and the emission): record lengths, seqio's `ptr`,
+// header lengths, gathered side by side ([5][rcap] int64 after the total) for
+// one device-to-host copy.  R = the header count, clipped at rcap (the host
+// re-runs the emission when it was larger).
+__global__ void k_records(const Fn* __restrict__ tot_p, uint64_t n, uint64_t rcap,
+                          const long long* __restrict__ rec_start, const long long* __restrict__ hdr,
+                          long long* __restrict__ rec_len, long long* __restrict__ out) {
+  const Fn tot = *tot_p;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<Fn*>(out) = tot;
+  if (tot.nl == 0) return;                                    // no line at all (:126-132)
+  const uint64_t R = tot.hdr < rcap ? tot.hdr : rcap;
+  // the unterminated last line counts when end > start > 0 (:131)
+  const bool has_tail = (long long)n - 1 > tot.last + 1;
+  const long long last_line_start = has_tail ? tot.last + 1 : (tot.last2 >= 0 ? tot.last2 + 1 : 0);
+  long long* pk = out + 8;                                    // (a Fn fits in 8 words)
+  // hdr: [0, rcap) header start, [rcap, 2 rcap) header terminator
   for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R;
        r += (uint64_t)gridDim.x * blockDim.x) {
     const long long s = rec_start[r];
-    rec_len[r] = (r + 1 < R ? rec_start[r + 1] : (long long)total) - s;
-    hdr[R + r] -= hdr[r];                                     // qid = line[:-1] (:160)
+    pk[r] = s;
+    const long long len = (r + 1 < R ? rec_start[r + 1] : (long long)tot.c0) - s;
+    rec_len[r] = len;
+    pk[rcap + r] = len;
     // seqio's ptr[0] when this record is yielded: the next header line's
     // start, or the last line's start at EOF (:153, :170-172)
-    rec_ptr[r] = r + 1 < R ? hdr[r + 1] : last_line_start;
+    pk[2 * rcap + r] = r + 1 < R ? hdr[r + 1] : last_line_start;
+    pk[3 * rcap + r] = hdr[r];
+    pk[4 * rcap + r] = hdr[rcap + r] - hdr[r];                // qid = line[:-1] (:160)
   }
 }
 
@@ -452,19 +470,6 @@ static void upload_byte_class(int device) {
   t[(uint8_t)'$'] = CLS_DOLLAR;
   PG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_byte_class), t, 256));
   done |= bit;
-}
-
-// the five per-record arrays side by side, for one device-to-host copy
-__global__ void k_pack_records(uint64_t R, const long long* __restrict__ rs, const long long* __restrict__ rl,
-                               const long long* __restrict__ rp, const long long* __restrict__ hdr,
-                               long long* __restrict__ out) {
-  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < R; r += (uint64_t)gridDim.x * blockDim.x) {
-    out[r] = rs[r];
-    out[R + r] = rl[r];
-    out[2 * R + r] = rp[r];
-    out[3 * R + r] = hdr[r];
-    out[4 * R + r] = hdr[R + r];
-  }
 }
 
 void parse_fasta(Ctx& c) {
@@ -490,48 +495,50 @@ void parse_fasta(Ctx& c) {
   c.scratch.reserve(bytes + 16);
   bytes = c.scratch.cap;
   PG_HIP(rocprim::inclusive_scan(c.scratch.p, bytes, fns, incl, (size_t)nspan, FnThen{}, st));
-  c.h_pin.reserve(sizeof(Fn));
-  PG_HIP(hipMemcpyAsync(c.h_pin.p, incl + nspan - 1, sizeof(Fn), hipMemcpyDeviceToHost, st));
-  c.sync();
-  const Fn tot = *c.h_pin.as<Fn>();
+  // Emission and the record table are queued behind the scan with no host
+  // round trip: the class stream is sized by the file (bases < n), the
+  // record arrays by the last parse's record count (re-run if exceeded).
+  static_assert(sizeof(Fn) <= 64, "the total in front of the packed record table");
+  c.cls.reserve(n + 64);
+  uint64_t R = 0;
+  Fn tot{};
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const uint64_t rcap = std::max<uint64_t>(c.rec_cap, 64);
+    c.rec_start.reserve(8 * (rcap + 1));
+    c.rec_len.reserve(8 * (rcap + 1));
+    c.rec_hdr.reserve(16 * (rcap + 1));
+    c.rec_ptr.reserve(8 * (rcap + 1));
+    c.rec_flag.reserve(rcap + 1);
+    c.rec_pack.reserve(64 + 40 * rcap);
+    c.h_pin.reserve(64 + 40 * rcap);
+    auto* hdr = c.rec_hdr.as<long long>();
+    hipLaunchKernelGGL(k_emit, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, nspan, incl, rcap, c.cls.as<uint8_t>(),
+                       c.rec_start.as<long long>(), hdr, hdr + rcap);
+    PG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_records, dim3(grid_for(rcap, 256, 1024)), dim3(256), 0, st, incl + nspan - 1, n, rcap,
+                       c.rec_start.as<long long>(), hdr, c.rec_len.as<long long>(), c.rec_pack.as<long long>());
+    PG_HIP(hipGetLastError());
+    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 64 + 40 * rcap, hipMemcpyDeviceToHost, st));
+    c.sync();
+    tot = *c.h_pin.as<Fn>();
+    R = tot.nl ? tot.hdr : 0;
+    if (R <= rcap) {
+      const int64_t* pk = c.h_pin.as<int64_t>() + 8;
+      c.h_rec_start.assign(pk, pk + R);
+      c.h_rec_len.assign(pk + rcap, pk + rcap + R);
+      c.h_rec_ptr.assign(pk + 2 * rcap, pk + 2 * rcap + R);
+      c.h_rec_hdr_start.assign(pk + 3 * rcap, pk + 3 * rcap + R);
+      c.h_rec_hdr_len.assign(pk + 4 * rcap, pk + 4 * rcap + R);
+      break;
+    }
+    c.rec_cap = R;
+  }
   c.n_nl = tot.nl;
   if (tot.nl == 0) { c.parsed = true; return; }             // no line at all (:126-132)
-  // the unterminated last line counts when end > start > 0 (:131)
   const bool has_tail = (long long)n - 1 > tot.last + 1;
   c.n_lines = tot.nl + (has_tail ? 1 : 0);
-  const long long last_line_start = has_tail ? tot.last + 1 : (tot.last2 >= 0 ? tot.last2 + 1 : 0);
-  const uint64_t R = tot.hdr;
   c.n_records = R;
-  c.cls.reserve(tot.c0 + 64);
-  c.rec_start.reserve(8 * (R + 1));
-  c.rec_len.reserve(8 * (R + 1));
-  c.rec_hdr.reserve(16 * (R + 1));
-  c.rec_ptr.reserve(8 * (R + 1));
-  c.rec_flag.reserve(R + 1);
-  auto* hdr = c.rec_hdr.as<long long>();
-  hipLaunchKernelGGL(k_emit, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, nspan, incl, c.cls.as<uint8_t>(),
-                     c.rec_start.as<long long>(), hdr, hdr + R);
-  PG_HIP(hipGetLastError());
-  if (R) {
-    hipLaunchKernelGGL(k_records, dim3(grid_for(R, 256)), dim3(256), 0, st, R, tot.c0, last_line_start,
-                       c.rec_start.as<long long>(), c.rec_len.as<long long>(), hdr, c.rec_ptr.as<long long>());
-    PG_HIP(hipGetLastError());
-    c.rec_pack.reserve(40 * R);
-    c.h_pin.reserve(40 * R);
-    hipLaunchKernelGGL(k_pack_records, dim3(grid_for(R, 256, 1024)), dim3(256), 0, st, R, c.rec_start.as<long long>(),
-                       c.rec_len.as<long long>(), c.rec_ptr.as<long long>(), hdr, c.rec_pack.as<long long>());
-    PG_HIP(hipGetLastError());
-    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 40 * R, hipMemcpyDeviceToHost, st));
-  }
-  c.sync();
-  if (R) {
-    const int64_t* pk = c.h_pin.as<int64_t>();
-    c.h_rec_start.assign(pk, pk + R);
-    c.h_rec_len.assign(pk + R, pk + 2 * R);
-    c.h_rec_ptr.assign(pk + 2 * R, pk + 3 * R);
-    c.h_rec_hdr_start.assign(pk + 3 * R, pk + 4 * R);
-    c.h_rec_hdr_len.assign(pk + 4 * R, pk + 5 * R);
-  }
+  c.rec_cap = std::max(c.rec_cap, R);
   uint64_t nb = 0;
   for (uint64_t r = 0; r < R; ++r) nb += (uint64_t)c.h_rec_len[r];
   c.n_bases = nb;
