@@ -107,10 +107,11 @@ __device__ __forceinline__ void init_keys(const uint8_t* sc, uint32_t o, int k, 
   uint32_t lo = 0, rlo = 0;
   uint64_t hi = 0, rhi = 0;
   const int kl = k < 13 ? k : 13, kh = k - kl;
-  for (int j = kl - 1; j >= 0; --j) lo = lo * 5u + digit_fw(sc[o + j]);
-  for (int j = k - 1; j >= kl; --j) hi = hi * 5u + digit_fw(sc[o + j]);
-  for (int j = 0; j < kh; ++j) rhi = rhi * 5u + digit_rc(sc[o + j]);
-  for (int j = kh; j < k; ++j) rlo = rlo * 5u + digit_rc(sc[o + j]);
+  auto S = [&](int j) { return (uint32_t)sc[o + j]; };
+  for (int j = kl - 1; j >= 0; --j) lo = lo * 5u + digit_fw(S(j));
+  for (int j = k - 1; j >= kl; --j) hi = hi * 5u + digit_fw(S(j));
+  for (int j = 0; j < kh; ++j) rhi = rhi * 5u + digit_rc(S(j));
+  for (int j = kh; j < k; ++j) rlo = rlo * 5u + digit_rc(S(j));
   K = (uint64_t)lo + hi * 1220703125ull;         // 5^13
   Kr = (uint64_t)rlo + rhi * 1220703125ull;
 }
@@ -344,10 +345,15 @@ template <int ND>
 __device__ __forceinline__ void lds_bytes16(const uint8_t* s, uint32_t idx, uint32_t (&out)[ND]) {
   constexpr int NW = ((ND + 3) / 4 + 1) * 4;       // dwords read: ceil(ND/4)+1 chunks of 16 B
   uint32_t raw[NW];
-  const uint32_t a = idx & ~15u;
+  // Whole 16-byte reads, pinned as such: left alone, the compiler sinks them
+  // into the switch below and narrows each to the dwords its case uses,
+  // ds_read2_b32 pairs whose 32-lane banking makes the 16-byte-strided lanes
+  // 4-way conflicted (822 conflict cycles per k_cover wave, PMC)
+  const uint4* s16 = reinterpret_cast<const uint4*>(__builtin_assume_aligned(s, 16));
 #pragma unroll
   for (int q = 0; q < NW / 4; ++q) {
-    const uint4 v = *reinterpret_cast<const uint4*>(s + a + 16u * q);
+    uint4 v = s16[(idx >> 4) + (uint32_t)q];
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
     raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
   }
   const uint32_t sb = idx & 3u;
@@ -590,7 +596,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
     }
   }
   __syncthreads();
-  if (dm0) cover_search(s_cls, s_ref, s_geo, rg[0], rg[1], s_best, qt, dm0, dm1);     // (block-uniform)
+  if (dm0 && !(PG_EXP_BITS & 32)) cover_search(s_cls, s_ref, s_geo, rg[0], rg[1], s_best, qt, dm0, dm1);
   // hints and drift sets: one lane per (member, reference)
   if (threadIdx.x < 2 * QM) {
     const int m = threadIdx.x >> 1, ri = threadIdx.x & 1;
@@ -612,7 +618,7 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
     const MemGeo& G = s_geo[m];
     const long long last = G.rn - k;
     uint32_t covered = 0;
-    if (((dm0 >> m) & 1u) && q0 > 0 && q0 + IW <= last) {
+    if (!(PG_EXP_BITS & 64) && ((dm0 >> m) & 1u) && q0 > 0 && q0 + IW <= last) {
       const uint32_t o = (uint32_t)(G.rs - G.a0 + q0 - 1);
       uint32_t Gb[NB];
       lds_bytes16(s_cls[m], o, Gb);
@@ -696,10 +702,15 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
             const unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift,
             TableView T, BinOut O) {
   static_assert(NQ == 64, "one wave scans the sub-queue counts");
-  // 16-byte front pad + 64 staged bytes per thread (the realigning dword reads
-  // past them land in the next row, or read 0 past the allocation); 20 KiB so
-  // that a work block fits beside the coverage blocks of the next chunk
-  __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][80];
+  // 16-byte front pad + 64 staged bytes + 4 per thread: rows of 21 dwords, an
+  // odd stride, so the rows' dword reads are bank-conflict free (80-byte rows
+  // were 4-way conflicted: 1847 conflict cycles per wave, PMC); the realigning
+  // dword reads past a row land in the next one, or read 0 past the
+  // allocation; 21 KiB so that a work block fits beside the coverage blocks of
+  // the next chunk
+  constexpr int SROW = 84;
+  static_assert(SROW % 8 == 4, "odd dword stride");
+  __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][SROW];
   __shared__ unsigned long long s_pre[NQ + 1];
   __shared__ uint32_t s_cnt[NBIN];
   __shared__ unsigned long long s_base[NBIN];
@@ -730,9 +741,12 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
         if (s_pre[lo + step] <= i) lo += step;
       const WorkItem w = queue[(unsigned long long)lo * qcap + (i - s_pre[lo])];
       const long long from = w.rs + w.q0 - 2, aligned = from > 0 ? from & ~15ll : 0;
+      uint32_t* s32 = reinterpret_cast<uint32_t*>(slot);          // (4-byte aligned rows)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        *reinterpret_cast<uint4*>(slot + 16 * j) = *reinterpret_cast<const uint4*>(cls + aligned + 16 * j);
+      for (int j = 0; j < 4; ++j) {
+        const uint4 v = *reinterpret_cast<const uint4*>(cls + aligned + 16 * j);
+        s32[4 * j] = v.x; s32[4 * j + 1] = v.y; s32[4 * j + 2] = v.z; s32[4 * j + 3] = v.w;
+      }
       segment_records<RC>(slot, w.rs - aligned, w.q0, w.last, k, shift, T, w.covered, hh, mm);
     } else {
 #pragma unroll
