@@ -249,8 +249,7 @@ def main():
         for _ in range(3):
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            ctx.set_fasta_host_ptr(host0.data_ptr(), host0.numel())
-            ctx.parse()
+            ctx.parse_host_ptr(host0.data_ptr(), host0.numel())      # chunked H2D under K1
             ctx.build(None, 0, True)
             ts.append(time.perf_counter() - t1)
         host_ms = 1e3 * min(ts)
@@ -342,6 +341,8 @@ def main():
         out["path"]["host_to_rdbg_ms"] = round(host_ms, 3)
         out["path"]["host_to_rdbg_gbps"] = round(per_batch[0] / host_ms / 1e6, 3)
         out["path"]["h2d_pinned_gbs"] = round(h2d_gbs, 2)
+        # the PCIe bound of that window: the FASTA's bare pinned H2D time
+        out["path"]["host_to_rdbg_frac_of_pcie_bound"] = round(nbytes[0] / (h2d_gbs * 1e9) / (host_ms * 1e-3), 4)
     if parity is not None:
         out["parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -73,6 +73,13 @@ int pg_set_fasta_device(pg_ctx* ctx, const uint8_t* device_bytes, uint64_t nbyte
 
 /* K1: readline_jit_ + seqio_jit_ (kmer_numba.py:122-172) on the device. */
 int pg_parse(pg_ctx* ctx, uint64_t* n_records, uint64_t* n_bases);
+/* pg_set_fasta + pg_parse for host bytes in one call (seq2bytes + seqio_jit_,
+ * :117-172): the copy to HBM goes in chunks (PG_TUNE_H2D_CHUNK, 64 MiB) on a
+ * side stream and K1 runs on each chunk once it has landed, so the parse of
+ * all but the last chunk hides under the PCIe transfer (pinned host memory
+ * makes the copies plain DMA).  The bytes are read until the call returns. */
+int pg_parse_host(pg_ctx* ctx, const uint8_t* host_bytes, uint64_t nbytes, uint64_t* n_records,
+                  uint64_t* n_bases);
 /* Per-record table (arrays of n_records): compacted sequence length, header
  * byte span (qid = bytes[hdr_start : hdr_start+hdr_len], '>' included,
  * :160) and seqio's resume pointer (:153). Any pointer may be NULL. */
@@ -174,6 +181,9 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 /* PG_TUNE_REGION_CAP: first stage A region size in records (0 = estimated):
  * a small value exercises the stage A re-run (results are unchanged). */
 #define PG_TUNE_REGION_CAP 3
+/* PG_TUNE_H2D_CHUNK: bytes per pg_parse_host chunk, rounded down to whole
+ * 16 KiB K1 spans (0 = 64 MiB): small values exercise the pipeline. */
+#define PG_TUNE_H2D_CHUNK 4
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Timings and counters of the last build (see pg_stats). */

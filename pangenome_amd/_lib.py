@@ -18,6 +18,7 @@ PG_OK = 0
 PG_TUNE_K3_CHUNKS = 1
 PG_TUNE_BUCKET_SHIFT = 2
 PG_TUNE_REGION_CAP = 3
+PG_TUNE_H2D_CHUNK = 4
 
 
 class PgStats(C.Structure):
@@ -46,6 +47,7 @@ SIGNATURES = {
     "pg_set_fasta": (C.c_int, [_P, _P, C.c_uint64]),
     "pg_set_fasta_device": (C.c_int, [_P, _P, C.c_uint64]),
     "pg_parse": (C.c_int, [_P, _U64P, _U64P]),
+    "pg_parse_host": (C.c_int, [_P, _P, C.c_uint64, _U64P, _U64P]),
     "pg_records": (C.c_int, [_P, _P, _P, _P, _P]),
     "pg_build_dbg": (C.c_int, [_P, _P, C.c_int, C.c_int, _SP]),
     "pg_build_rdbg": (C.c_int, [_P, _U64P, _SP]),
@@ -152,6 +154,20 @@ class Context:
     def parse(self):
         nr, nb = C.c_uint64(), C.c_uint64()
         check(self.lib.pg_parse(self.h, C.byref(nr), C.byref(nb)), "pg_parse")
+        self.n_records, self.n_bases = nr.value, nb.value
+        return self.n_records, self.n_bases
+
+    def parse_host(self, data):
+        """set_fasta + parse of host bytes in one call: chunked H2D pipelined
+        with K1 (pg_parse_host)."""
+        arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        return self.parse_host_ptr(arr.ctypes.data if arr.shape[0] else None, arr.shape[0])
+
+    def parse_host_ptr(self, host_ptr, nbytes: int):
+        """parse_host from a raw address (e.g. a pinned torch tensor's data_ptr())."""
+        nr, nb = C.c_uint64(), C.c_uint64()
+        check(self.lib.pg_parse_host(self.h, C.c_void_p(host_ptr), nbytes, C.byref(nr), C.byref(nb)),
+              "pg_parse_host")
         self.n_records, self.n_bases = nr.value, nb.value
         return self.n_records, self.n_bases
 

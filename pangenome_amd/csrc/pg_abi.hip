@@ -132,6 +132,23 @@ int pg_set_fasta_device(pg_ctx* x, const uint8_t* dev, uint64_t n) {
   });
 }
 
+int pg_parse_host(pg_ctx* x, const uint8_t* host, uint64_t n, uint64_t* n_records, uint64_t* n_bases) {
+  return guard([&] {
+    if (!x || (!host && n)) throw pg::Error(PG_EINVAL, "pg_parse_host: bad arguments");
+    pg::Ctx& c = x->c;
+    PG_HIP(hipSetDevice(c.device));
+    auto t0 = std::chrono::steady_clock::now();
+    c.fasta_own.reserve(n + 64);
+    c.d_fasta = c.fasta_own.as<uint8_t>();
+    c.n_bytes = n;
+    c.parsed = c.built = c.reduced = false;
+    pg::parse_fasta(c, host);
+    c.ms_parse = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (n_records) *n_records = c.n_records;
+    if (n_bases) *n_bases = c.n_bases;
+  });
+}
+
 int pg_parse(pg_ctx* x, uint64_t* n_records, uint64_t* n_bases) {
   return guard([&] {
     if (!x) throw pg::Error(PG_EINVAL, "pg_parse: ctx is NULL");
@@ -204,6 +221,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
       case PG_TUNE_REGION_CAP:
         if (value < 0) throw pg::Error(PG_EINVAL, "pg_tune: region size must be >= 0");
         x->c.region_cap_force = (uint64_t)value;
+        break;
+      case PG_TUNE_H2D_CHUNK:
+        if (value < 0) throw pg::Error(PG_EINVAL, "pg_tune: H2D chunk must be >= 0");
+        x->c.h2d_chunk = value ? (uint64_t)value : (64ull << 20);
         break;
       default:
         throw pg::Error(PG_EINVAL, "pg_tune: unknown parameter " + std::to_string(what));

@@ -98,6 +98,7 @@ struct Ctx {
   hipEvent_t ev[16] = {};         // ordering events between the two streams
   int n_cu = 256;                 // compute units (persistent-kernel grids)
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
+  uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
   int bb_shift = 0;               // pg_tune: table bits below the sized ones (tests of the overflow paths)
   uint64_t region_cap_force = 0;  // pg_tune: first stage A region size (tests of the re-run path)
 
@@ -195,7 +196,7 @@ struct Ctx {
 };
 
 // pg_parse.hip
-void parse_fasta(Ctx& c);
+void parse_fasta(Ctx& c, const uint8_t* h_src = nullptr);
 // pg_dbg.hip
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0);
 void build_rdbg(Ctx& c);

@@ -202,10 +202,10 @@ __device__ __forceinline__ void load_span(const uint8_t* buf, uint64_t p0, uint6
   }
 }
 
-__global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__ buf, uint64_t n,
+__global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
                                                      uint64_t nspan, Fn* __restrict__ out) {
   const int lane = threadIdx.x & 63;
-  const uint64_t span = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  const uint64_t span = span0 + (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
   if (span >= nspan) return;                                  // wave-uniform
   const uint64_t p0 = span * WSPAN;
   uint4 v[WSTEPS];
@@ -276,7 +276,8 @@ __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__
 
 __constant__ uint8_t c_byte_class[256];
 
-__global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf, uint64_t n, uint64_t nspan,
+__global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
+                                                 uint64_t nspan,
                                                  const Fn* __restrict__ incl, uint64_t rcap,
                                                  uint8_t* __restrict__ out, long long* __restrict__ rec_start,
                                                  long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
@@ -287,7 +288,7 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
   lut[threadIdx.x] = c_byte_class[threadIdx.x];
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const uint64_t span = (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  const uint64_t span = span0 + (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
   if (span >= nspan) return;                                  // wave-uniform, after the only barrier
   uint8_t* stage = stage_all[threadIdx.x >> 6];
   auto wave_sync = []() {
@@ -472,7 +473,11 @@ static void upload_byte_class(int device) {
   done |= bit;
 }
 
-void parse_fasta(Ctx& c) {
+// Host input (h_src != NULL): the FASTA goes up in chunks of whole spans on
+// the side stream, and K1 works on each chunk as soon as it has landed -
+// span functions, the scan of every span so far, the emission of the chunk's
+// spans - so only the last chunk's K1 follows the copy.
+void parse_fasta(Ctx& c, const uint8_t* h_src) {
   upload_byte_class(c.device);
   hipStream_t st = c.stream;
   const uint64_t n = c.n_bytes;
@@ -488,22 +493,16 @@ void parse_fasta(Ctx& c) {
   c.span_start.reserve(sizeof(Fn) * nspan);
   auto* fns = c.span_sum.as<Fn>();
   auto* incl = c.span_start.as<Fn>();
-  hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, nspan, fns);
-  PG_HIP(hipGetLastError());
   size_t bytes = 0;
   PG_HIP(rocprim::inclusive_scan(nullptr, bytes, fns, incl, (size_t)nspan, FnThen{}, st));
   c.scratch.reserve(bytes + 16);
-  bytes = c.scratch.cap;
-  PG_HIP(rocprim::inclusive_scan(c.scratch.p, bytes, fns, incl, (size_t)nspan, FnThen{}, st));
-  // Emission and the record table are queued behind the scan with no host
-  // round trip: the class stream is sized by the file (bases < n), the
-  // record arrays by the last parse's record count (re-run if exceeded).
-  static_assert(sizeof(Fn) <= 64, "the total in front of the packed record table");
+  auto scan = [&](uint64_t upto) {
+    size_t b = c.scratch.cap;
+    PG_HIP(rocprim::inclusive_scan(c.scratch.p, b, fns, incl, (size_t)upto, FnThen{}, st));
+  };
   c.cls.reserve(n + 64);
-  uint64_t R = 0;
-  Fn tot{};
-  for (int attempt = 0; attempt < 2; ++attempt) {
-    const uint64_t rcap = std::max<uint64_t>(c.rec_cap, 64);
+  const uint64_t rcap0 = std::max<uint64_t>(c.rec_cap, 64);
+  auto reserve_records = [&](uint64_t rcap) {
     c.rec_start.reserve(8 * (rcap + 1));
     c.rec_len.reserve(8 * (rcap + 1));
     c.rec_hdr.reserve(16 * (rcap + 1));
@@ -511,10 +510,48 @@ void parse_fasta(Ctx& c) {
     c.rec_flag.reserve(rcap + 1);
     c.rec_pack.reserve(64 + 40 * rcap);
     c.h_pin.reserve(64 + 40 * rcap);
+  };
+  auto emit = [&](uint64_t s0, uint64_t s1, uint64_t rcap) {
     auto* hdr = c.rec_hdr.as<long long>();
-    hipLaunchKernelGGL(k_emit, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, nspan, incl, rcap, c.cls.as<uint8_t>(),
-                       c.rec_start.as<long long>(), hdr, hdr + rcap);
+    hipLaunchKernelGGL(k_emit, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta, n, s0,
+                       s1, incl, rcap, c.cls.as<uint8_t>(), c.rec_start.as<long long>(), hdr, hdr + rcap);
     PG_HIP(hipGetLastError());
+  };
+  reserve_records(rcap0);
+  if (h_src) {
+    const uint64_t C = std::max<uint64_t>(WSPAN, c.h2d_chunk / WSPAN * WSPAN);
+    int e = 0;
+    for (uint64_t off = 0; off < n; off += C, e = (e + 1) & 15) {
+      const uint64_t len = std::min(C, n - off);
+      const uint64_t s0 = off / WSPAN, s1 = std::min(nspan, (off + len + WSPAN - 1) / WSPAN);
+      PG_HIP(hipMemcpyAsync(c.fasta_own.as<uint8_t>() + off, h_src + off, len, hipMemcpyHostToDevice, c.stream2));
+      PG_HIP(hipEventRecord(c.ev[e], c.stream2));
+      PG_HIP(hipStreamWaitEvent(st, c.ev[e], 0));
+      hipLaunchKernelGGL(k_span_sum, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta,
+                         n, s0, s1, fns);
+      PG_HIP(hipGetLastError());
+      scan(s1);
+      emit(s0, s1, rcap0);
+    }
+  } else {
+    hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
+    PG_HIP(hipGetLastError());
+    scan(nspan);
+    emit(0, nspan, rcap0);
+  }
+  // Emission and the record table are queued behind the scan with no host
+  // round trip: the class stream is sized by the file (bases < n), the
+  // record arrays by the last parse's record count (re-run if exceeded).
+  static_assert(sizeof(Fn) <= 64, "the total in front of the packed record table");
+  uint64_t R = 0;
+  Fn tot{};
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    const uint64_t rcap = attempt ? std::max<uint64_t>(c.rec_cap, 64) : rcap0;
+    if (attempt) {                                            // the exact record count: emission again
+      reserve_records(rcap);
+      emit(0, nspan, rcap);
+    }
+    auto* hdr = c.rec_hdr.as<long long>();
     hipLaunchKernelGGL(k_records, dim3(grid_for(rcap, 256, 1024)), dim3(256), 0, st, incl + nspan - 1, n, rcap,
                        c.rec_start.as<long long>(), hdr, c.rec_len.as<long long>(), c.rec_pack.as<long long>());
     PG_HIP(hipGetLastError());

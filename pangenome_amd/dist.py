@@ -268,8 +268,7 @@ class GpuShard:
         self.ctx = Context(k, device)
 
     def load(self, data):
-        self.ctx.set_fasta(data)
-        self.ctx.parse()
+        self.ctx.parse_host(data)
         return self.ctx.records()
 
     def stage(self, keys, masks=None, counts=None):

@@ -77,8 +77,7 @@ class DeviceGraph:
         self.k = min(max(1, int(kmer)), 27)                    # :1236
         self.buf = seq2bytes(qry) if data is None else data
         self.ctx = Context(self.k, device)
-        self.ctx.set_fasta(self.buf)
-        self.ctx.parse()
+        self.ctx.parse_host(self.buf)            # H2D in chunks, pipelined with K1
         rec = self.ctx.records()
         self.seq_len, self.hdr_start, self.hdr_len = rec["seq_len"], rec["hdr_start"], rec["hdr_len"]
         self.rec_ptr = rec["ptr"]

@@ -142,3 +142,31 @@ def test_parse_fast_steps(oracle_mod, widths):
     _check(_mixed_fasta(sum(widths), widths), oracle_mod)
     # unterminated last line, and a record longer than a 16 KiB span
     _check(_mixed_fasta(7, widths, nrec=3, reclen=50_000)[:-1], oracle_mod)
+
+
+@pytest.mark.parametrize("chunk", [16 * 1024, 3 * 16 * 1024, 0])
+def test_parse_host_pipelined(oracle_mod, chunk):
+    """pg_parse_host: the upload in chunks of whole K1 spans on a side stream,
+    K1 on each chunk as it lands.  Same record table and class stream (via the
+    k=5 dBG) as the one-shot upload, with chunk edges on every span edge."""
+    from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK
+    # (> 64 records: the first parse of a context re-runs the emission with the exact record count)
+    buf = _mixed_fasta(3, (60, 17), nrec=70, reclen=3_000) + CASES["empty_records"] + _long_cases()["long_header"]
+    ref = Context(5)
+    ref.set_fasta(buf)
+    rr = ref.parse()
+    rrec = ref.records()
+    ref.build_dbg(None, 0, True)
+    rk, rm = ref.dbg()
+    ref.close()
+    ctx = Context(5)
+    ctx.tune(PG_TUNE_H2D_CHUNK, chunk)
+    for _ in range(2):                              # the second parse reuses the record capacity
+        assert ctx.parse_host(buf) == rr
+        got = ctx.records()
+        for key in rrec:
+            assert np.array_equal(got[key], rrec[key]), key
+        ctx.build_dbg(None, 0, True)
+        keys, masks = ctx.dbg()
+        assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
+    ctx.close()
