@@ -128,6 +128,8 @@ def main():
     ap.add_argument("--config", default="c3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", action="store_true", help="CPU baseline on 12 of the 100 C3 genomes (~12 s)")
+    ap.add_argument("--no-host-window", action="store_true",
+                    help="skip the host-resident window (profiler runs: its chunked K1 dispatches)")
     args = ap.parse_args()
 
     import torch
@@ -244,7 +246,7 @@ def main():
     # ---- host-resident input (BASELINE.md §3 window): pinned host FASTA ->
     # H2D -> parse -> build -> rdBG count on the host; and the bare H2D rate
     host_ms, h2d_gbs = None, None
-    if world == 1:
+    if world == 1 and not args.no_host_window:
         ts = []
         for _ in range(3):
             torch.cuda.synchronize()

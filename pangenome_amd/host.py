@@ -92,13 +92,18 @@ def _resumed_records(pos: int, R: int, shape: FileShape):
 
 
 def plan_dbg(seq_len: np.ndarray, shape: FileShape, rc0: bool, Ns: int, chunk: int = CHUNK,
-             resume: int | None = None):
+             resume: int | None = None, checkpoint: bool = False):
     """seq2rdbg (:1251-1266) over seq2dbg_jit_ (:1204-1230): which records the
     dBG pass inserts, and how many extra empty records it meets.  `resume`
-    is the record a -r checkpoint restarts at (resume_position)."""
+    is the record a -r checkpoint restarts at (resume_position).  With
+    `checkpoint`, also the state of the last `<in>_db_brkpt.npz` dump
+    (:1255-1259; each dump overwrites the previous one): (flags, extra,
+    record) of the records inserted when it was written and the record whose
+    seqio ptr is its offset - or None when no pass crossed `chunk`."""
     R = seq_len.shape[0]
     flags = np.zeros(R, np.uint8)
     extra = 0
+    ckpt = None
     mult = 2 if rc0 else 1
     recs = list(range(R)) if not resume else _resumed_records(resume, R, shape)
     N = 0
@@ -120,20 +125,25 @@ def plan_dbg(seq_len: np.ndarray, shape: FileShape, rc0: bool, Ns: int, chunk: i
                 break
         if done != -1:
             break
+        ckpt = (flags.copy(), extra, last)
         recs = _resumed_records(last + 1, R, shape)
         N += Nl
         if ns_hit(N, Ns):
             break
-    return flags, extra
+    return (flags, extra, ckpt) if checkpoint else (flags, extra)
 
 
-def plan_edges(seq_len: np.ndarray, shape: FileShape, Ns: int, chunk: int = CHUNK, resume: int | None = None):
+def plan_edges(seq_len: np.ndarray, shape: FileShape, Ns: int, chunk: int = CHUNK, resume: int | None = None,
+               checkpoint: bool = False):
     """seq2graph (:1876-1890) over rdbg_edge_weight_jit_ (:1809-1827): walked
     records and, per record, the checkpoint segment it belongs to.  `resume`
-    is the record a -R checkpoint restarts at (resume_position)."""
+    is the record a -R checkpoint restarts at (resume_position).  With
+    `checkpoint`, also the record whose seqio ptr is the offset of the last
+    `<in>_rdb_brkpt.npz` dump (:1880-1887), or None (no checkpoint)."""
     R = seq_len.shape[0]
     flags = np.zeros(R, np.uint8)
     segment = np.full(R, -1, np.int64)
+    ckpt = None
     recs = list(range(R)) if not resume else _resumed_records(resume, R, shape)
     N = 0
     seg = 0
@@ -156,9 +166,10 @@ def plan_edges(seq_len: np.ndarray, shape: FileShape, Ns: int, chunk: int = CHUN
         if done != -1:
             break
         n_checkpoints += 1
+        ckpt = last
         seg += 1
         recs = _resumed_records(last + 1, R, shape)
-    return flags, segment, n_checkpoints
+    return (flags, segment, n_checkpoints, ckpt) if checkpoint else (flags, segment, n_checkpoints)
 
 
 def plan_rows(seq_len: np.ndarray, shape: FileShape, buf, Ns: int):
@@ -324,6 +335,16 @@ def resume_position(offset: int, rec_ptr: np.ndarray) -> int:
     if hit.shape[0] == 0:
         raise ValueError("checkpoint offset %d is not a record boundary of this input" % offset)
     return int(hit[0]) + 1
+
+
+def write_edge_npz(fn: str, tuples, counts, offset: int):
+    """dump(jit=True, ksize=4, vsize=1) of the edge Dict (:243-250): parameters
+    [4, 1, offset], then dict2array's popitem order (:221-235) - the Dict's
+    iteration order reversed.  `tuples` / `counts` are in iteration order."""
+    fn = fn[:-4] if fn.endswith(".npz") else fn
+    t = np.ascontiguousarray(np.asarray(tuples, dtype=np.uint64)[::-1]).reshape(-1)
+    c = np.ascontiguousarray(np.asarray(counts)[::-1]).astype(np.uint64)
+    np.savez(fn, parameters=np.asarray([4, 1, offset], dtype=np.uint64), keys=t, values=c)
 
 
 def read_edge_npz(fn: str):

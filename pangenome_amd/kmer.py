@@ -101,9 +101,11 @@ class DeviceGraph:
 def seq2rdbg(qry, kmer=13, bits=5, Ns=1e6, chunk=2 ** 32, brkpt="./breakpoint", saved="dBG_disk",
              hashfunc=None, jit=True, rc=True, device=0):
     """:1234-1268.  Returns the device dBG.  An existing `brkpt` npz (-r) is
-    the table so far plus the offset to resume at (:1239-1241).  The GPU
-    build does not write `<in>_db_brkpt.npz` / `<in>_rdb_brkpt.npz`
-    checkpoints itself (they appear past 2^33 bases); it reads both."""
+    the table so far plus the offset to resume at (:1239-1241).  When a pass
+    crosses `chunk` bases the reference dumps the table so far to
+    `<in>_db_brkpt.npz` (:1255-1259, each dump replacing the last); here the
+    last such state is built, dumped and written once, then the whole build
+    runs."""
     if seq_chk(qry) != "fasta":
         raise ValueError("%s: only FASTA input is supported (the reference's FASTQ branch is "
                          "broken, kmer_numba.py:174-186)" % qry)
@@ -113,7 +115,13 @@ def seq2rdbg(qry, kmer=13, bits=5, Ns=1e6, chunk=2 ** 32, brkpt="./breakpoint", 
         offset, keys, values, counts = host.read_db_npz(brkpt)
         g.ctx.dbg_load(keys, values, counts)
         resume = host.resume_position(offset, g.rec_ptr)
-    flags, extra = host.plan_dbg(g.seq_len, g.shape, bool(rc), int(Ns), int(chunk), resume=resume)
+    flags, extra, ckpt = host.plan_dbg(g.seq_len, g.shape, bool(rc), int(Ns), int(chunk), resume=resume,
+                                       checkpoint=True)
+    if ckpt is not None:
+        cf, ce, last = ckpt
+        g.ctx.build_dbg(cf, ce, bool(rc))
+        cap, size, keys, values, counts = g.ctx.dbg_dump()
+        host.write_db_npz(qry + "_db_brkpt", cap, size, keys, values, counts, offset=int(g.rec_ptr[last]))
     g.stats = g.ctx.build_dbg(flags, extra, bool(rc))
     return g
 
@@ -150,12 +158,22 @@ def rdbg_edges(g: DeviceGraph, Ns, chunk, rc, brkpt=""):
     if brkpt and os.path.isfile(brkpt):
         offset, lt, lc = host.read_edge_npz(brkpt)
         loaded, resume = (lt, lc), host.resume_position(offset, g.rec_ptr)
-    flags, segment, ncp = host.plan_edges(g.seq_len, g.shape, int(Ns), int(chunk), resume=resume)
-    tuples, counts, walk_first = g.ctx.edges(flags, bool(rc))
-    if loaded is not None:
-        return host.merge_edges(loaded[0], loaded[1], tuples, counts, walk_first, segment, ncp)
-    order = host.edge_order(walk_first, segment, ncp)
-    return tuples[order], counts[order]
+    flags, segment, ncp, ckpt = host.plan_edges(g.seq_len, g.shape, int(Ns), int(chunk), resume=resume,
+                                                checkpoint=True)
+
+    def state(fl, upto):                          # the Dict after segments 0..upto, in iteration order
+        tuples, counts, walk_first = g.ctx.edges(fl, bool(rc))
+        if loaded is not None:
+            return host.merge_edges(loaded[0], loaded[1], tuples, counts, walk_first, segment, upto)
+        order = host.edge_order(walk_first, segment, upto)
+        return tuples[order], counts[order]
+    if ckpt is not None:
+        # the last `<in>_rdb_brkpt.npz` dump (:1880-1887): the Dict after the
+        # segments before the last checkpoint, each dump replacing the last
+        last_seg = ncp - 1
+        t, c = state((flags.astype(bool) & (segment <= last_seg)).astype(np.uint8), last_seg)
+        host.write_edge_npz(g.qry + "_rdb_brkpt", t, c, int(g.rec_ptr[ckpt]))
+    return state(flags, ncp)
 
 
 def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_dict=None, saved=None,

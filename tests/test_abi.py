@@ -67,6 +67,33 @@ def test_plan_dbg_checkpoints():
     assert f.tolist() == [1, 1, 1, 1]
 
 
+def test_plan_checkpoint_states():
+    """The state of the last <in>_db_brkpt / <in>_rdb_brkpt dump (:1255-1259,
+    :1880-1887): records inserted when it was written, and the record whose
+    seqio ptr is its offset; None without a checkpoint."""
+    from pangenome_amd import host
+    lens = np.array([10, 10, 10, 10], np.int64)
+    shape_gt = host.FileShape(ord(">"), True, 0, False)
+    f, extra, ck = host.plan_dbg(lens, shape_gt, True, 2 ** 63, chunk=25, checkpoint=True)
+    assert f.tolist() == [1, 1, 1, 1] and extra == 1
+    cf, ce, last = ck                                          # dumps after records 1 and 3: the last wins
+    assert cf.tolist() == [1, 1, 1, 1] and ce == 0 and last == 3
+    f, _, ck = host.plan_dbg(lens, shape_gt, True, 2 ** 63, chunk=45, checkpoint=True)
+    assert ck[0].tolist() == [1, 1, 1, 0] and ck[2] == 2
+    assert host.plan_dbg(lens, shape_gt, True, 2 ** 63, checkpoint=True)[2] is None
+    f, seg, ncp, last = host.plan_edges(lens, shape_gt, 2 ** 63, chunk=15, checkpoint=True)
+    assert seg.tolist() == [0, 0, 1, 1] and ncp == 2 and last == 3     # dumps after records 1 and 3
+    assert host.plan_edges(lens, shape_gt, 2 ** 63, checkpoint=True)[3] is None
+
+
+def test_write_edge_npz_popitem_order(tmp_path):
+    from pangenome_amd import host
+    t = np.arange(12, dtype=np.uint64).reshape(3, 4)
+    host.write_edge_npz(str(tmp_path / "e"), t, np.array([5, 6, 7]), 99)
+    off, lt, lc = host.read_edge_npz(str(tmp_path / "e.npz"))
+    assert off == 99 and lt.tolist() == t[::-1].tolist() and lc.tolist() == [7, 6, 5]
+
+
 def test_plan_edges_and_rows():
     from pangenome_amd import host
     lens = np.array([10, 10, 10], np.int64)

@@ -147,3 +147,38 @@ def test_cli_resumes_reference_checkpoint(name, tmp_path):
         assert np.array_equal(z["keys"][sel][o], fx.graph["dbg_keys"])
         assert np.array_equal(z["values"][sel][o], fx.graph["dbg_masks"])
         assert np.array_equal(z["counts"][sel][o], fx.graph["dbg_counts"])
+
+
+@pytest.mark.parametrize("name", __import__("golden_util").resume_names())
+def test_writes_reference_checkpoint(name, tmp_path):
+    """The mid-run checkpoint side files: a pass crossing `chunk` bases dumps
+    the state so far to <in>_db_brkpt.npz (seq2rdbg :1255-1259) or
+    <in>_rdb_brkpt.npz (seq2graph :1880-1887); the file left behind equals
+    the one the reference itself wrote with the same chunk (the fixture's
+    brkpt.npz): oakht parameters and slot contents, or the edge Dict in
+    popitem order with its walk counts and offset."""
+    from golden_util import ResumeFixture
+    from pangenome_amd import kmer
+    fx = ResumeFixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    ref = np.load(fx.brkpt)
+    chunk = int(fx.meta["chunk"])
+    if fx.flag == "-r":
+        kmer.seq2rdbg(str(q), fx.k, 5, 2 ** 63, brkpt="", chunk=chunk, rc=(fx.c >> 1) == 1)
+        z = np.load(str(q) + "_db_brkpt.npz")
+        assert z["parameters"].tolist() == ref["parameters"].tolist()
+        sel, rsel = z["counts"] > 0, ref["counts"] > 0
+        o, ro = np.argsort(z["keys"][sel], kind="stable"), np.argsort(ref["keys"][rsel], kind="stable")
+        assert np.array_equal(z["keys"][sel][o], ref["keys"][rsel][ro])
+        assert np.array_equal(z["values"][sel][o], ref["values"][rsel][ro])
+        assert np.array_equal(z["counts"][sel][o], ref["counts"][rsel][ro])
+    else:
+        g = kmer.seq2rdbg(str(q), fx.k, 5, 2 ** 63, brkpt="", chunk=2 ** 33, rc=(fx.c >> 1) == 1)
+        kmer.dbg2rdbg(g)
+        kmer.seq2graph(str(q), kmer=fx.k, bits=5, Ns=2 ** 63, rdbg_dict=g, chunk=chunk, brkpt="",
+                       rc=(fx.c & 1) == 1, out=io.StringIO())
+        z = np.load(str(q) + "_rdb_brkpt.npz")
+        for a in ("parameters", "keys", "values"):
+            assert z[a].tolist() == ref[a].tolist(), a
