@@ -702,14 +702,14 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
             const unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift,
             TableView T, BinOut O) {
   static_assert(NQ == 64, "one wave scans the sub-queue counts");
-  // 16-byte front pad + 64 staged bytes + 4 per thread: rows of 21 dwords, an
-  // odd stride, so the rows' dword reads are bank-conflict free (80-byte rows
-  // were 4-way conflicted: 1847 conflict cycles per wave, PMC); the realigning
-  // dword reads past a row land in the next one, or read 0 past the
-  // allocation; 21 KiB so that a work block fits beside the coverage blocks of
-  // the next chunk
-  constexpr int SROW = 84;
-  static_assert(SROW % 8 == 4, "odd dword stride");
+  // 64 staged bytes + 4 per thread: rows of 17 dwords, an odd stride, so the
+  // rows' dword reads are bank-conflict free (80-byte rows were 4-way
+  // conflicted: 1847 conflict cycles per wave, PMC); the realigning dword
+  // reads past a row land in the next one, or read 0 past the allocation.
+  // 18.7 KiB in all, so that a work block fits beside 5 coverage blocks
+  // (5 x 27.8 KiB) of the next chunk on a CU's 160 KiB.
+  constexpr int SROW = 68;
+  static_assert(SROW % 8 == 4 && SROW >= 64, "odd dword stride, 64 staged bytes");
   __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][SROW];
   __shared__ unsigned long long s_pre[NQ + 1];
   __shared__ uint32_t s_cnt[NBIN];
@@ -727,7 +727,7 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
     s_cnt[threadIdx.x] = 0u;
   }
   __syncthreads();
-  uint8_t* slot = scratch[threadIdx.x] + 16;
+  uint8_t* slot = scratch[threadIdx.x];
   const unsigned long long n = s_pre[NQ];
   for (unsigned long long i0 = (unsigned long long)blockIdx.x * IBLOCK; i0 < n;
        i0 += (unsigned long long)gridDim.x * IBLOCK) {          // block-uniform trip count
