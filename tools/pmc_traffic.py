@@ -58,7 +58,7 @@ spans = {}
 for name, rx in SPANS.items():
     spans[name] = int(sum(v["fetch_bytes"] + v["write_bytes"] for k, v in per_kernel.items() if re.search(rx, k)))
 out = {"source": "tools/pmc_kernels.sh (rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE, separate passes) on "
-                 "python bench.py --steps 2 --warmup 1 --no-cpu-baseline; folded by tools/pmc_traffic.py",
+                 "python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-window; folded by tools/pmc_traffic.py",
        "hbm_bytes_per_build": spans,
        "per_kernel": {k: {kk: (int(vv) if kk != "dispatches_per_build" else vv) for kk, vv in v.items()}
                       for k, v in sorted(per_kernel.items())}}
