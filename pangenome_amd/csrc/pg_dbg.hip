@@ -1885,9 +1885,11 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
   init_hash(c);
   uint64_t cap = region_cap(n + 64);
   ACount a;
-  for (int attempt = 0; attempt < 3; ++attempt) {
+  // every record count is known here (n): stages B/C go right behind stage A
+  // (finish_build's spec form, one host round trip), unless a region overflows
+  auto enqueue = [&](uint64_t rcap) {
     FillList fl;
-    const BinOut O = stageA_begin(c, cap, fl);
+    const BinOut O = stageA_begin(c, rcap, fl);
     c.t1.init();
     c.t1.start(c.stream);
     fl.launch(c.stream);
@@ -1898,6 +1900,18 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
       PG_HIP(hipGetLastError());
     }
     c.t1.stop(c.stream);
+  };
+  enqueue(cap);
+  a.total = n + (sentinel ? 1 : 0);
+  a.maxreg = cap;
+  a.maxbin = 8 * cap;
+  const bool ok = finish_build(c, a, true);
+  c.ms_insert = c.t1.ms();
+  c.n_records_a = a.total;
+  if (ok) return;
+  cap = a.maxreg + a.maxreg / 8 + 512;              // every region's exact count is known now
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    enqueue(cap);
     a = stageA_read(c);
     if (!(a.bits & F_A_OVER)) break;
     cap = a.maxreg + a.maxreg / 8 + 512;
