@@ -247,14 +247,20 @@ def main():
     # H2D -> parse -> build -> rdBG count on the host; and the bare H2D rate
     host_ms, h2d_gbs = None, None
     if world == 1 and not args.no_host_window:
-        ts = []
+        # pg_build_host: chunked H2D, K1 per chunk, stage A over each chunk's
+        # completed records under the copy, then stages B/C
+        ts, host_counts = [], []
         for _ in range(3):
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            ctx.parse_host_ptr(host0.data_ptr(), host0.numel())      # chunked H2D under K1
-            ctx.build(None, 0, True)
+            sth = ctx.build_host_ptr(host0.data_ptr(), host0.numel(), True)
             ts.append(time.perf_counter() - t1)
+            host_counts.append((sth.n_dbg, sth.n_rdbg))
         host_ms = 1e3 * min(ts)
+        if parity is not None and digests[0]:
+            ok_host = all(hc == (digests[0]["n_dbg"], digests[0]["n_rdbg"]) for hc in host_counts)
+            parity["host_window_ok"] = bool(ok_host)
+            parity["ok"] = bool(parity["ok"] and ok_host)
         tmp = torch.empty_like(d_in[0])
         hs = []
         for _ in range(3):

@@ -80,6 +80,14 @@ int pg_parse(pg_ctx* ctx, uint64_t* n_records, uint64_t* n_bases);
  * makes the copies plain DMA).  The bytes are read until the call returns. */
 int pg_parse_host(pg_ctx* ctx, const uint8_t* host_bytes, uint64_t nbytes, uint64_t* n_records,
                   uint64_t* n_bases);
+/* pg_parse_host + pg_build of every record (seq2rdbg + dbg2rdbg,
+ * kmer_numba.py:1234-1321, for an input no -n limit or 2^33-base checkpoint
+ * touches) with the build's first stage streamed under the upload: the
+ * records a chunk completes go through the coverage / emission pass while
+ * the next chunk is copied.  Results equal pg_parse + pg_build(NULL, 0, rc0);
+ * the record table is available afterwards (pg_records). */
+int pg_build_host(pg_ctx* ctx, const uint8_t* host_bytes, uint64_t nbytes, int rc0, uint64_t* n_rdbg,
+                  pg_stats* stats);
 /* Per-record table (arrays of n_records): compacted sequence length, header
  * byte span (qid = bytes[hdr_start : hdr_start+hdr_len], '>' included,
  * :160) and seqio's resume pointer (:153). Any pointer may be NULL. */

@@ -52,6 +52,7 @@ SIGNATURES = {
     "pg_build_dbg": (C.c_int, [_P, _P, C.c_int, C.c_int, _SP]),
     "pg_build_rdbg": (C.c_int, [_P, _U64P, _SP]),
     "pg_build": (C.c_int, [_P, _P, C.c_int, C.c_int, _U64P, _SP]),
+    "pg_build_host": (C.c_int, [_P, _P, C.c_uint64, C.c_int, _U64P, _SP]),
     "pg_dbg_export": (C.c_int, [_P, _P, _P, C.c_uint64, _U64P]),
     "pg_rdbg_export": (C.c_int, [_P, _P, C.c_uint64, _U64P]),
     "pg_dbg_partition": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
@@ -198,6 +199,21 @@ class Context:
         f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
         check(self.lib.pg_build(self.h, ptr(f), int(extra_empty), int(bool(rc0)), C.byref(n), C.byref(st)),
               "pg_build")
+        return st
+
+    def build_host(self, data, rc0: bool = True) -> PgStats:
+        """parse + build of every record from host bytes with stage A streamed
+        under the chunked upload (pg_build_host); the record table is
+        available afterwards (records())."""
+        arr = np.frombuffer(data, dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        return self.build_host_ptr(arr.ctypes.data if arr.shape[0] else None, arr.shape[0], rc0)
+
+    def build_host_ptr(self, host_ptr, nbytes: int, rc0: bool = True) -> PgStats:
+        st = PgStats()
+        n = C.c_uint64()
+        check(self.lib.pg_build_host(self.h, C.c_void_p(host_ptr), nbytes, int(bool(rc0)), C.byref(n), C.byref(st)),
+              "pg_build_host")
+        self.n_records, self.n_bases = st.n_records, st.n_bases
         return st
 
     def tune(self, what: int, value: int):

@@ -65,7 +65,9 @@ int pg_create(pg_ctx** out, int device, int k) {
     x->c.k = k < 1 ? 1 : (k > 27 ? 27 : k);
     PG_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
     PG_HIP(hipStreamCreateWithFlags(&x->c.stream2, hipStreamNonBlocking));
+    PG_HIP(hipStreamCreateWithFlags(&x->c.stream3, hipStreamNonBlocking));
     for (auto& e : x->c.ev) PG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (auto& e : x->c.cev) PG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     PG_HIP(hipDeviceGetAttribute(&x->c.n_cu, hipDeviceAttributeMultiprocessorCount, device));
     *out = x;
   });
@@ -93,6 +95,9 @@ void pg_destroy(pg_ctx* x) {
   c.t6.destroy();
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto e : c.cev)
+    if (e) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c.stream3);
   (void)hipStreamDestroy(c.stream2);
   (void)hipStreamDestroy(c.stream);
   delete x;
@@ -203,6 +208,23 @@ int pg_build(pg_ctx* x, const uint8_t* rec_flags, int extra_empty, int rc0, uint
     pg::build_rdbg(x->c);                      // (the degree scan ran inside the build)
     if (n_rdbg) *n_rdbg = x->c.n_rdbg;
     fill_stats(x->c, stats);
+  });
+}
+
+int pg_build_host(pg_ctx* x, const uint8_t* host, uint64_t n, int rc0, uint64_t* n_rdbg, pg_stats* stats) {
+  return guard([&] {
+    if (!x || (!host && n)) throw pg::Error(PG_EINVAL, "pg_build_host: bad arguments");
+    pg::Ctx& c = x->c;
+    PG_HIP(hipSetDevice(c.device));
+    auto t0 = std::chrono::steady_clock::now();
+    c.fasta_own.reserve(n + 64);
+    c.d_fasta = c.fasta_own.as<uint8_t>();
+    c.n_bytes = n;
+    c.parsed = c.built = c.reduced = false;
+    pg::build_host(c, host, n, rc0 != 0);
+    c.ms_parse = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (n_rdbg) *n_rdbg = c.n_rdbg;
+    fill_stats(c, stats);
   });
 }
 

@@ -1193,7 +1193,7 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
 // LEAD stripes ahead).  Group g's members are descs[QM*g .. QM*g + QM); an
 // empty slot has r = -1 and the group's stripe.
 constexpr uint32_t LEAD = 4;
-__global__ void k_tiles(const uint32_t* __restrict__ sched, uint32_t nj, uint32_t lead_stripes,
+__global__ void k_tiles(const uint32_t* __restrict__ sched, uint32_t nj, uint32_t lead_stripes, uint32_t lead_off,
                         const long long* __restrict__ rec_start, const long long* __restrict__ rec_len,
                         TileDesc* __restrict__ out, uint64_t ngroups) {
   const uint32_t* off = sched;
@@ -1216,7 +1216,7 @@ __global__ void k_tiles(const uint32_t* __restrict__ sched, uint32_t nj, uint32_
       if (m == 0) r = (int)ord[0];
     } else {
       if (lead) --i;
-      stripe = (int)(lo - LEAD);
+      stripe = (int)(lo - lead_off);
       const uint32_t f = i * QM + m;
       if (f < nf[lo]) r = (int)ord[1 + f];
     }
@@ -1376,38 +1376,49 @@ static void init_hash(Ctx& c) {
 // The host sorts the records and sends the per-stripe group offsets and
 // follower counts; k_tiles expands the descriptors on the device.  Cached
 // while the record table and flags repeat.  Returns the number of groups.
-static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
+// follow: the flagged records are all followers of the references already
+// chosen (c.k3_ref, c.k3_ref2, left as they are; both skipped if flagged), no
+// lead groups (pg_build_host's later chunks); never cached.
+static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag, bool follow = false) {
   const uint64_t R = c.n_records;
-  if (c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k) return c.n_tiles;
+  if (!follow && c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k) return c.n_tiles;
   std::vector<std::pair<uint64_t, int>> nt;           // (stripes, record)
   for (uint64_t r = 0; r < R; ++r) {
     const int64_t n = c.h_rec_len[r];
     if (!flag[r] || n < c.k + 2) continue;
+    if (follow && ((int)r == c.k3_ref || (int)r == c.k3_ref2)) continue;
     nt.push_back({(uint64_t)((n - c.k + 1 + TILE - 1) / TILE), (int)r});
   }
   std::stable_sort(nt.begin(), nt.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
-  c.k3_ref = nt.size() >= 2 ? nt[0].second : -1;      // the lead is every follower's dedup reference
-  c.k3_ref2 = nt.size() >= 3 ? nt[1].second : -1;     // the second reference (k_cover)
+  if (!follow) {
+    c.k3_ref = nt.size() >= 2 ? nt[0].second : -1;    // the lead is every follower's dedup reference
+    c.k3_ref2 = nt.size() >= 3 ? nt[1].second : -1;   // the second reference (k_cover)
+  }
   c.k3_hint.reserve(64 * (R + 1) + 64);               // drift hints per XCD, reference, record
-  const uint64_t lead_s = nt.empty() ? 0 : nt[0].first;
-  const uint32_t nj = nt.empty() ? 0u : (uint32_t)(lead_s + LEAD);
-  std::vector<uint32_t> sched(2 * nj + 1 + nt.size());
+  // normal: ord[0] = the lead, its tiles one group per stripe, the followers
+  // (ord[1..]) LEAD stripes behind; follow: followers only (ord[0] unused)
+  const uint64_t lead_s = follow || nt.empty() ? 0 : nt[0].first;
+  const uint32_t lead_off = follow ? 0u : LEAD;
+  const uint32_t nj = nt.empty() ? 0u : (uint32_t)(follow ? nt[0].first : lead_s + LEAD);
+  const size_t skip = follow ? 0 : 1;                 // followers: nt[skip ..]
+  std::vector<uint32_t> sched(2 * nj + 2 + nt.size());
   uint64_t total = 0;
   size_t live = nt.size();
   for (uint32_t j = 0; j < nj; ++j) {
     sched[j] = (uint32_t)total;
     uint64_t cnt = j < lead_s ? 1 : 0, nfol = 0;
-    if (j >= LEAD) {
-      const uint64_t jf = j - LEAD;                   // the followers' stripe
+    if (j >= lead_off) {
+      const uint64_t jf = j - lead_off;               // the followers' stripe
       while (live && nt[live - 1].first <= jf) --live;
-      nfol = live > 1 ? live - 1 : 0;
+      nfol = live > skip ? live - skip : 0;
       cnt += (nfol + QM - 1) / QM;
     }
     sched[nj + 1 + j] = (uint32_t)nfol;
     total += cnt;
   }
   sched[nj] = (uint32_t)total;
-  for (size_t i = 0; i < nt.size(); ++i) sched[2 * nj + 1 + i] = (uint32_t)nt[i].second;
+  if (follow) sched[2 * nj + 1] = 0u;                 // ord[0] (unused)
+  for (size_t i = 0; i < nt.size(); ++i) sched[2 * nj + 1 + (follow ? 1 : 0) + i] = (uint32_t)nt[i].second;
   if (total * QM >= (1ull << 32)) throw Error(-22, "make_tiles: too many tiles");
   c.tile_desc.reserve(sizeof(TileDesc) * (QM * total + 1));
   if (total) {
@@ -1416,27 +1427,35 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag) {
     std::memcpy(c.tile_pin.p, sched.data(), 4 * sched.size());
     PG_HIP(hipMemcpyAsync(c.tile_sched.p, c.tile_pin.p, 4 * sched.size(), hipMemcpyHostToDevice, c.stream));
     hipLaunchKernelGGL(k_tiles, dim3(grid_for(QM * total, 256, 2048)), dim3(256), 0, c.stream,
-                       c.tile_sched.as<uint32_t>(), nj, (uint32_t)lead_s, c.rec_start.as<long long>(),
+                       c.tile_sched.as<uint32_t>(), nj, (uint32_t)lead_s, lead_off, c.rec_start.as<long long>(),
                        c.rec_len.as<long long>(), c.tile_desc.as<TileDesc>(), total);
     PG_HIP(hipGetLastError());
   }
-  c.tile_sig_len = c.h_rec_len;
-  c.tile_sig_flag = flag;
-  c.tile_k = c.k;
+  if (follow) {
+    c.tile_sig_len.clear();                           // the cached list is gone
+  } else {
+    c.tile_sig_len = c.h_rec_len;
+    c.tile_sig_flag = flag;
+    c.tile_k = c.k;
+  }
   c.n_tiles = total;
   return total;
 }
 
 // ---- stage A: buffers for `cap` records per region; the regions' cursors and
 // the flags are zeroed by the caller's fill list
-static BinOut stageA_begin(Ctx& c, uint64_t cap, FillList& fl) {
-  c.capA = cap;
-  c.recA_key.reserve(8 * NREG * cap);
-  c.recA_mw.reserve(4 * NREG * cap);
-  c.ctrA.reserve(8 * CSTRIDE * NREG);
-  c.flags.reserve(4 * N_FLAGS);
-  fl.add(c.ctrA.p, 8 * CSTRIDE * NREG);
-  fl.add(c.flags.p, 4 * N_FLAGS);
+// (reset = false: the regions of the stage A in progress take more records)
+static BinOut stageA_begin(Ctx& c, uint64_t cap, FillList& fl, bool reset = true) {
+  if (reset) {
+    c.capA = cap;
+    c.recA_key.reserve(8 * NREG * cap);
+    c.recA_mw.reserve(4 * NREG * cap);
+    c.ctrA.reserve(8 * CSTRIDE * NREG);
+    c.flags.reserve(4 * N_FLAGS);
+    fl.add(c.ctrA.p, 8 * CSTRIDE * NREG);
+    fl.add(c.flags.p, 4 * N_FLAGS);
+  }
+  cap = c.capA;
   return BinOut{c.recA_key.as<unsigned long long>(), c.recA_mw.as<uint32_t>(), c.ctrA.as<unsigned long long>(),
                 cap, (uint32_t)(c.kb - c.cbits), c.flags.as<unsigned>()};
 }
@@ -1630,11 +1649,16 @@ static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, const B
 // coverage pass of chunk i+1; the last work pass runs on s0 right behind the
 // last coverage pass, beside the previous one — chunks' records commute),
 // the short records beside it, then the staged npz slots; s1 joins s0.
-static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int extra_empty) {
+// part: 0 = a whole stage A; pg_build_host's parts: SA_FIRST starts it (the
+// regions reset, no short records yet), SA_MORE adds tiles, SA_TAIL adds the
+// short records, the n<k flag and the staged slots (no tiles).
+enum { SA_WHOLE = 0, SA_FIRST = 1, SA_MORE = 2, SA_TAIL = 3 };
+static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int extra_empty, int part = SA_WHOLE) {
   const uint64_t shift = pow5(c.k - 1);
   hipStream_t s0 = c.stream, s1 = c.stream2;
   FillList fl;
-  const BinOut O = stageA_begin(c, cap, fl);
+  const BinOut O = stageA_begin(c, cap, fl, part == SA_WHOLE || part == SA_FIRST);
+  if (part == SA_TAIL) ntiles = 0;
   const uint8_t* cls = c.cls.as<uint8_t>();
   const dim3 b(IBLOCK);
   int nch = ntiles >= (uint64_t)K3_CHUNKS * K3_CHUNK_MIN ? K3_CHUNKS : 1;
@@ -1681,8 +1705,10 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     hipStream_t ws = s1;
     if (nch > 1 && i + 1 == nch) {
       ws = s0;
-      launch_short(c, s1, rc0, shift, O);                      // k_short beside the last work pass
-      short_done = true;
+      if (part == SA_WHOLE) {
+        launch_short(c, s1, rc0, shift, O);                    // k_short beside the last work pass
+        short_done = true;
+      }
     } else {
       PG_HIP(hipEventRecord(c.ev[1 + i], s0));
       PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: work 0 .. i-1, then this
@@ -1697,9 +1723,10 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
                          shift, c.tv, O);
     PG_HIP(hipGetLastError());
   }
-  if (!short_done) launch_short(c, s0, rc0, shift, O);
-  if (extra_empty) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, s0, c.flags.as<unsigned>());
-  if (c.n_preload) {
+  const bool tail = part == SA_WHOLE || part == SA_TAIL;
+  if (!short_done && tail) launch_short(c, s0, rc0, shift, O);
+  if (extra_empty && tail) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, s0, c.flags.as<unsigned>());
+  if (c.n_preload && tail) {
     hipLaunchKernelGGL(k_preload_emit, dim3(grid_for(c.n_preload, 4 * IBLOCK, 4096)), dim3(IBLOCK), 0, s0,
                        c.preload.as<PreEnt>(), c.n_preload, c.tv, O);
     PG_HIP(hipGetLastError());
@@ -1921,6 +1948,84 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
   c.sentinel = a.sentinel ? 1 : 0;
   c.n_records_a = a.total;
   finish_build(c, a, false);
+}
+
+// pg_build_host: K1 over the chunked upload, and stage A streamed under it.
+// After each chunk's K1 the host gets the records completed so far; the
+// first time there are three long ones, stage A starts with the usual lead
+// and second reference among them (SA_FIRST), and every later batch of
+// completed records goes through the coverage / emission pass as followers of
+// those two (SA_MORE); the short records, once the record table is final
+// (SA_TAIL).  Stages B and C then run from stage A's exact counts.  The
+// choice of references only decides how much the coverage pass skips, never
+// what is inserted, so the table is the one pg_build makes.  A stage A
+// region overflow (the regions are sized from the file before the records
+// are known), or more records than the parse could stream, falls back to
+// pg_build over the parsed records.
+void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
+  c.rc0 = rc0;
+  c.built = c.reduced = false;
+  c.n_dbg = c.n_rdbg = c.n_canon = 0;
+  init_hash(c);
+  // regions for ~ the last build's records per base (the file's bytes bound
+  // the bases), or a quarter record per byte on a first build
+  const uint64_t est = c.u_ratio > 0 ? (uint64_t)(c.u_ratio * 1.25 * (double)n) : n / 4;
+  const uint64_t cap = region_cap(std::min<uint64_t>(est, n) + 4096);
+  uint64_t done = 0;
+  bool started = false, broken = c.n_preload != 0;
+  c.t1.init();
+  std::function<void(uint64_t)> on_chunk = [&](uint64_t rc) {
+    if (broken) return;
+    if (rc == ~0ull) { broken = true; return; }               // the parse could not stream
+    if (rc <= done) return;
+    std::vector<uint8_t> flag(c.n_records, 0);
+    uint64_t nlong = 0;
+    for (uint64_t r = done; r < rc; ++r) {
+      flag[r] = 1;
+      nlong += c.h_rec_len[r] >= c.k + 2;
+    }
+    const bool final_call = c.parsed;
+    if (!started) {
+      if (nlong < 3 && !final_call) return;                   // wait for three long records
+      const uint64_t nt = make_tiles(c, flag);
+      enqueue_stageA(c, cap, nt, rc0, 0, SA_FIRST);
+      started = true;
+    } else {
+      const uint64_t nt = make_tiles(c, flag, true);
+      if (nt) enqueue_stageA(c, cap, nt, rc0, 0, SA_MORE);
+    }
+    done = rc;
+  };
+  parse_fasta(c, h_src, &on_chunk);
+  const uint64_t R = c.n_records;
+  std::vector<uint8_t> all(R, 1);
+  if (!broken && (done != R || !started)) broken = true;
+  if (!broken) {
+    if (R) PG_HIP(hipMemsetAsync(c.rec_flag.p, 1, R, c.stream));
+    c.windows_fw = 0;
+    for (uint64_t r = 0; r < R; ++r) {
+      const int64_t m = c.h_rec_len[r];
+      c.windows_fw += m > c.k ? (uint64_t)(m - c.k + 1) : 1;
+    }
+    c.windows_total = c.windows_fw * (rc0 ? 2 : 1);
+    c.last_flag = all;
+    c.last_extra = 0;
+    c.dump_ready = false;
+    enqueue_stageA(c, cap, 0, rc0, 0, SA_TAIL);
+    ACount a = stageA_read(c);
+    if (!(a.bits & F_A_OVER)) {
+      c.ms_insert = c.t1.ms();
+      c.ms_clear = 0;
+      c.sentinel = a.sentinel ? 1 : 0;
+      c.n_records_a = a.total;
+      finish_build(c, a, false);
+      if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
+      c.tile_sig_len.clear();                                 // (the tile list holds the last batch only)
+      return;
+    }
+  }
+  c.tile_sig_len.clear();
+  build_dbg(c, all.data(), 0, rc0);
 }
 
 }  // namespace pg

@@ -9,6 +9,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <functional>
 #include <vector>
 
 #include "pg_common.h"
@@ -95,7 +96,9 @@ struct Ctx {
   int k = 27;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // side stream: K3 work passes overlap the next coverage pass
+  hipStream_t stream3 = nullptr;  // copy stream: chunked host uploads (pg_parse_host, pg_build_host)
   hipEvent_t ev[16] = {};         // ordering events between the two streams
+  hipEvent_t cev[16] = {};        // chunk-landed events of the copy stream
   int n_cu = 256;                 // compute units (persistent-kernel grids)
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
@@ -196,7 +199,14 @@ struct Ctx {
 };
 
 // pg_parse.hip
-void parse_fasta(Ctx& c, const uint8_t* h_src = nullptr);
+// h_src: host bytes, uploaded in chunks pipelined with K1.  on_chunk (host
+// input only): called after each chunk with the number of records complete
+// so far (their lengths in c.h_rec_len, c.n_records = that count), and once
+// at the end with all of them; it may enqueue work on c.stream.
+void parse_fasta(Ctx& c, const uint8_t* h_src = nullptr, const std::function<void(uint64_t)>* on_chunk = nullptr);
+// pg_build_host: parse of host bytes with stage A of the build streamed under
+// the upload (every record, no -n / checkpoint plan), then stages B and C
+void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0);
 // pg_dbg.hip
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0);
 void build_rdbg(Ctx& c);

@@ -477,7 +477,7 @@ static void upload_byte_class(int device) {
 // the side stream, and K1 works on each chunk as soon as it has landed -
 // span functions, the scan of every span so far, the emission of the chunk's
 // spans - so only the last chunk's K1 follows the copy.
-void parse_fasta(Ctx& c, const uint8_t* h_src) {
+void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t)>* on_chunk) {
   upload_byte_class(c.device);
   hipStream_t st = c.stream;
   const uint64_t n = c.n_bytes;
@@ -485,7 +485,11 @@ void parse_fasta(Ctx& c, const uint8_t* h_src) {
   c.n_lines = c.n_records = c.n_bases = c.n_nl = 0;
   c.h_rec_start.clear(); c.h_rec_len.clear(); c.h_rec_hdr_start.clear();
   c.h_rec_hdr_len.clear(); c.h_rec_ptr.clear();
-  if (n == 0) { c.parsed = true; return; }
+  if (n == 0) {
+    c.parsed = true;
+    if (on_chunk) (*on_chunk)(0);
+    return;
+  }
 
   const uint64_t nspan = (n + WSPAN - 1) / WSPAN;
   const unsigned nblk = (unsigned)((nspan + WAVES - 1) / WAVES);
@@ -501,7 +505,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src) {
     PG_HIP(rocprim::inclusive_scan(c.scratch.p, b, fns, incl, (size_t)upto, FnThen{}, st));
   };
   c.cls.reserve(n + 64);
-  const uint64_t rcap0 = std::max<uint64_t>(c.rec_cap, 64);
+  const uint64_t rcap0 = std::max<uint64_t>(c.rec_cap, on_chunk ? 4096 : 64);
   auto reserve_records = [&](uint64_t rcap) {
     c.rec_start.reserve(8 * (rcap + 1));
     c.rec_len.reserve(8 * (rcap + 1));
@@ -518,20 +522,46 @@ void parse_fasta(Ctx& c, const uint8_t* h_src) {
     PG_HIP(hipGetLastError());
   };
   reserve_records(rcap0);
+  bool streaming = on_chunk != nullptr;
   if (h_src) {
     const uint64_t C = std::max<uint64_t>(WSPAN, c.h2d_chunk / WSPAN * WSPAN);
-    int e = 0;
-    for (uint64_t off = 0; off < n; off += C, e = (e + 1) & 15) {
-      const uint64_t len = std::min(C, n - off);
+    const uint64_t nch = (n + C - 1) / C;
+    // copies run up to 8 chunks ahead of K1 on the copy stream (16 events:
+    // an event is recorded again only after K1's wait on it was queued)
+    uint64_t queued = 0;
+    auto queue_copy = [&](uint64_t i) {
+      const uint64_t off = i * C, len = std::min(C, n - off);
+      PG_HIP(hipMemcpyAsync(c.fasta_own.as<uint8_t>() + off, h_src + off, len, hipMemcpyHostToDevice, c.stream3));
+      PG_HIP(hipEventRecord(c.cev[i & 15], c.stream3));
+    };
+    for (uint64_t i = 0; i < nch; ++i) {
+      while (queued < nch && queued < i + 8) queue_copy(queued++);
+      const uint64_t off = i * C, len = std::min(C, n - off);
       const uint64_t s0 = off / WSPAN, s1 = std::min(nspan, (off + len + WSPAN - 1) / WSPAN);
-      PG_HIP(hipMemcpyAsync(c.fasta_own.as<uint8_t>() + off, h_src + off, len, hipMemcpyHostToDevice, c.stream2));
-      PG_HIP(hipEventRecord(c.ev[e], c.stream2));
-      PG_HIP(hipStreamWaitEvent(st, c.ev[e], 0));
+      PG_HIP(hipStreamWaitEvent(st, c.cev[i & 15], 0));
       hipLaunchKernelGGL(k_span_sum, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta,
                          n, s0, s1, fns);
       PG_HIP(hipGetLastError());
       scan(s1);
       emit(s0, s1, rcap0);
+      if (!streaming || i + 1 == nch) continue;
+      // the records complete so far (every header seen but the last one):
+      // the host waits for this chunk's K1 while the copies go on
+      auto* hdr = c.rec_hdr.as<long long>();
+      hipLaunchKernelGGL(k_records, dim3(grid_for(rcap0, 256, 1024)), dim3(256), 0, st, incl + s1 - 1, n, rcap0,
+                         c.rec_start.as<long long>(), hdr, c.rec_len.as<long long>(), c.rec_pack.as<long long>());
+      PG_HIP(hipGetLastError());
+      PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 64 + 40 * rcap0, hipMemcpyDeviceToHost, st));
+      c.sync();
+      const Fn t = *c.h_pin.as<Fn>();
+      const uint64_t Rs = t.nl ? t.hdr : 0;
+      if (Rs > rcap0) { streaming = false; continue; }        // more records than the arrays hold
+      const int64_t* pk = c.h_pin.as<int64_t>() + 8;
+      const uint64_t Rc = Rs ? Rs - 1 : 0;
+      c.h_rec_start.assign(pk, pk + Rc);
+      c.h_rec_len.assign(pk + rcap0, pk + rcap0 + Rc);
+      c.n_records = Rc;
+      (*on_chunk)(Rc);
     }
   } else {
     hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
@@ -571,7 +601,11 @@ void parse_fasta(Ctx& c, const uint8_t* h_src) {
     c.rec_cap = R;
   }
   c.n_nl = tot.nl;
-  if (tot.nl == 0) { c.parsed = true; return; }             // no line at all (:126-132)
+  if (tot.nl == 0) {                                        // no line at all (:126-132)
+    c.parsed = true;
+    if (on_chunk) (*on_chunk)(streaming ? 0 : ~0ull);
+    return;
+  }
   const bool has_tail = (long long)n - 1 > tot.last + 1;
   c.n_lines = tot.nl + (has_tail ? 1 : 0);
   c.n_records = R;
@@ -580,6 +614,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src) {
   for (uint64_t r = 0; r < R; ++r) nb += (uint64_t)c.h_rec_len[r];
   c.n_bases = nb;
   c.parsed = true;
+  if (on_chunk) (*on_chunk)(streaming ? R : ~0ull);          // ~0: the stream broke off
 }
 
 }  // namespace pg

@@ -170,3 +170,51 @@ def test_parse_host_pipelined(oracle_mod, chunk):
         keys, masks = ctx.dbg()
         assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
     ctx.close()
+
+
+def _build_ref(buf, k=27):
+    from pangenome_amd._lib import Context
+    ctx = Context(k)
+    ctx.set_fasta(buf)
+    ctx.parse()
+    rec = ctx.records()
+    st = ctx.build(None, 0, True)
+    out = (rec, ctx.dbg(), ctx.rdbg(), st.n_dbg, st.n_rdbg)
+    ctx.close()
+    return out
+
+
+@pytest.mark.parametrize("case", ["pangenome", "mixed", "few_long", "tiny_records"])
+def test_build_host_streamed(case):
+    """pg_build_host: stage A over each chunk's completed records under the
+    chunked upload (the lead and second reference picked among the first
+    completed records) - the same record table, dBG and rdBG as parse + build,
+    cold and warm, with chunk edges inside records and records spanning many
+    chunks."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK
+    if case == "pangenome":
+        buf, chunks = synth.pangenome(12, 150_000, snp=1e-3, indel=1e-4, seed=11), (64 * 1024, 16 * 1024)
+    elif case == "mixed":
+        buf, chunks = _mixed_fasta(5, (60, 17, 1000), nrec=10, reclen=20_000), (16 * 1024, 3 * 16 * 1024)
+    elif case == "few_long":                       # never three long records before the last chunk
+        buf, chunks = _mixed_fasta(9, (60,), nrec=2, reclen=60_000), (16 * 1024,)
+    else:                                          # records of length < k, = k, k+1, k+2 between long ones
+        rng = np.random.default_rng(3)
+        acgt = np.frombuffer(b"ACGT", np.uint8)
+        recs = [acgt[rng.integers(0, 4, m)].tobytes() for m in (40_000, 5, 27, 28, 29, 40_000, 0, 30_000, 26, 35_000)]
+        buf, chunks = b"".join(b">r%d\n%s\n" % (i, r) for i, r in enumerate(recs)), (16 * 1024,)
+    rec, (rk, rm), rr, n_dbg, n_rdbg = _build_ref(buf)
+    for chunk in chunks:
+        ctx = Context(27)
+        ctx.tune(PG_TUNE_H2D_CHUNK, chunk)
+        for _ in range(2):                          # cold, then warm (sized from the first build)
+            st = ctx.build_host(buf, True)
+            assert (st.n_dbg, st.n_rdbg) == (n_dbg, n_rdbg)
+            got = ctx.records()
+            for key in rec:
+                assert np.array_equal(got[key], rec[key]), key
+            keys, masks = ctx.dbg()
+            assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
+            assert np.array_equal(ctx.rdbg(), rr)
+        ctx.close()
