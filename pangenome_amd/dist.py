@@ -326,9 +326,10 @@ class DistRun:
     """The CLI stages of entry_point (:2073-2146) over world shards."""
 
     def __init__(self, qry: str, k: int, shard, comm: Comm, device=None, out=None, dev_index: int = 0,
-                 edge_chunk: int = host.CHUNK):
+                 edge_chunk: int = host.CHUNK, dbg_chunk: int = host.CHUNK):
         self.qry, self.k, self.sh, self.comm = qry, min(max(1, int(k)), 27), shard, comm
         self.edge_chunk = int(edge_chunk)                  # seq2graph's checkpoint size (:2073; tests vary it)
+        self.dbg_chunk = int(dbg_chunk)                    # seq2rdbg's
         self.device, self.dev_index = device, dev_index
         self.rank, self.world = comm.rank, comm.world
         self.out = out or sys.stdout
@@ -360,7 +361,13 @@ class DistRun:
             if self.rank == 0:
                 self.sh.stage(keys, values, counts)
             resume = host.resume_position(offset, self.S.ptr)
-        flags, extra = host.plan_dbg(self.S.seq_len, self.shape, bool(rc0), int(Ns), host.CHUNK, resume=resume)
+        flags, extra, ckpt = host.plan_dbg(self.S.seq_len, self.shape, bool(rc0), int(Ns), self.dbg_chunk,
+                                           resume=resume, checkpoint=True)
+        if ckpt is not None:
+            # <in>_db_brkpt.npz (:1255-1259): the last dump's state, built and dumped once
+            cf, ce, last = ckpt
+            self.sh.build(self.S.local(cf, self.rank), ce if self.rank == 0 else 0, rc0)
+            self.dump(self.qry + "_db_brkpt", offset=int(self.S.ptr[last]))
         self.sentinel = self.sh.build(self.S.local(flags, self.rank), extra if self.rank == 0 else 0, rc0)
 
     def load_dbg(self, fn, rdbg: bool, rc0):
@@ -377,7 +384,7 @@ class DistRun:
             self.sh.stage(keys, values, counts)
         self.sentinel = self.sh.build(zeros, 0, rc0)
 
-    def dump(self, fn):
+    def dump(self, fn, offset: int = 0):
         """dump() (:243-261) of the global dBG, written by rank 0."""
         keys, masks, counts = self.sh.counts()
         parts = self.comm.gather_bytes(_pack(keys.astype(np.uint64), masks.astype(np.uint16).astype(np.int64),
@@ -390,7 +397,7 @@ class DistRun:
             cap, size, K, V, C = self.sh.dump_global(np.concatenate(ks), np.concatenate(ms).astype(np.uint16),
                                                      np.minimum(np.concatenate(cs), 255).astype(np.uint8),
                                                      self.k, self.dev_index)
-            host.write_db_npz(fn, cap, size, K, V, C)
+            host.write_db_npz(fn, cap, size, K, V, C, offset=offset)
         self.comm.barrier()
 
     # --------------------------------------------------------------- rdBG
@@ -416,19 +423,30 @@ class DistRun:
         if brkpt and os.path.isfile(brkpt):
             offset, lt, lc = host.read_edge_npz(brkpt)
             loaded, resume = (lt, lc), host.resume_position(offset, self.S.ptr)
-        eflags, segment, ncp = host.plan_edges(self.S.seq_len, self.shape, int(Ns), self.edge_chunk, resume=resume)
-        t, c, w = self.sh.edges(self.S.local(eflags, self.rank), rc1)
-        w = np.asarray(w, np.int64) + 2 * int(self.S.off[self.rank])
-        parts = self.comm.gather_bytes(_pack(np.ascontiguousarray(t, np.uint64), np.asarray(c, np.int64), w))
+        eflags, segment, ncp, ckpt = host.plan_edges(self.S.seq_len, self.shape, int(Ns), self.edge_chunk,
+                                                     resume=resume, checkpoint=True)
+
+        def state(fl, upto):
+            """the edge Dict after segments 0..upto on rank 0 (iteration order)"""
+            t, c, w = self.sh.edges(self.S.local(fl, self.rank), rc1)
+            w = np.asarray(w, np.int64) + 2 * int(self.S.off[self.rank])
+            parts = self.comm.gather_bytes(_pack(np.ascontiguousarray(t, np.uint64), np.asarray(c, np.int64), w))
+            if self.rank != 0:
+                return None, None
+            tuples, counts, walk = reduce_edges([_unpack(p, (np.uint64, np.int64, np.int64)) for p in parts])
+            if loaded is not None:
+                return host.merge_edges(loaded[0], loaded[1], tuples, counts, walk, segment, upto)
+            o = host.edge_order(walk, segment, upto)
+            return tuples[o], counts[o]
+        if ckpt is not None:
+            # <in>_rdb_brkpt.npz (:1880-1887): the Dict before the last checkpoint
+            t_c, c_c = state((eflags.astype(bool) & (segment <= ncp - 1)).astype(np.uint8), ncp - 1)
+            if self.rank == 0:
+                host.write_edge_npz(self.qry + "_rdb_brkpt", t_c, c_c, int(self.S.ptr[ckpt]))
+        tuples, counts = state(eflags, ncp)
         oname = self.qry + "_rdbg_weight.xyz"
         payload = np.zeros(0, np.uint8)
         if self.rank == 0:
-            tuples, counts, walk = reduce_edges([_unpack(p, (np.uint64, np.int64, np.int64)) for p in parts])
-            if loaded is not None:
-                tuples, counts = host.merge_edges(loaded[0], loaded[1], tuples, counts, walk, segment, ncp)
-            else:
-                o = host.edge_order(walk, segment, ncp)
-                tuples, counts = tuples[o], counts[o]
             from ._lib import format_xyz
             with open(oname, "wb") as f:                       # :1893-1904
                 f.write(format_xyz(tuples, counts))
@@ -476,7 +494,8 @@ def reduce_edges(parts):
     return t[first[o]], tot[o], w[first[o]]
 
 
-def entry_point(argv, out=None, shard_factory=None, device=None, dev_index: int = 0, edge_chunk: int = host.CHUNK):
+def entry_point(argv, out=None, shard_factory=None, device=None, dev_index: int = 0, edge_chunk: int = host.CHUNK,
+                dbg_chunk: int = host.CHUNK):
     """kmer.entry_point (:1971-2146) on every rank of an initialised process
     group; rank 0 prints.  `shard_factory(k)` makes the rank's backend
     (default: GpuShard on dev_index)."""
@@ -494,7 +513,8 @@ def entry_point(argv, out=None, shard_factory=None, device=None, dev_index: int 
     k = min(max(1, kmer), 27)
     shard = shard_factory(k) if shard_factory else GpuShard(k, dev_index)
     comm = Comm(device)
-    run = DistRun(qry, k, shard, comm, device=device, out=out, dev_index=dev_index, edge_chunk=edge_chunk)
+    run = DistRun(qry, k, shard, comm, device=device, out=out, dev_index=dev_index, edge_chunk=edge_chunk,
+                  dbg_chunk=dbg_chunk)
     if dbs or rdb:                                      # :2073-2101
         if not rdb:
             run.say("load dBG from disk")

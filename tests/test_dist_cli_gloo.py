@@ -96,3 +96,4 @@ def test_shard_bounds_parse_like_the_whole_file(world):
         _bounds_case(buf, world)
     from pangenome_amd import synth
     _bounds_case(synth.pangenome(7, 3000, seed=5), world)
+

@@ -59,7 +59,7 @@ def _exchange_rank_sharded(rank, world, port, q, shards):
     _exchange_rank(rank, world, port, q, shards[rank])
 
 
-def _cli_rank(rank, world, port, q, argv, chunk, cwd):
+def _cli_rank(rank, world, port, q, argv, chunk, cwd, dbg_chunk=2 ** 33):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -70,7 +70,8 @@ def _cli_rank(rank, world, port, q, argv, chunk, cwd):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = io.StringIO()
     try:
-        pdist.entry_point(argv, out=out, device=torch.device("cuda", 0), dev_index=0, edge_chunk=chunk)
+        pdist.entry_point(argv, out=out, device=torch.device("cuda", 0), dev_index=0, edge_chunk=chunk,
+                          dbg_chunk=dbg_chunk)
     finally:
         dist.destroy_process_group()
     q.put((rank, out.getvalue()))
@@ -80,8 +81,8 @@ def rows_of(text):
     return [ln for ln in text.split("\n") if len(ln.split("\t")) == 5 and ln.split("\t")[3] in ("+", "-")]
 
 
-def _run(tmp_path, world, argv, chunk=2 ** 33):
-    outs = spawn_ranks(world, _cli_rank, (argv, chunk, str(tmp_path)))
+def _run(tmp_path, world, argv, chunk=2 ** 33, dbg_chunk=2 ** 33):
+    outs = spawn_ranks(world, _cli_rank, (argv, chunk, str(tmp_path), dbg_chunk))
     assert all(rows_of(outs[r]) == [] for r in range(1, world))
     return outs[0]
 
@@ -176,3 +177,26 @@ def test_torchrun_launch(tmp_path):
     assert p.returncode == 0, p.stderr[-3000:]
     assert rows_of(p.stdout) == fx.rows
     assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
+
+
+def test_dist_cli_writes_reference_checkpoints(tmp_path):
+    """The sharded CLI with passes crossing their chunk leaves the
+    <in>_db_brkpt.npz (dBG chunk 100000, :1255-1259) and <in>_rdb_brkpt.npz
+    (edge chunk 30000, :1880-1887) the reference itself wrote
+    (tests/golden/resume), and still prints the reference's rows."""
+    fr, fR = ResumeFixture("pan8_k27_r"), ResumeFixture("pan8_k27_R")
+    assert (fr.meta["chunk"], fR.meta["chunk"], fr.c, fR.c) == (100000, 30000, 3, 3)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fr.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    text = _run(tmp_path, 2, ["kmer_numba.py", "-i", str(q), "-k", "27", "-c", "3"], chunk=30000, dbg_chunk=100000)
+    assert rows_of(text) == fR.rows
+    z, ref = np.load(str(q) + "_db_brkpt.npz"), np.load(fr.brkpt)
+    assert z["parameters"].tolist() == ref["parameters"].tolist()
+    sel, rsel = z["counts"] > 0, ref["counts"] > 0
+    o, ro = np.argsort(z["keys"][sel], kind="stable"), np.argsort(ref["keys"][rsel], kind="stable")
+    for a in ("keys", "values", "counts"):
+        assert np.array_equal(z[a][sel][o], ref[a][rsel][ro]), a
+    z, ref = np.load(str(q) + "_rdb_brkpt.npz"), np.load(fR.brkpt)
+    for a in ("parameters", "keys", "values"):
+        assert z[a].tolist() == ref[a].tolist(), a
