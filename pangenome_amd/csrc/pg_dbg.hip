@@ -130,7 +130,7 @@ struct TileDesc {
 // reference window's key and both masks (:1069-1080); the reference inserts
 // that window, so g's record would OR nothing new and is not emitted.  The
 // drift delta only decides how much is skipped, never what is inserted.
-constexpr int DRIFT = 512;                    // searched offsets: [-DRIFT, DRIFT]
+constexpr int DRIFT = (PG_EXP_BITS & 128) ? 384 : (PG_EXP_BITS & 256) ? 256 : 512;  // searched offsets: [-DRIFT, DRIFT]
 constexpr int RSPAN = TILE + 2 * DRIFT + 96;  // staged reference bytes
 constexpr int NANCH = 3;                      // anchors per tile
 constexpr int ALEN = 32;                      // anchor length (bytes)

@@ -66,22 +66,32 @@ import numpy as np
 from . import host
 
 SENTINEL = 2 ** 64 - 1
+# A shard whose planned dBG pass holds more forward bases than this streams
+# its exchange in chunks of this size (exchange_stream; C5: 3.75 Gbp per GPU
+# in 4 chunks).  C3 / C4 shards (0.5-0.63 Gbp) exchange whole.
+STREAM_BASES = 1 << 30
 
 
 def _is_cuda(device) -> bool:
     return getattr(device, "type", str(device)).startswith("cuda")
 
 
-def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bool, group=None):
-    """Owner all-to-all + OR-merge + rdBG rule on the owner partition.
-    Returns (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent)."""
+def _comm_device(device, group):
+    """(stage through host memory?, the device collectives run on): gloo moves
+    host tensors only."""
     import torch
     import torch.distributed as dist
-
-    # gloo moves host tensors only: stage device buffers through host memory
     stage = _is_cuda(device) and dist.get_backend(group) == "gloo"
-    comm = torch.device("cpu") if stage else device
+    return stage, (torch.device("cpu") if stage else device)
 
+
+def _route(table, world: int, device, group=None):
+    """This rank's table -> owner runs of 16-byte records (pg_dbg_partition)
+    -> one all-to-all.  Returns (the records this rank owns as an (n, 2)
+    int64 tensor on `device`, bytes sent to other ranks)."""
+    import torch
+    import torch.distributed as dist
+    stage, comm = _comm_device(device, group)
     counts = table.partition(world)
     total = int(counts.sum())
     send = torch.empty((max(total, 1), 2), dtype=torch.int64, device=device)
@@ -97,16 +107,120 @@ def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bo
                            input_split_sizes=counts.astype(np.int64).tolist(), group=group)
     if stage:
         recv = recv.to(device)
+    rank = dist.get_rank(group)
+    return recv[:nrecv], 16 * (total - int(counts[rank]))
+
+
+def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None):
+    """OR-merge the owned records into a fresh owner table, rdBG rule on it;
+    global (n_dbg, n_rdbg) by a sum all-reduce.  Returns (n_dbg_total,
+    n_rdbg_total, n_rdbg_local)."""
+    import torch
+    import torch.distributed as dist
+    _, comm = _comm_device(device, group)
     flag = torch.tensor([1 if sentinel_local else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     if _is_cuda(device):
         torch.cuda.synchronize(device)
     # the n<k sentinel key belongs to one owner: rank 0
-    table.merge(recv.data_ptr(), nrecv, sentinel=bool(flag.item()) and rank == 0)
+    n = int(recv.shape[0])
+    table.merge(recv.data_ptr(), n, sentinel=bool(flag.item()) and rank == 0)
     st = table.build_rdbg()
     sums = torch.tensor([st.n_dbg, st.n_rdbg], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
-    return int(sums[0].item()), int(sums[1].item()), int(st.n_rdbg), 16 * (total - int(counts[rank]))
+    return int(sums[0].item()), int(sums[1].item()), int(st.n_rdbg)
+
+
+def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bool, group=None):
+    """Owner all-to-all + OR-merge + rdBG rule on the owner partition.
+    Returns (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent)."""
+    recv, sent = _route(table, world, device, group)
+    return _owner_reduce(table, recv, rank, device, sentinel_local, group) + (sent,)
+
+
+def stream_chunks(flags, seq_len, limit: int) -> list:
+    """A rank's flagged records as consecutive chunks of at most `limit`
+    forward bases each (a longer record is a chunk of its own): record flag
+    arrays, one per chunk."""
+    flags = np.asarray(flags, np.uint8)
+    out, cur, n = [], [], 0
+    for r in np.flatnonzero(flags).tolist():
+        L = int(seq_len[r])
+        if cur and n + L > limit:
+            out.append(cur)
+            cur, n = [], 0
+        cur.append(r)
+        n += L
+    if cur:
+        out.append(cur)
+    res = []
+    for c in out:
+        f = np.zeros(flags.shape[0], np.uint8)
+        f[c] = 1
+        res.append(f)
+    return res
+
+
+def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_records: int, rc0: bool, extra: int = 0,
+                    staged=None, group=None, on_chunk=None, compact_at: int = 1 << 26):
+    """The streaming exchange of SURVEY §8(e) for shards whose whole local
+    table does not fit beside the owner partition (C5: 3.75 Gbp per GPU).
+
+    Per chunk of records (stream_chunks): the local OR-table of the chunk
+    (`shard.build`, K1 already done for the whole shard), its entries to their
+    owners with one all-to-all (`_route`), appended to the owner's record log
+    on the device.  When the log has doubled since its last compaction (and
+    holds at least `compact_at` records) the owner OR-merges it and
+    re-exports the merged table as the new log (pg_dbg_merge, then
+    pg_dbg_partition into one run), so the log stays within ~2x the owner's
+    distinct entries.  After the last chunk the log is merged once and the
+    rdBG rule runs on the owner partition, exactly as exchange_and_reduce.
+    Every rank runs the same number of rounds (the maximum chunk count; a
+    rank out of records builds an empty chunk).  `staged` (rank 0's -r
+    checkpoint slots) goes into the first chunk only; `extra` (the n<k empty
+    records) too.  `on_chunk()` runs after each chunk's build (the dump
+    gathers its occurrence counts there).  Returns (n_dbg_total,
+    n_rdbg_total, n_rdbg_local, bytes_sent, rounds)."""
+    import torch
+    import torch.distributed as dist
+    _, comm = _comm_device(device, group)
+    nch = torch.tensor([len(chunks)], dtype=torch.int64, device=comm)
+    dist.all_reduce(nch, op=dist.ReduceOp.MAX, group=group)
+    rounds = max(1, int(nch.item()))
+    log, logn, base, sentinel, sent = [], 0, 0, False, 0
+    for i in range(rounds):
+        if staged is not None and i < 2:
+            if i == 0:
+                shard.stage(*staged)
+            else:
+                shard.stage(np.zeros(0, np.uint64))
+        f = chunks[i] if i < len(chunks) else np.zeros(n_records, np.uint8)
+        sentinel |= bool(shard.build(f, extra if i == 0 else 0, rc0))
+        if on_chunk is not None:
+            on_chunk()
+        recv, s = _route(shard, world, device, group)
+        sent += s
+        if recv.shape[0]:
+            log.append(recv)
+            logn += int(recv.shape[0])
+        if logn >= compact_at and logn >= 2 * base and len(log) > 1:
+            cat = torch.cat(log)
+            if _is_cuda(device):
+                torch.cuda.synchronize(device)
+            shard.merge(cat.data_ptr(), logn, False)
+            m = int(shard.partition(1)[0])
+            out = torch.empty((max(m, 1), 2), dtype=torch.int64, device=device)
+            if m:
+                shard.partition(1, out.data_ptr(), m)
+            del cat
+            log, logn, base = ([out[:m]] if m else []), m, m
+    if len(log) > 1:
+        allr = torch.cat(log)
+    elif log:
+        allr = log[0]
+    else:
+        allr = torch.empty((0, 2), dtype=torch.int64, device=device)
+    return _owner_reduce(shard, allr, rank, device, sentinel, group) + (sent, rounds)
 
 
 # ------------------------------------------------------------------ sharding
@@ -326,8 +440,12 @@ class DistRun:
     """The CLI stages of entry_point (:2073-2146) over world shards."""
 
     def __init__(self, qry: str, k: int, shard, comm: Comm, device=None, out=None, dev_index: int = 0,
-                 edge_chunk: int = host.CHUNK, dbg_chunk: int = host.CHUNK):
+                 edge_chunk: int = host.CHUNK, dbg_chunk: int = host.CHUNK, stream_bases: int = STREAM_BASES,
+                 compact_at: int = 1 << 26):
         self.qry, self.k, self.sh, self.comm = qry, min(max(1, int(k)), 27), shard, comm
+        self.stream_bases = int(stream_bases)              # a shard above this streams its exchange
+        self.compact_at = int(compact_at)
+        self.streamed = None
         self.edge_chunk = int(edge_chunk)                  # seq2graph's checkpoint size (:2073; tests vary it)
         self.dbg_chunk = int(dbg_chunk)                    # seq2rdbg's
         self.device, self.dev_index = device, dev_index
@@ -355,20 +473,68 @@ class DistRun:
     # ---------------------------------------------------------------- dBG
     def build_dbg(self, Ns, rc0, brkpt=""):
         """seq2rdbg (:1234-1268) over the shards; -r stages the checkpoint on rank 0."""
-        resume = None
+        resume, staged = None, None
         if brkpt and os.path.isfile(brkpt):
             offset, keys, values, counts = host.read_db_npz(brkpt)
             if self.rank == 0:
-                self.sh.stage(keys, values, counts)
+                staged = (keys, values, counts)
+                self.sh.stage(*staged)
             resume = host.resume_position(offset, self.S.ptr)
         flags, extra, ckpt = host.plan_dbg(self.S.seq_len, self.shape, bool(rc0), int(Ns), self.dbg_chunk,
                                            resume=resume, checkpoint=True)
+        # stream the exchange when the largest shard's planned bases exceed
+        # stream_bases (the same decision on every rank: global record table)
+        stream = self._max_local_bases(flags) > self.stream_bases
         if ckpt is not None:
             # <in>_db_brkpt.npz (:1255-1259): the last dump's state, built and dumped once
             cf, ce, last = ckpt
-            self.sh.build(self.S.local(cf, self.rank), ce if self.rank == 0 else 0, rc0)
-            self.dump(self.qry + "_db_brkpt", offset=int(self.S.ptr[last]))
+            if stream:
+                parts = []
+                chunks = stream_chunks(self.S.local(cf, self.rank), self.S.local(self.S.seq_len, self.rank),
+                                       self.stream_bases)
+                self._chunked_builds(chunks, ce if self.rank == 0 else 0, rc0, staged, parts)
+                self.dump(self.qry + "_db_brkpt", offset=int(self.S.ptr[last]), parts=parts)
+            else:
+                self.sh.build(self.S.local(cf, self.rank), ce if self.rank == 0 else 0, rc0)
+                self.dump(self.qry + "_db_brkpt", offset=int(self.S.ptr[last]))
+        if stream:
+            # C5 form: chunked local builds, one all-to-all per chunk into the
+            # owner's record log; the counts of each chunk gathered for the dump
+            self.stream_parts = []
+            chunks = stream_chunks(self.S.local(flags, self.rank), self.S.local(self.S.seq_len, self.rank),
+                                   self.stream_bases)
+            grab = lambda: self._grab_counts(self.stream_parts)
+            self.streamed = exchange_stream(self.sh, self.world, self.rank, self.device, chunks, self.R_local, rc0,
+                                            extra if self.rank == 0 else 0, staged, self.comm.group, grab,
+                                            self.compact_at)
+            return
         self.sentinel = self.sh.build(self.S.local(flags, self.rank), extra if self.rank == 0 else 0, rc0)
+
+    def _max_local_bases(self, flags) -> int:
+        sl = self.S.seq_len * np.asarray(flags, np.int64)
+        return max(int(self.S.local(sl, r).sum()) for r in range(self.world)) if self.world else 0
+
+    def _grab_counts(self, parts: list):
+        """This build's occurrence counts, gathered to rank 0 (appended to parts)."""
+        keys, masks, counts = self.sh.counts()
+        got = self.comm.gather_bytes(_pack(keys.astype(np.uint64), masks.astype(np.uint16).astype(np.int64),
+                                           counts.astype(np.int64)))
+        if self.rank == 0:
+            parts.extend(got)
+
+    def _chunked_builds(self, chunks, extra, rc0, staged, parts):
+        """Local builds of the chunks (same round count on every rank), counts
+        gathered after each: the dump of a streamed checkpoint."""
+        import torch
+        _, dev = _comm_device(self.device, self.comm.group)
+        n = torch.tensor([len(chunks)], dtype=torch.int64, device=dev)
+        self.comm.dist.all_reduce(n, op=self.comm.dist.ReduceOp.MAX, group=self.comm.group)
+        for i in range(max(1, int(n.item()))):
+            if staged is not None and i < 2:
+                self.sh.stage(*staged) if i == 0 else self.sh.stage(np.zeros(0, np.uint64))
+            f = chunks[i] if i < len(chunks) else np.zeros(self.R_local, np.uint8)
+            self.sh.build(f, extra if i == 0 else 0, rc0)
+            self._grab_counts(parts)
 
     def load_dbg(self, fn, rdbg: bool, rc0):
         """load_on_disk (:289-335) of a -d / -D file: staged on rank 0 (-d: the
@@ -384,11 +550,14 @@ class DistRun:
             self.sh.stage(keys, values, counts)
         self.sentinel = self.sh.build(zeros, 0, rc0)
 
-    def dump(self, fn, offset: int = 0):
-        """dump() (:243-261) of the global dBG, written by rank 0."""
-        keys, masks, counts = self.sh.counts()
-        parts = self.comm.gather_bytes(_pack(keys.astype(np.uint64), masks.astype(np.uint16).astype(np.int64),
-                                             counts.astype(np.int64)))
+    def dump(self, fn, offset: int = 0, parts=None):
+        """dump() (:243-261) of the global dBG, written by rank 0 (a streamed
+        build: from the counts gathered chunk by chunk)."""
+        if parts is None and self.streamed is not None:
+            parts = self.stream_parts
+        if parts is None:
+            parts = []
+            self._grab_counts(parts)
         if self.rank == 0:
             ks, ms, cs = [], [], []
             for p in parts:
@@ -406,8 +575,11 @@ class DistRun:
         membership = the union of the owners' rdBG keys."""
         if getattr(self, "reduced", False):
             return
-        n_dbg, n_rdbg, _, _ = exchange_and_reduce(self.sh, self.world, self.rank, self.device, self.sentinel,
-                                                  self.comm.group)
+        if self.streamed is not None:
+            n_dbg, n_rdbg = self.streamed[:2]
+        else:
+            n_dbg, n_rdbg, _, _ = exchange_and_reduce(self.sh, self.world, self.rank, self.device, self.sentinel,
+                                                      self.comm.group)
         own = np.ascontiguousarray(self.sh.owner_rdbg(), dtype=np.uint64)
         allk = np.sort(np.concatenate([p.view(np.uint64) for p in self.comm.allgather_bytes(own.view(np.uint8))]))
         if allk.shape[0] != n_rdbg:
@@ -495,7 +667,7 @@ def reduce_edges(parts):
 
 
 def entry_point(argv, out=None, shard_factory=None, device=None, dev_index: int = 0, edge_chunk: int = host.CHUNK,
-                dbg_chunk: int = host.CHUNK):
+                dbg_chunk: int = host.CHUNK, stream_bases: int = STREAM_BASES, compact_at: int = 1 << 26):
     """kmer.entry_point (:1971-2146) on every rank of an initialised process
     group; rank 0 prints.  `shard_factory(k)` makes the rank's backend
     (default: GpuShard on dev_index)."""
@@ -514,7 +686,7 @@ def entry_point(argv, out=None, shard_factory=None, device=None, dev_index: int 
     shard = shard_factory(k) if shard_factory else GpuShard(k, dev_index)
     comm = Comm(device)
     run = DistRun(qry, k, shard, comm, device=device, out=out, dev_index=dev_index, edge_chunk=edge_chunk,
-                  dbg_chunk=dbg_chunk)
+                  dbg_chunk=dbg_chunk, stream_bases=stream_bases, compact_at=compact_at)
     if dbs or rdb:                                      # :2073-2101
         if not rdb:
             run.say("load dBG from disk")
@@ -565,6 +737,7 @@ def main():
     else:
         dist.init_process_group(backend)
     try:
-        return entry_point(sys.argv, device=device, dev_index=dev_index)
+        return entry_point(sys.argv, device=device, dev_index=dev_index,
+                           stream_bases=int(os.environ.get("PG_DIST_STREAM_BASES", STREAM_BASES)))
     finally:
         dist.destroy_process_group()

@@ -209,22 +209,42 @@ class OracleShard:
         self.data = bytes(np.asarray(data, np.uint8))
         recs = seqio_records(self.data)
         cols = list(zip(*recs)) if recs else [(), (), (), ()]
-        return {name: np.asarray(col, np.int64) for name, col in zip(("seq_len", "hdr_start", "hdr_len", "ptr"), cols)}
+        self.meta = {name: np.asarray(col, np.int64)
+                     for name, col in zip(("seq_len", "hdr_start", "hdr_len", "ptr"), cols)}
+        self.run = None
+        return self.meta
 
     def stage(self, keys, masks=None, counts=None):
         raise NotImplementedError("OracleShard: staged npz slots are covered by the GPU tests")
 
     def build(self, flags, extra, rc0):
-        assert extra == 0 and np.all(np.asarray(flags) == 1), "OracleShard runs the default pass plan only"
+        """All records (the default plan), or a contiguous run of them (a
+        chunk of the streaming exchange: the run's bytes parse exactly as in
+        the shard, since they end before a header line or at the end)."""
         from oracle import oracle
+        flags = np.asarray(flags)
+        assert extra == 0, "OracleShard runs the default pass plan only"
         self.rc0 = bool(rc0)
-        self.run = oracle.OracleRun(self.data, self.k, 2 if rc0 else 0)
-        keys, masks = self.run.dbg()
+        if np.all(flags == 1):
+            self.run = self.cnt = oracle.OracleRun(self.data, self.k, 2 if rc0 else 0)
+        else:
+            idx = np.flatnonzero(flags)
+            if idx.size == 0:
+                self.cnt = None
+                self.table.load_dbg(np.zeros(0, np.uint64), np.zeros(0, np.uint16))
+                return self.table.sentinel
+            assert np.all(np.diff(idx) == 1), "a chunk is a contiguous run of records"
+            hs = self.meta["hdr_start"]
+            end = int(hs[idx[-1] + 1]) if idx[-1] + 1 < hs.shape[0] else len(self.data)
+            self.cnt = oracle.OracleRun(self.data[int(hs[idx[0]]):end], self.k, 2 if rc0 else 0)
+        keys, masks = self.cnt.dbg()
         self.table.load_dbg(keys, masks)
         return self.table.sentinel
 
     def counts(self):
-        return self.run.dbg_counts()
+        if self.cnt is None:
+            return np.zeros(0, np.uint64), np.zeros(0, np.uint16), np.zeros(0, np.uint8)
+        return self.cnt.dbg_counts()
 
     def partition(self, nparts, ptr=None, cap=0):
         return self.table.partition(nparts, ptr, cap)
@@ -239,6 +259,9 @@ class OracleShard:
         return self.table.rdbg_keys()
 
     def members(self, keys, n_records, rc0):
+        if self.run is None:                       # a streamed build ran chunks only
+            from oracle import oracle
+            self.run = oracle.OracleRun(self.data, self.k, 2 if rc0 else 0)
         self.run.set_rdbg(keys)
 
     def edges(self, flags, rc1):

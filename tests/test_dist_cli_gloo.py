@@ -19,7 +19,7 @@ from dist_util import ROOT, OracleShard, seqio_records, spawn_ranks
 from golden_util import Fixture
 
 
-def _cli_rank(rank, world, port, q, qry, argv):
+def _cli_rank(rank, world, port, q, qry, argv, kw=None):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
@@ -28,7 +28,7 @@ def _cli_rank(rank, world, port, q, qry, argv):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = io.StringIO()
     try:
-        pdist.entry_point(argv, out=out, shard_factory=OracleShard)
+        pdist.entry_point(argv, out=out, shard_factory=OracleShard, **(kw or {}))
     finally:
         dist.destroy_process_group()
     q.put((rank, out.getvalue()))
@@ -61,6 +61,40 @@ def test_dist_cli_matches_reference(name, world, tmp_path):
     assert np.array_equal(z["values"][sel][o], fx.dbg_masks)
     assert np.array_equal(z["counts"][sel][o], fx.dbg_counts)
     assert z["parameters"].tolist() == fx.db_params.tolist()
+
+
+@pytest.mark.parametrize("name,world,stream,compact", [("pan8_k27_c2", 2, 30_000, 1), ("pan8_k27_c2", 3, 1, 1),
+                                                        ("pan8_k15", 2, 50_000, 1 << 26), ("edge_k27", 2, 1, 1)])
+def test_dist_cli_streamed_exchange(name, world, stream, compact, tmp_path):
+    """The streaming exchange (exchange_stream, the C5 form of SURVEY 8(e)):
+    each rank's records in chunks of at most `stream` bases, one all-to-all
+    per chunk into the owner's record log, the log compacted (merged and
+    re-exported) whenever it doubles past `compact` records; the dump from
+    the counts gathered chunk by chunk.  Same outputs as the reference's."""
+    fx = Fixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text(fx.mcl)
+    argv = ["kmer_numba.py", "-i", str(q), "-k", str(fx.k), "-c", str(fx.c)]
+    outs = spawn_ranks(world, _cli_rank, (str(q), argv, {"stream_bases": stream, "compact_at": compact}))
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
+    assert rows_of(outs[0]) == fx.rows
+    z = np.load(str(q) + "_db.npz")
+    sel = z["counts"] > 0
+    o = np.argsort(z["keys"][sel], kind="stable")
+    assert np.array_equal(z["keys"][sel][o], fx.dbg_keys)
+    assert np.array_equal(z["values"][sel][o], fx.dbg_masks)
+    assert np.array_equal(z["counts"][sel][o], fx.dbg_counts)
+
+
+def test_stream_chunks():
+    from pangenome_amd.dist import stream_chunks
+    seq_len = np.array([5, 7, 3, 10, 2, 2], np.int64)
+    flags = np.array([1, 1, 0, 1, 1, 1], np.uint8)
+    ch = stream_chunks(flags, seq_len, 8)
+    assert [np.flatnonzero(c).tolist() for c in ch] == [[0], [1], [3], [4, 5]]
+    assert stream_chunks(np.zeros(3, np.uint8), seq_len[:3], 8) == []
+    assert [np.flatnonzero(c).tolist() for c in stream_chunks(flags, seq_len, 100)] == [[0, 1, 3, 4, 5]]
 
 
 def _bounds_case(buf, world):

@@ -59,7 +59,7 @@ def _exchange_rank_sharded(rank, world, port, q, shards):
     _exchange_rank(rank, world, port, q, shards[rank])
 
 
-def _cli_rank(rank, world, port, q, argv, chunk, cwd, dbg_chunk=2 ** 33):
+def _cli_rank(rank, world, port, q, argv, chunk, cwd, dbg_chunk=2 ** 33, stream=None):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -70,8 +70,9 @@ def _cli_rank(rank, world, port, q, argv, chunk, cwd, dbg_chunk=2 ** 33):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = io.StringIO()
     try:
+        kw = {} if stream is None else {"stream_bases": stream[0], "compact_at": stream[1]}
         pdist.entry_point(argv, out=out, device=torch.device("cuda", 0), dev_index=0, edge_chunk=chunk,
-                          dbg_chunk=dbg_chunk)
+                          dbg_chunk=dbg_chunk, **kw)
     finally:
         dist.destroy_process_group()
     q.put((rank, out.getvalue()))
@@ -81,8 +82,8 @@ def rows_of(text):
     return [ln for ln in text.split("\n") if len(ln.split("\t")) == 5 and ln.split("\t")[3] in ("+", "-")]
 
 
-def _run(tmp_path, world, argv, chunk=2 ** 33, dbg_chunk=2 ** 33):
-    outs = spawn_ranks(world, _cli_rank, (argv, chunk, str(tmp_path), dbg_chunk))
+def _run(tmp_path, world, argv, chunk=2 ** 33, dbg_chunk=2 ** 33, stream=None):
+    outs = spawn_ranks(world, _cli_rank, (argv, chunk, str(tmp_path), dbg_chunk, stream))
     assert all(rows_of(outs[r]) == [] for r in range(1, world))
     return outs[0]
 
@@ -112,6 +113,57 @@ def test_dist_cli_vs_reference(name, world, tmp_path):
     assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
     assert rows_of(text) == fx.rows
     _check_dump(str(q) + "_db.npz", fx.dbg_keys, fx.dbg_masks, fx.dbg_counts, fx.db_params)
+
+
+# the streaming exchange (dist.exchange_stream, SURVEY 8(e)'s C5 form) with
+# tiny chunks: (stream_bases, compact_at) -> every few records a chunk, the
+# owner log compacted through pg_dbg_merge + pg_dbg_partition(1)
+STREAMS = [(20_000, 1), (60_000, 1 << 26)]
+
+
+@pytest.mark.parametrize("name,world,stream", [("pan8_k27_c3", 2, STREAMS[0]), ("pan8_k27_n", 3, STREAMS[0]),
+                                               ("pan8_k27_chunk", 2, STREAMS[1]), ("edge_k27", 2, (1, 1))])
+def test_dist_cli_streamed_vs_reference(name, world, stream, tmp_path):
+    fx = Fixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text(fx.mcl)
+    argv = ["kmer_numba.py", "-i", str(q), "-k", str(fx.k), "-c", str(fx.c)]
+    if fx.ns is not None:
+        argv += ["-n", str(fx.meta["n"])]
+    text = _run(tmp_path, world, argv, fx.edge_chunk, stream=stream)
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
+    assert rows_of(text) == fx.rows
+    _check_dump(str(q) + "_db.npz", fx.dbg_keys, fx.dbg_masks, fx.dbg_counts, fx.db_params)
+
+
+def test_dist_cli_streamed_resume_and_checkpoints(tmp_path):
+    """Streamed: a -r resume (rank 0's staged checkpoint slots go into the
+    first chunk only) and a run writing <in>_db_brkpt.npz from chunked
+    builds, both against the reference's own files."""
+    fx = ResumeFixture("pan8_k27_r")
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    text = _run(tmp_path, 2, ["kmer_numba.py", "-i", str(q), "-k", str(fx.k), "-c", str(fx.c), fx.flag, fx.brkpt],
+                stream=STREAMS[0])
+    assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
+    assert rows_of(text) == fx.rows
+    if fx.graph is not None:
+        _check_dump(str(q) + "_db.npz", fx.graph["dbg_keys"], fx.graph["dbg_masks"], fx.graph["dbg_counts"])
+    d2 = tmp_path / "ck"
+    d2.mkdir()
+    q2 = d2 / "input.fsa"
+    q2.write_bytes(fx.fasta)
+    (d2 / "input.fsa_rdbg_weight.xyz.mcl").write_text("")
+    _run(d2, 2, ["kmer_numba.py", "-i", str(q2), "-k", "27", "-c", "3"], chunk=30000, dbg_chunk=100000,
+         stream=STREAMS[0])
+    z, ref = np.load(str(q2) + "_db_brkpt.npz"), np.load(fx.brkpt)
+    assert z["parameters"].tolist() == ref["parameters"].tolist()
+    sel, rsel = z["counts"] > 0, ref["counts"] > 0
+    o, ro = np.argsort(z["keys"][sel], kind="stable"), np.argsort(ref["keys"][rsel], kind="stable")
+    for a in ("keys", "values", "counts"):
+        assert np.array_equal(z[a][sel][o], ref[a][rsel][ro]), a
 
 
 def test_dist_cli_reload_d_and_D(tmp_path):
