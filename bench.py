@@ -170,11 +170,11 @@ def main():
 
     def step(ctx, i):
         d = d_in[i % len(d_in)]
+        if world == 1:                      # parse + seq2rdbg + dbg2rdbg in one call (pg_build_device)
+            st = ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d)
+            return st, st, st.n_dbg, st.n_rdbg, 0
         ctx.set_fasta_device(d.data_ptr(), d.numel(), keepalive=d)
         ctx.parse()
-        if world == 1:                      # seq2rdbg + dbg2rdbg in one call (pg_build)
-            st = ctx.build(None, 0, True)
-            return st, st, st.n_dbg, st.n_rdbg, 0
         st_b = ctx.build_dbg(None, 0, True)
         n_dbg, n_rdbg, _, sent = exchange_and_reduce(ctx, world, rank, device, bool(st_b.sentinel))
         return st_b, ctx.stats(), n_dbg, n_rdbg, sent

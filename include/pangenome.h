@@ -88,6 +88,13 @@ int pg_parse_host(pg_ctx* ctx, const uint8_t* host_bytes, uint64_t nbytes, uint6
  * the record table is available afterwards (pg_records). */
 int pg_build_host(pg_ctx* ctx, const uint8_t* host_bytes, uint64_t nbytes, int rc0, uint64_t* n_rdbg,
                   pg_stats* stats);
+/* pg_set_fasta_device + pg_parse + pg_build(NULL, 0, rc0) in one call, for a
+ * FASTA already in HBM (seq2rdbg + dbg2rdbg, kmer_numba.py:1234-1321, no -n
+ * limit or checkpoint): the host step between the parse and the build runs
+ * in C++ with no return to the caller.  The bytes must outlive the call;
+ * the record table is available afterwards (pg_records). */
+int pg_build_device(pg_ctx* ctx, const uint8_t* device_bytes, uint64_t nbytes, int rc0, uint64_t* n_rdbg,
+                    pg_stats* stats);
 /* Per-record table (arrays of n_records): compacted sequence length, header
  * byte span (qid = bytes[hdr_start : hdr_start+hdr_len], '>' included,
  * :160) and seqio's resume pointer (:153). Any pointer may be NULL. */

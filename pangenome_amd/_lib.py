@@ -53,6 +53,7 @@ SIGNATURES = {
     "pg_build_rdbg": (C.c_int, [_P, _U64P, _SP]),
     "pg_build": (C.c_int, [_P, _P, C.c_int, C.c_int, _U64P, _SP]),
     "pg_build_host": (C.c_int, [_P, _P, C.c_uint64, C.c_int, _U64P, _SP]),
+    "pg_build_device": (C.c_int, [_P, _P, C.c_uint64, C.c_int, _U64P, _SP]),
     "pg_dbg_export": (C.c_int, [_P, _P, _P, C.c_uint64, _U64P]),
     "pg_rdbg_export": (C.c_int, [_P, _P, C.c_uint64, _U64P]),
     "pg_dbg_partition": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
@@ -213,6 +214,17 @@ class Context:
         n = C.c_uint64()
         check(self.lib.pg_build_host(self.h, C.c_void_p(host_ptr), nbytes, int(bool(rc0)), C.byref(n), C.byref(st)),
               "pg_build_host")
+        self.n_records, self.n_bases = st.n_records, st.n_bases
+        return st
+
+    def build_device(self, dev_ptr: int, nbytes: int, rc0: bool = True, keepalive=None) -> PgStats:
+        """set_fasta_device + parse + build of every record in one call
+        (pg_build_device) for a FASTA already in HBM."""
+        st = PgStats()
+        n = C.c_uint64()
+        self._keepalive = keepalive
+        check(self.lib.pg_build_device(self.h, C.c_void_p(dev_ptr), nbytes, int(bool(rc0)), C.byref(n),
+                                       C.byref(st)), "pg_build_device")
         self.n_records, self.n_bases = st.n_records, st.n_bases
         return st
 

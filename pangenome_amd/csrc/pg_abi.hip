@@ -88,10 +88,10 @@ void pg_destroy(pg_ctx* x) {
   for (auto* b : bufs) b->release();
   c.rec_pack.release();
   c.h_pin.release();
+  c.h_out.release();
   c.tile_pin.release();
   c.t0.destroy();
   c.t1.destroy();
-  c.t5.destroy();
   c.t6.destroy();
   for (auto& e : c.ev)
     if (e) (void)hipEventDestroy(e);
@@ -208,6 +208,30 @@ int pg_build(pg_ctx* x, const uint8_t* rec_flags, int extra_empty, int rc0, uint
     pg::build_rdbg(x->c);                      // (the degree scan ran inside the build)
     if (n_rdbg) *n_rdbg = x->c.n_rdbg;
     fill_stats(x->c, stats);
+  });
+}
+
+int pg_build_device(pg_ctx* x, const uint8_t* dev, uint64_t n, int rc0, uint64_t* n_rdbg, pg_stats* stats) {
+  return guard([&] {
+    if (!x || (!dev && n)) throw pg::Error(PG_EINVAL, "pg_build_device: bad arguments");
+    pg::Ctx& c = x->c;
+    PG_HIP(hipSetDevice(c.device));
+    if (reinterpret_cast<uintptr_t>(dev) % 16 != 0) {
+      c.fasta_own.reserve(n + 64);
+      PG_HIP(hipMemcpyAsync(c.fasta_own.p, dev, n, hipMemcpyDeviceToDevice, c.stream));
+      c.d_fasta = c.fasta_own.as<uint8_t>();
+    } else {
+      c.d_fasta = dev;
+    }
+    c.n_bytes = n;
+    c.parsed = c.built = c.reduced = false;
+    auto t0 = std::chrono::steady_clock::now();
+    pg::parse_fasta(c);
+    c.ms_parse = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    pg::build_dbg(c, nullptr, 0, rc0 != 0);
+    pg::build_rdbg(c);
+    if (n_rdbg) *n_rdbg = c.n_rdbg;
+    fill_stats(c, stats);
   });
 }
 

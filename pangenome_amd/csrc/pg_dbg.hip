@@ -58,7 +58,8 @@ enum : unsigned { F_OVF_FULL = 1u, F_A_OVER = 2u, F_LDS_SPILL = 4u, F_SPLIT_OVER
 constexpr int N_FLAGS = 16;
 
 // overflow table: linear probing on 16-byte slots (CAS on key1, then OR);
-// a full table sets F_OVF_FULL in *fl
+// a full table sets F_OVF_FULL in *fl (C3: ~2 % of the keys land here, in
+// buckets that drew a third key)
 __device__ int ovf_or(const TableView& T, uint64_t c, uint32_t mw, unsigned* fl) {
   const unsigned long long key1 = (unsigned long long)c + 1ull;
   uint64_t slot = fmix64(c) & T.omask;
@@ -1334,6 +1335,21 @@ __global__ void k_gather_segs(const unsigned long long* __restrict__ seg, uint64
 // Small fills (counters, flags, drift hints, the overflow table) in ONE
 // launch, one grid row per region, instead of a hipMemsetAsync each (~5 us of
 // dispatch apiece on the critical stream).
+// The build's last readback in one launch: the stage C counters per block,
+// the flags and (spec) stage A's region cursors, copied into pinned host
+// memory by plain vector stores (three DMA copies cost ~20 us of copy-engine
+// starts on the critical path).
+struct Gather { const unsigned long long* src[3]; uint32_t n[3], stride[3]; };
+__global__ void __launch_bounds__(256) k_gather_out(Gather g, unsigned long long* __restrict__ dst) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < g.n[j]; i += gridDim.x * 256u)
+      dst[o + i] = g.src[j][(uint64_t)i * g.stride[j]];
+    o += g.n[j];
+  }
+}
+
 struct Fill { uint4* p; uint64_t n16; unsigned v; };
 constexpr int NFILL = 8;
 struct Fills { Fill r[NFILL]; };
@@ -1465,12 +1481,12 @@ struct ACount {
   unsigned sentinel = 0, bits = 0;
 };
 // stage A's counts and flags from a pinned copy of ctrA and the flags
-static ACount stageA_counts(const unsigned long long* h, const unsigned* fl) {
+static ACount stageA_counts(const unsigned long long* h, const unsigned* fl, int stride = CSTRIDE) {
   ACount a;
   for (int p = 0; p < NBIN; ++p) {
     uint64_t bin = 0;
     for (int x = 0; x < 8; ++x) {
-      const uint64_t n = h[CSTRIDE * (p * 8 + x)];
+      const uint64_t n = h[stride * (p * 8 + x)];
       a.total += n;
       bin += n;
       a.maxreg = std::max(a.maxreg, n);
@@ -1513,7 +1529,6 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
   double capx = 1.15;
   uint64_t ovf_mult = 1;
   double rseg_frac = c.r_ratio > 0 ? std::min(2.0, 1.5 * c.r_ratio + 0.002) : 2.0;
-  c.t5.init();
   c.t6.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
     const int fp = std::max(cb, bb - RANGE_BITS);
@@ -1562,8 +1577,19 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
     fl.add(c.ovf.p, sizeof(Slot) * ovf);
     fl.add(c.ctrS.p, 8 * ctr_words);
     fl.add(c.flags.as<unsigned>() + 4, 16);                   // stage B/C bits (not the sentinel)
-    c.t5.start(c.stream);
-    fl.launch(c.stream);
+    // the fills (C3: the 64 MB overflow table, 12 us) go on the side stream,
+    // behind its share of stage A (which touches none of them), so that they
+    // run beside stage A's last work pass; stage B waits for them
+    // (this is also where the main stream joins stage A's side stream, and
+    // where stage A's timer stops when the build queued it unjoined: one
+    // wait and one event between stage A's last work pass and k_split)
+    fl.launch(c.stream2);
+    PG_HIP(hipEventRecord(c.ev[15], c.stream2));
+    PG_HIP(hipStreamWaitEvent(c.stream, c.ev[15], 0));
+    if (c.t1_open) {
+      c.t1.stop(c.stream);
+      c.t1_open = false;
+    }
     Recs in{c.recA_key.as<unsigned long long>(), c.recA_mw.as<uint32_t>(), c.ctrA.as<unsigned long long>(), c.capA,
             8};
     for (size_t i = 0; i < lv.size(); ++i) {
@@ -1583,23 +1609,28 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
     hipLaunchKernelGGL(k_build_range, dim3(grid), dim3(RB_T), 0, c.stream, in, c.tv, rbits, (uint32_t)nparts, ro,
                        c.flags.as<unsigned>());
     PG_HIP(hipGetLastError());
-    c.t5.stop(c.stream);
     c.t6.stop(c.stream);
-    const size_t kbytes = 8 * RB_CTR * grid, abytes = spec ? 8 * CSTRIDE * NREG : 0;
-    c.h_pin.reserve(kbytes + 4 * N_FLAGS + abytes);
-    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.k5_ctr.p, kbytes, hipMemcpyDeviceToHost, c.stream));
-    PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + kbytes, c.flags.p, 4 * N_FLAGS, hipMemcpyDeviceToHost, c.stream));
-    if (spec)
-      PG_HIP(hipMemcpyAsync(c.h_pin.as<uint8_t>() + kbytes + 4 * N_FLAGS, c.ctrA.p, abytes, hipMemcpyDeviceToHost,
-                            c.stream));
+    // one readback: stage C's counters, the flags, (spec) stage A's cursors
+    // (one word per region: stride CSTRIDE on the device, 1 in the copy)
+    const size_t kbytes = 8 * RB_CTR * grid, abytes = spec ? 8 * NREG : 0;
+    c.h_out.reserve(kbytes + 4 * N_FLAGS + abytes);
+    Gather gth{{c.k5_ctr.as<unsigned long long>(), c.flags.as<unsigned long long>(), c.ctrA.as<unsigned long long>()},
+               {(uint32_t)(RB_CTR * grid), (uint32_t)(N_FLAGS / 2), spec ? (uint32_t)NREG : 0u},
+               {1u, 1u, (uint32_t)CSTRIDE}};
+    hipLaunchKernelGGL(k_gather_out, dim3(4), dim3(256), 0, c.stream, gth,
+                       reinterpret_cast<unsigned long long*>(c.h_out.dp));
+    PG_HIP(hipGetLastError());
     c.sync();
-    c.ms_scan = c.t5.ms();
     c.ms_range = c.t6.ms();
-    c.ms_split = c.ms_scan - c.ms_range;
-    const unsigned long long* h = c.h_pin.as<unsigned long long>();
-    const unsigned* hf = reinterpret_cast<const unsigned*>(c.h_pin.as<uint8_t>() + kbytes);
+    float tsplit = 0.f;                        // stage A's end (t1) to stage C's start
+    PG_HIP(hipEventElapsedTime(&tsplit, c.t1.b, c.t6.a));
+    c.ms_split = (double)tsplit;
+    c.ms_scan = c.ms_split + c.ms_range;
+    const unsigned long long* h = c.h_out.as<unsigned long long>();
+    const unsigned* hf = reinterpret_cast<const unsigned*>(c.h_out.as<uint8_t>() + kbytes);
     if (spec) {                                // stage A's exact counts, and whether it fit
-      a = stageA_counts(reinterpret_cast<const unsigned long long*>(c.h_pin.as<uint8_t>() + kbytes + 4 * N_FLAGS), hf);
+      a = stageA_counts(reinterpret_cast<const unsigned long long*>(c.h_out.as<uint8_t>() + kbytes + 4 * N_FLAGS), hf,
+                        1);
       c.sentinel = a.sentinel ? 1 : 0;
       spec = false;
       if (a.bits & F_A_OVER) return false;
@@ -1653,7 +1684,10 @@ static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, const B
 // regions reset, no short records yet), SA_MORE adds tiles, SA_TAIL adds the
 // short records, the n<k flag and the staged slots (no tiles).
 enum { SA_WHOLE = 0, SA_FIRST = 1, SA_MORE = 2, SA_TAIL = 3 };
-static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int extra_empty, int part = SA_WHOLE) {
+// join = false: the side stream is joined (and t1 stopped) by finish_build,
+// behind the stage B/C fills it queues on the side stream.
+static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int extra_empty, int part = SA_WHOLE,
+                           bool join = true) {
   const uint64_t shift = pow5(c.k - 1);
   hipStream_t s0 = c.stream, s1 = c.stream2;
   FillList fl;
@@ -1731,6 +1765,10 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
                        c.preload.as<PreEnt>(), c.n_preload, c.tv, O);
     PG_HIP(hipGetLastError());
   }
+  if (!join) {
+    c.t1_open = true;
+    return;
+  }
   PG_HIP(hipEventRecord(c.ev[15], s1));                       // join: s0 continues after s1's work
   PG_HIP(hipStreamWaitEvent(s0, c.ev[15], 0));
   c.t1.stop(s0);
@@ -1746,7 +1784,13 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   std::vector<uint8_t> flag(R, 1);
   if (h_rec_flag)
     for (uint64_t r = 0; r < R; ++r) flag[r] = h_rec_flag[r] & 1;
-  if (R) PG_HIP(hipMemcpyAsync(c.rec_flag.p, flag.data(), R, hipMemcpyHostToDevice, c.stream));
+  // (the device copy of the flags is kept while it holds these: a pageable
+  // upload costs a staged copy on the critical path)
+  if (R && !(c.dev_flag_p == c.rec_flag.p && c.dev_flag == flag)) {
+    PG_HIP(hipMemcpyAsync(c.rec_flag.p, flag.data(), R, hipMemcpyHostToDevice, c.stream));
+    c.dev_flag = flag;
+    c.dev_flag_p = c.rec_flag.p;
+  }
   uint64_t nshort = 0, nlong = 0;
   for (uint64_t r = 0; r < R; ++r)
     if (flag[r]) {
@@ -1777,7 +1821,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   // spec form: one host round trip instead of two); the table is then sized
   // from the last build's records per window, 5 % up
   if (c.u_ratio > 0 && !c.region_cap_force) {
-    enqueue_stageA(c, cap, ntiles, rc0, extra_empty);
+    enqueue_stageA(c, cap, ntiles, rc0, extra_empty, SA_WHOLE, false);
     a.total = (uint64_t)(c.u_ratio * 1.05 * (double)c.windows_fw) + extra;
     a.maxreg = cap;
     a.maxbin = 8 * cap;
@@ -1920,6 +1964,8 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
     c.t1.init();
     c.t1.start(c.stream);
     fl.launch(c.stream);
+    PG_HIP(hipEventRecord(c.ev[0], c.stream));           // the side stream (stage B/C fills) after all of this
+    PG_HIP(hipStreamWaitEvent(c.stream2, c.ev[0], 0));
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
     if (n) {
       hipLaunchKernelGGL(k_slots_emit, dim3(grid_for(n, 4 * IBLOCK, 4096)), dim3(IBLOCK), 0, c.stream,
@@ -2002,6 +2048,8 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
   if (!broken && (done != R || !started)) broken = true;
   if (!broken) {
     if (R) PG_HIP(hipMemsetAsync(c.rec_flag.p, 1, R, c.stream));
+    c.dev_flag.assign(R, 1);
+    c.dev_flag_p = c.rec_flag.p;
     c.windows_fw = 0;
     for (uint64_t r = 0; r < R; ++r) {
       const int64_t m = c.h_rec_len[r];

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -53,13 +54,16 @@ struct DevBuf {
 // on the stream (a pageable destination costs a staged, synchronous copy).
 struct PinBuf {
   void* p = nullptr;
+  void* dp = nullptr;             // device view (coherent buffers written by kernels)
   size_t cap = 0;
+  unsigned flags = hipHostMallocDefault;
   void reserve(size_t bytes) {
     if (bytes <= cap) return;
     if (p) PG_HIP(hipHostFree(p));
-    p = nullptr;
+    p = dp = nullptr;
     size_t nb = bytes + bytes / 8 + 256;
-    PG_HIP(hipHostMalloc(&p, nb, hipHostMallocDefault));
+    PG_HIP(hipHostMalloc(&p, nb, flags));
+    if (flags & hipHostMallocMapped) PG_HIP(hipHostGetDevicePointer(&dp, p, 0));
     cap = nb;
   }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
@@ -132,6 +136,10 @@ struct Ctx {
   int kb = 0, cbits = 0, hash_k = 0, bb = 0;   // key bits, coarse bin bits, k of tv's hash, bucket bits
   uint64_t cap = 0;               // primary buckets (power of two)
   uint64_t ovf_cap = 0;           // overflow slots (power of two)
+  PinBuf h_out{nullptr, nullptr, 0, hipHostMallocMapped | hipHostMallocCoherent};   // k_gather_out's target
+  std::vector<uint8_t> dev_flag;  // the record flags last uploaded to rec_flag (at dev_flag_p)
+  const void* dev_flag_p = nullptr;
+  bool t1_open = false;           // stage A queued, its side stream not yet joined (finish_build joins)
   DevBuf flags;                   // [0] sentinel seen, [1] stage A bits, [4] stage B/C bits
   uint64_t n_dbg = 0, n_rdbg = 0, n_canon = 0, sentinel = 0;
   bool built = false, reduced = false;
@@ -191,11 +199,24 @@ struct Ctx {
   uint64_t dump_size = 0, dump_sentinel = 0;
 
   // timings of the last calls (ms, HIP events on `stream`)
-  Timer t0, t1, t5, t6;
+  Timer t0, t1, t6;
   double ms_parse = 0, ms_clear = 0, ms_insert = 0, ms_short = 0, ms_scan = 0, ms_split = 0, ms_range = 0;
   double ms_total_build = 0;
 
-  void sync() { PG_HIP(hipStreamSynchronize(stream)); }
+  // Wait for the stream by polling it: the blocking wait's wake-up costs
+  // ~20-30 us per host round trip on the build's critical path (two per
+  // build).  After 50 ms of polling it blocks (long waits, and errors come
+  // back through the blocking call).
+  void sync() {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipStreamQuery(stream);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) break;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    }
+    PG_HIP(hipStreamSynchronize(stream));
+  }
 };
 
 // pg_parse.hip

@@ -511,7 +511,9 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     c.rec_len.reserve(8 * (rcap + 1));
     c.rec_hdr.reserve(16 * (rcap + 1));
     c.rec_ptr.reserve(8 * (rcap + 1));
+    const size_t fcap = c.rec_flag.cap;
     c.rec_flag.reserve(rcap + 1);
+    if (c.rec_flag.cap != fcap) c.dev_flag_p = nullptr;     // new memory (possibly at the old address)
     c.rec_pack.reserve(64 + 40 * rcap);
     c.h_pin.reserve(64 + 40 * rcap);
   };

@@ -218,3 +218,41 @@ def test_build_host_streamed(case):
             assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
             assert np.array_equal(ctx.rdbg(), rr)
         ctx.close()
+
+
+def test_build_device_one_call(oracle_mod):
+    """pg_build_device (set_fasta_device + parse + build in one call, the
+    bench's step): the oracle's dBG / rdBG, the record table of parse, with
+    the context alternating between inputs of different record counts (the
+    kept device copy of the record flags, the overflow table's skipped
+    clear, the one-launch readback)."""
+    import torch
+    from oracle import oracle
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    rng = np.random.default_rng(5)
+    acgt = np.frombuffer(b"ACGT", np.uint8)
+    recs = [acgt[rng.integers(0, 4, m)].tobytes() for m in (40_000, 5, 27, 28, 29, 40_000, 0, 30_000, 26)]
+    bufs = [synth.pangenome(12, 150_000, snp=1e-3, indel=1e-4, seed=11),
+            b"".join(b">r%d\n%s\n" % (i, r) for i, r in enumerate(recs)),
+            _mixed_fasta(5, (60, 17, 1000), nrec=10, reclen=20_000),
+            synth.pangenome(7, 90_000, snp=2e-3, indel=1e-4, seed=12)]
+    refs = []
+    for b in bufs:
+        o = oracle.OracleRun(b, 27, 2)
+        dk, dm = o.dbg()
+        refs.append((_build_ref(b)[0], dk, dm, o.rdbg()))
+    ctx = Context(27)
+    dev = [torch.frombuffer(bytearray(b), dtype=torch.uint8).to("cuda") for b in bufs]
+    for i in (0, 1, 2, 3, 0, 0, 3, 1):
+        st = ctx.build_device(dev[i].data_ptr(), dev[i].numel(), True, keepalive=dev[i])
+        rec, dk, dm, rk = refs[i]
+        assert (st.n_dbg, st.n_rdbg) == (dk.shape[0], rk.shape[0]), i
+        got = ctx.records()
+        for key in rec:
+            assert np.array_equal(got[key], rec[key]), (i, key)
+        keys, masks = ctx.dbg()
+        assert np.array_equal(keys, dk) and np.array_equal(masks, dm), i
+        assert np.array_equal(ctx.rdbg(), rk), i
+    ctx.close()
+
