@@ -1663,7 +1663,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
 }
 
 // chunks of the tile list whose work pass overlaps the next coverage pass
-constexpr int K3_CHUNKS = 4;
+constexpr int K3_CHUNKS = (PG_EXP_BITS & 4096) ? 2 : (PG_EXP_BITS & 512) ? 4 : (PG_EXP_BITS & 1024) ? 5 : (PG_EXP_BITS & 2048) ? 6 : 3;
 constexpr int K3_WBLK = 2;                    // work blocks per CU (chunked form)
 constexpr uint64_t K3_CHUNK_MIN = 1024;       // coverage groups per chunk below which one chunk runs
 
