@@ -243,7 +243,7 @@ constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long 
 // the full +-DRIFT with the whole block (rare: ~1 % of tiles).  best[] gets
 // (|delta| << 16 | drift) of every matching candidate (atomicMin: the
 // smallest drift wins).  The hints and drift sets are published by the caller.
-constexpr int HWIN2 = 56;
+constexpr int HWIN2 = (PG_EXP_BITS & 32768) ? 40 : 56;
 constexpr int QM = 4;                         // member tiles per coverage block (one stripe)
 struct MemGeo {                               // a member tile: record, staging window, hints
   long long rs, rn, a0, hi;
@@ -1664,7 +1664,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
 
 // chunks of the tile list whose work pass overlaps the next coverage pass
 constexpr int K3_CHUNKS = (PG_EXP_BITS & 4096) ? 2 : (PG_EXP_BITS & 512) ? 4 : (PG_EXP_BITS & 1024) ? 5 : (PG_EXP_BITS & 2048) ? 6 : 3;
-constexpr int K3_WBLK = 2;                    // work blocks per CU (chunked form)
+constexpr int K3_WBLK = (PG_EXP_BITS & 8192) ? 3 : (PG_EXP_BITS & 16384) ? 1 : 2;                    // work blocks per CU (chunked form)
 constexpr uint64_t K3_CHUNK_MIN = 1024;       // coverage groups per chunk below which one chunk runs
 
 static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, const BinOut& O) {
