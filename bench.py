@@ -1,12 +1,18 @@
 #!/usr/bin/env python3
 """Gbp/s of the k-mer -> rdBG build at k=27 on MI355X (BASELINE.json metric).
 
-One step = one pass of the hot path over this rank's synthetic pangenome
-shard, FASTA already resident in HBM: K1 parse -> K3 dBG insert (both
-strands, the reference's default -c 2) -> [N>1: owner all-to-all over RCCL
-and OR-merge] -> K5 degree scan + rdBG compaction, ending with the rdBG key
-count on the host.  Weak scaling: every rank owns the same number of genomes
-(C3 = 100 x 5 Mbp per GPU; 8 GPUs = 800 genomes, C4-scale).
+One step = the window SURVEY.md §8(d) times, over this rank's synthetic
+pangenome shard: FASTA bytes in a page-cache-warm np.memmap of the file
+(kmer.seq2bytes, what the CLI passes; the reference's seq2bytes,
+kmer_numba.py:117-119) -> H2D through the pinned staging ring -> K1 parse ->
+K3 dBG build (both strands, the reference's default -c 2) -> [N>1: owner
+all-to-all over RCCL and OR-merge] -> rdBG rule, ending with the rdBG key
+count on the host (pg_build_host).  Weak scaling: every rank owns 100 x 5 Mbp
+genomes (C3 per GPU; 8 GPUs = 800 genomes).
+
+The same build from HBM-resident input (pg_build_device) is timed too
+(`path.device_resident_gbps`); its per-kernel HIP-event spans give the
+roofline of the dominant kernel.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c4]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -14,9 +20,12 @@ count on the host.  Weak scaling: every rank owns the same number of genomes
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import shutil
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -29,26 +38,43 @@ K = 27
 
 
 def workload(config: str, rank: int, world: int):
-    """[(fasta, digest name or None), ...] batches of this rank, and the description.
-    C3 alternates two distinct batches of the same population (genomes
-    r*100.. and (world+r)*100..), so that no step rebuilds the input the step
-    before it built."""
-    from pangenome_amd import synth
+    """[(genome spec, digest name or None), ...] batches of this rank, the
+    digest of the global population (N>1), and the description.
+
+    N=1, C3: two batches of the same population alternate (genomes 0-99 =
+    c3a, 100-199 = c3b), so no step rebuilds the input the step before it
+    built.  N>1: the population is genomes 0 .. 100N-1; rank r holds block r
+    on even steps and block (r+1) mod N on odd ones, so every step builds the
+    same global population (one oracle digest per N, tests/golden/scale/popN)
+    from a different shard than the step before."""
     if config == "c2":
-        return [(synth.ecoli_like(), "c2")], "C2: synthetic E. coli K-12 stand-in, 4,641,652 bp, 1 record"
-    if config == "c3":
-        n = 100
-        b = [(synth.pangenome(n, 5_000_000, snp=1e-3, indel=1e-4, first_index=(i * world + rank) * n),
-              ("c3a", "c3b")[i] if world == 1 else None) for i in range(2)]
-        return b, ("C3: 100 x 5 Mbp variants (0.1%% SNP, 0.01%% indel) per GPU and step, two alternating "
-                   "batches of the same population; %d genomes per step in total" % (n * world))
-    if config == "c4":
-        n = 1000 // world
-        return ([(synth.pangenome(n, 5_000_000, snp=1e-3, indel=1e-4, first_index=rank * n), None)],
-                "C4: 1000 x 5 Mbp variants sharded %d per GPU" % n)
+        return [("c2", "c2" if world == 1 else None)], None, "C2: synthetic E. coli K-12 stand-in, 4,641,652 bp, 1 record"
+    if config in ("c3", "c4"):
+        n = 100 if config == "c3" else 1000 // world
+        if world == 1:
+            if config == "c3":
+                return ([(("pan", n, 0), "c3a"), (("pan", n, 100), "c3b")], None,
+                        "C3: 100 x 5 Mbp variants (0.1% SNP, 0.01% indel), two alternating batches of the "
+                        "same population (genomes 0-99, 100-199)")
+            return [(("pan", n, 0), "c4")], None, "C4: 1000 x 5 Mbp variants (5 Gbp, 5.08 GB of FASTA) on one GPU"
+        blocks = [rank, (rank + 1) % world]
+        pop = ("pop%d" % world) if config == "c3" else "c4"
+        return ([(("pan", n, b * n), None) for b in blocks], pop,
+                "%s: %d x 5 Mbp variants per GPU and step (genomes 0..%d in total, each rank's block rotating "
+                "between steps)" % (config.upper(), n, n * world - 1))
     if config == "small":
-        return [(synth.pangenome(10, 1_000_000, first_index=rank * 10), None)], "small: 10 x 1 Mbp per GPU"
+        return [(("pan_small", 10, rank * 10), None)], None, "small: 10 x 1 Mbp per GPU"
     raise SystemExit("unknown --config %s" % config)
+
+
+def make_fasta(spec) -> bytes:
+    from pangenome_amd import synth
+    if spec == "c2":
+        return synth.ecoli_like()
+    kind, n, first = spec
+    if kind == "pan_small":
+        return synth.pangenome(n, 1_000_000, first_index=first)
+    return synth.pangenome(n, 5_000_000, snp=1e-3, indel=1e-4, first_index=first)
 
 
 def cpu_baseline(config: str, sample: bool = False):
@@ -108,16 +134,35 @@ def _digest(name):
     return json.load(open(p)) if os.path.isfile(p) else None
 
 
-def _full_check(ctx, dg):
-    """SHA-256 of the sorted dBG and rdBG against the oracle's digest."""
-    import hashlib
-    keys, masks = ctx.dbg()
+def _sha_dbg(keys, masks):
     h = hashlib.sha256()
     h.update(np.ascontiguousarray(keys, dtype="<u8").tobytes())
     h.update(np.ascontiguousarray(masks, dtype="<u2").tobytes())
-    ok_dbg = h.hexdigest() == dg["dbg_sha256"]
-    ok_rdbg = hashlib.sha256(np.ascontiguousarray(ctx.rdbg(), dtype="<u8").tobytes()).hexdigest() == dg["rdbg_sha256"]
-    return ok_dbg and ok_rdbg
+    return h.hexdigest()
+
+
+def _sha_rdbg(keys):
+    return hashlib.sha256(np.ascontiguousarray(np.sort(keys), dtype="<u8").tobytes()).hexdigest()
+
+
+def _gather_rdbg_sha(ctx, world, rank, device, rehearse):
+    """SHA-256 of the sorted union of the owners' rdBG keys (all-gathered)."""
+    import torch
+    import torch.distributed as dist
+    comm = torch.device("cpu") if rehearse else device
+    keys = torch.from_numpy(ctx.rdbg().view(np.int64)).to(comm)
+    n = torch.tensor([keys.shape[0]], dtype=torch.int64, device=comm)
+    ns = [torch.empty_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    m = max(int(x.item()) for x in ns)
+    pad = torch.zeros(max(m, 1), dtype=torch.int64, device=comm)
+    pad[:keys.shape[0]] = keys
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    if rank != 0:
+        return None
+    allk = np.concatenate([p[:int(c.item())].cpu().numpy() for p, c in zip(parts, ns)]).view(np.uint64)
+    return _sha_rdbg(allk)
 
 
 def main():
@@ -129,7 +174,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", action="store_true", help="CPU baseline on 12 of the 100 C3 genomes (~12 s)")
     ap.add_argument("--no-host-window", action="store_true",
-                    help="skip the host-resident window (profiler runs: its chunked K1 dispatches)")
+                    help="profiler runs: time only the HBM-resident build (no chunked host-window launches "
+                         "mixed into the per-kernel averages); `value` is then the device-resident rate")
+    ap.add_argument("--tmpdir", default=None, help="where the FASTA files go (default: a fresh dir in $TMPDIR)")
     args = ap.parse_args()
 
     import torch
@@ -153,132 +200,215 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=device)
 
+    from pangenome_amd import kmer
     from pangenome_amd._lib import Context
     from pangenome_amd.dist import exchange_and_reduce
 
-    batches, desc = workload(args.config, rank, world)
-    d_in, digests, host0 = [], [], None
-    for i, (fasta, dname) in enumerate(batches):
+    batches, pop_name, desc = workload(args.config, rank, world)
+    tmp = tempfile.mkdtemp(prefix="pgbench_r%d_" % rank, dir=args.tmpdir)
+    try:
+        run(args, torch, dist, kmer, Context, exchange_and_reduce, batches, pop_name, desc, world, rank,
+            dev_index, device, rehearse, tmp)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def run(args, torch, dist, kmer, Context, exchange_and_reduce, batches, pop_name, desc, world, rank, dev_index,
+        device, rehearse, tmp):
+    # ---- inputs: FASTA files, read once (page cache warm), memory-mapped
+    # read-only exactly as the CLI maps them; and HBM copies for the
+    # device-resident loop
+    paths, mms, d_in, digests = [], [], [], []
+    for i, (spec, dname) in enumerate(batches):
+        p = os.path.join(tmp, "batch%d.fa" % i)
+        fasta = make_fasta(spec)
+        with open(p, "wb") as f:
+            f.write(fasta)
         d_in.append(torch.frombuffer(bytearray(fasta), dtype=torch.uint8).to(device))
+        del fasta
+        with open(p, "rb") as f:                            # page-cache warm
+            while f.read(1 << 26):
+                pass
+        paths.append(p)
+        mms.append(kmer.seq2bytes(p))
         digests.append(_digest(dname))
-        if i == 0:
-            host0 = torch.empty(len(fasta), dtype=torch.uint8, pin_memory=True)
-            host0.numpy()[:] = np.frombuffer(fasta, np.uint8)
-    nbytes = [d.numel() for d in d_in]
-    del batches, fasta
+    pop = _digest(pop_name)
+    nbytes = [int(m.shape[0]) for m in mms]
     torch.cuda.synchronize()
 
-    def step(ctx, i):
-        d = d_in[i % len(d_in)]
-        if world == 1:                      # parse + seq2rdbg + dbg2rdbg in one call (pg_build_device)
-            st = ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d)
-            return st, st, st.n_dbg, st.n_rdbg, 0
-        ctx.set_fasta_device(d.data_ptr(), d.numel(), keepalive=d)
-        ctx.parse()
-        st_b = ctx.build_dbg(None, 0, True)
-        n_dbg, n_rdbg, _, sent = exchange_and_reduce(ctx, world, rank, device, bool(st_b.sentinel))
-        return st_b, ctx.stats(), n_dbg, n_rdbg, sent
+    def exchange(ctx, st):
+        return exchange_and_reduce(ctx, world, rank, device, bool(st.sentinel))
 
-    # cold first build: a fresh context (no working memory, no learned sizes, no cached tiles)
+    def step_host(ctx, i):
+        """mmap -> H2D (pinned staging ring) -> parse -> build -> rdBG count."""
+        st = ctx.build_host(mms[i % len(mms)], True)
+        if world == 1:
+            return st, st, st.n_dbg, st.n_rdbg, 0
+        n_dbg, n_rdbg, _, sent = exchange(ctx, st)
+        return st, ctx.stats(), n_dbg, n_rdbg, sent
+
+    def step_device(ctx, i):
+        """the same build from the HBM-resident copy (pg_build_device)."""
+        d = d_in[i % len(d_in)]
+        st = ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d)
+        if world == 1:
+            return st, st, st.n_dbg, st.n_rdbg, 0
+        n_dbg, n_rdbg, _, sent = exchange(ctx, st)
+        return st, ctx.stats(), n_dbg, n_rdbg, sent
+
+    def timed(ctx, step):
+        for i in range(args.warmup):
+            step(ctx, i)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        recs = []
+        for i in range(args.steps):
+            r = step(ctx, args.warmup + i)
+            recs.append(((args.warmup + i) % len(mms), r))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return time.perf_counter() - t0, recs
+
+    # cold first build: a fresh context (no working memory, no learned sizes,
+    # no staging threads) from the mmap
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     cold = Context(K, dev_index)
-    cst = step(cold, 0)
+    cst = step_host(cold, 0)
     cold_ms = 1e3 * (time.perf_counter() - t0)
     cold.close()
     del cold
 
     ctx = Context(K, dev_index)
-    for i in range(args.warmup):
-        step(ctx, i)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ins_ms, split_ms, range_ms, parse_ms, counts = [], [], [], [], []
-    last = None
-    for i in range(args.steps):
-        last = step(ctx, args.warmup + i)
-        ins_ms.append(last[0].ms_insert)
-        split_ms.append(last[1].ms_split)
-        range_ms.append(last[1].ms_range)
-        parse_ms.append(last[0].ms_parse)
-        counts.append(((args.warmup + i) % len(d_in), last[2], last[3]))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    host_window = not args.no_host_window
+    if host_window:
+        el_host, recs_host = timed(ctx, step_host)
+        # SHA-256 of the last host-window build (N=1: the whole dBG and rdBG;
+        # N>1: the union of the owners' rdBG)
+        last_host_batch = recs_host[-1][0]
+        if world == 1:
+            keys, masks = ctx.dbg()
+            host_sha = (_sha_dbg(keys, masks), _sha_rdbg(ctx.rdbg()))
+            del keys, masks
+        else:
+            host_sha = (None, _gather_rdbg_sha(ctx, world, rank, device, rehearse))
+    el_dev, recs_dev = timed(ctx, step_device)
+    if world > 1 and not host_window:
+        host_sha = (None, _gather_rdbg_sha(ctx, world, rank, device, rehearse))
+
+    el, recs = (el_host, recs_host) if host_window else (el_dev, recs_dev)
     if world > 1:
         comm = torch.device("cpu") if rehearse else device
-        t = torch.tensor([elapsed], dtype=torch.float64, device=comm)
+        t = torch.tensor([el, el_dev], dtype=torch.float64, device=comm)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tot = torch.tensor([last[0].n_bases, last[0].n_windows // 2, nbytes[0]], dtype=torch.int64, device=comm)
+        el, el_dev = t.tolist()
+        tot = torch.tensor([sum(r[0].n_bases for _, r in recs), sum(r[0].n_bases for _, r in recs_dev),
+                            sum(r[0].n_windows // 2 for _, r in recs[-1:]), nbytes[0]], dtype=torch.int64,
+                           device=comm)
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        bases_all, wfw_all, bytes_all = [int(x) for x in tot.tolist()]
-        total_bases = bases_all * args.steps
+        total_bases, total_bases_dev, wfw_all, bytes_all = [int(x) for x in tot.tolist()]
     else:
-        bases_all, wfw_all, bytes_all = last[0].n_bases, last[0].n_windows // 2, nbytes[-1]
-        # bases of every timed step (the batches differ by a few indels)
-        per_batch = {}
-        for j in range(len(d_in)):
-            ctx.set_fasta_device(d_in[j].data_ptr(), d_in[j].numel(), keepalive=d_in[j])
-            per_batch[j] = ctx.parse()[1]
-        total_bases = sum(per_batch[b] for b, _, _ in counts)
+        total_bases = sum(r[0].n_bases for _, r in recs)
+        total_bases_dev = sum(r[0].n_bases for _, r in recs_dev)
+        wfw_all, bytes_all = recs[-1][1][0].n_windows // 2, nbytes[recs[-1][0]]
 
-    # ---- parity after the timed region: every timed step's counts against the
-    # oracle digest of its batch, and the full dBG / rdBG digests of one build
+    # ---- parity, after the timed regions: every timed step's counts (both
+    # loops) and the cold build's against the oracle digest of its batch (N>1:
+    # of the global population), SHA-256 of one host-window build
     parity = None
     if world == 1 and all(digests):
-        ok = all((n_dbg, n_rdbg) == (digests[b]["n_dbg"], digests[b]["n_rdbg"]) for b, n_dbg, n_rdbg in counts)
-        jb = (args.warmup + args.steps - 1) % len(d_in)
-        d = d_in[jb]
-        ctx.set_fasta_device(d.data_ptr(), d.numel(), keepalive=d)
-        ctx.parse()
-        ctx.build(None, 0, True)
-        full = _full_check(ctx, digests[jb])
+        def cnt_ok(rr):
+            return all((r[2], r[3]) == (digests[b]["n_dbg"], digests[b]["n_rdbg"]) for b, r in rr)
+        ok_host = cnt_ok(recs_host) if host_window else True
+        ok_dev = cnt_ok(recs_dev)
         ok_cold = (cst[2], cst[3]) == (digests[0]["n_dbg"], digests[0]["n_rdbg"])
-        parity = {"ok": bool(ok and full and ok_cold),
-                  "checked": "n_dbg/n_rdbg of every timed step and of the cold build vs the oracle digests "
-                             "(tests/golden/scale); SHA-256 of one more build's sorted dBG and rdBG",
-                  "steps_ok": bool(ok), "sha256_ok": bool(full), "cold_ok": bool(ok_cold)}
+        if host_window:
+            dg = digests[last_host_batch]
+            sha_ok = host_sha == (dg["dbg_sha256"], dg["rdbg_sha256"])
+        else:
+            ctx.build_device(d_in[0].data_ptr(), d_in[0].numel(), True, keepalive=d_in[0])
+            keys, masks = ctx.dbg()
+            sha_ok = (_sha_dbg(keys, masks), _sha_rdbg(ctx.rdbg())) == (digests[0]["dbg_sha256"],
+                                                                        digests[0]["rdbg_sha256"])
+        parity = {"ok": bool(ok_host and ok_dev and ok_cold and sha_ok),
+                  "checked": "n_dbg/n_rdbg of every timed step (host window and HBM-resident loops) and of the "
+                             "cold build vs the oracle digests (tests/golden/scale); SHA-256 of the sorted dBG and "
+                             "rdBG of the last host-window build",
+                  "host_steps_ok": bool(ok_host), "device_steps_ok": bool(ok_dev), "cold_ok": bool(ok_cold),
+                  "sha256_ok": bool(sha_ok)}
+    elif world > 1 and pop is not None:
+        def cnt_ok(rr):
+            return all((r[2], r[3]) == (pop["n_dbg"], pop["n_rdbg"]) for _, r in rr)
+        ok = cnt_ok(recs_dev) and (cnt_ok(recs_host) if host_window else True) and \
+            (cst[2], cst[3]) == (pop["n_dbg"], pop["n_rdbg"])
+        sha_ok = host_sha[1] == pop["rdbg_sha256"] if rank == 0 else None
+        parity = {"ok": bool(ok and sha_ok) if rank == 0 else bool(ok),
+                  "checked": "global n_dbg/n_rdbg of every timed step and of the cold build vs the oracle digest "
+                             "of the whole population (tests/golden/scale/%s.json); SHA-256 of the all-gathered "
+                             "owner rdBG keys of the last %s build" % (pop_name, "host-window" if host_window
+                                                                     else "HBM-resident"),
+                  "counts_ok": bool(ok), "rdbg_sha256_ok": sha_ok}
 
-    # ---- host-resident input (BASELINE.md §3 window): pinned host FASTA ->
-    # H2D -> parse -> build -> rdBG count on the host; and the bare H2D rate
-    host_ms, h2d_gbs = None, None
-    if world == 1 and not args.no_host_window:
-        # pg_build_host: chunked H2D, K1 per chunk, stage A over each chunk's
-        # completed records under the copy, then stages B/C
-        ts, host_counts = [], []
-        for _ in range(3):
-            torch.cuda.synchronize()
+    # ---- the bounds of the window: a bare staged upload of the mmap (the
+    # pinned ring alone, pg_set_fasta) and a bare pinned H2D; and the same
+    # build from a pinned host buffer (pg_build_host with plain DMA)
+    extra = {}
+    if host_window:
+        jb = 0
+        m = mms[jb]
+        def best(fn, reps=3):
+            ts = []
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append(time.perf_counter() - t1)
+            return min(ts)
+        t_stage = best(lambda: ctx.set_fasta(m))
+        pin = torch.empty(nbytes[jb], dtype=torch.uint8, pin_memory=True)
+        pin.numpy()[:] = m
+        dst = torch.empty_like(d_in[jb])
+        t_pin = best(lambda: dst.copy_(pin, non_blocking=True))
+        t_pin_build = best(lambda: ctx.build_host_ptr(pin.data_ptr(), pin.numel(), True))
+        pin_counts = (ctx.stats().n_dbg, ctx.stats().n_rdbg)
+        del pin, dst
+        ms_step = 1e3 * el / args.steps
+        extra = {"h2d_staged_mmap_gbs": round(nbytes[jb] / t_stage / 1e9, 2),
+                 "h2d_pinned_gbs": round(nbytes[jb] / t_pin / 1e9, 2),
+                 "window_frac_of_staged_h2d": round(t_stage * 1e3 / ms_step, 4),
+                 "window_frac_of_pinned_h2d": round(t_pin * 1e3 / ms_step, 4),
+                 "pinned_host_ms": round(1e3 * t_pin_build, 3),
+                 "pinned_host_gbps": round(recs_host[0][1][0].n_bases / t_pin_build / 1e9, 3)}
+        if parity is not None and world == 1:
+            ok_pin = pin_counts == (digests[jb]["n_dbg"], digests[jb]["n_rdbg"])
+            parity["pinned_ok"] = bool(ok_pin)
+            parity["ok"] = bool(parity["ok"] and ok_pin)
+        if world == 1:
+            # the CLI's own dBG pass (kmer.seq2rdbg: a fresh context, build
+            # from the mmap), as `# build the dBG` times it
             t1 = time.perf_counter()
-            sth = ctx.build_host_ptr(host0.data_ptr(), host0.numel(), True)
-            ts.append(time.perf_counter() - t1)
-            host_counts.append((sth.n_dbg, sth.n_rdbg))
-        host_ms = 1e3 * min(ts)
-        if parity is not None and digests[0]:
-            ok_host = all(hc == (digests[0]["n_dbg"], digests[0]["n_rdbg"]) for hc in host_counts)
-            parity["host_window_ok"] = bool(ok_host)
-            parity["ok"] = bool(parity["ok"] and ok_host)
-        tmp = torch.empty_like(d_in[0])
-        hs = []
-        for _ in range(3):
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            tmp.copy_(host0, non_blocking=True)
-            torch.cuda.synchronize()
-            hs.append(time.perf_counter() - t1)
-        h2d_gbs = host0.numel() / min(hs) / 1e9
-        del tmp
+            g = kmer.seq2rdbg(paths[jb], K, 5, 2 ** 63, brkpt="", chunk=2 ** 33, rc=True, device=dev_index)
+            extra["cli_seq2rdbg_ms"] = round(1e3 * (time.perf_counter() - t1), 3)
+            if parity is not None:
+                ok_cli = (g.stats.n_dbg, g.stats.n_rdbg) == (digests[jb]["n_dbg"], digests[jb]["n_rdbg"])
+                parity["cli_ok"] = bool(ok_cli)
+                parity["ok"] = bool(parity["ok"] and ok_cli)
+            g.ctx.close()
+            del g
 
-    st_b, st_r, n_dbg, n_rdbg, sent = last
-    ms_step = 1e3 * elapsed / args.steps
-    value = total_bases / elapsed / 1e9
+    last = recs[-1][1]
+    st_b, st_c, n_dbg, n_rdbg, sent = last
+    ms_step = 1e3 * el / args.steps
+    value = total_bases / el / 1e9
 
-    # ---- roofline.  Per kernel, ALGORITHMIC bytes = what the kernel must read
-    # and write by its own definition, over its HIP-event time
-    # on the context's stream, averaged over the timed steps:
+    # ---- roofline, from the HBM-resident loop.  Per kernel, ALGORITHMIC
+    # bytes = what the kernel must read and write by its own definition
+    # (DESIGN.md §4), over its HIP-event time on the context's stream,
+    # averaged over the timed steps:
     #   K1 parse    F FASTA bytes read + B class codes written
     #   K3 stage A  B class codes read + 12 B per emitted record (8 B h + 4 B mask word)
     #   K3 stage B  24 B per record (read + write; one split pass at C3)
@@ -288,16 +418,18 @@ def main():
     # a separate rocprofv3 run).  SURVEY.md §8(d)'s path model, F + 20 W +
     # 10 D + 8 R, is `path.alg_bytes_s8d`: it charges every window 20 B that
     # the coverage pass never moves, so it is an "equivalent" figure.
-    st_b, st_c = last[0], last[1]             # stage A stats; stage B/C (N>1: the owner merge's)
-    nrec_a = st_b.n_records_a
+    dst_b = recs_dev[-1][1][0]
+    dst_c = recs_dev[-1][1][1]
+    nrec_a = dst_b.n_records_a
+    mean = lambda f: float(np.mean([f(r) for _, r in recs_dev]))   # noqa: E731
     spans = {
-        "k1_parse": (float(np.mean(parse_ms)), nbytes[-1] + st_b.n_bases,
+        "k1_parse": (mean(lambda r: r[0].ms_parse), nbytes[recs_dev[-1][0]] + dst_b.n_bases,
                      "F FASTA bytes read + B class codes written"),
-        "k3a_cover_emit": (float(np.mean(ins_ms)), st_b.n_bases + 12 * nrec_a,
+        "k3a_cover_emit": (mean(lambda r: r[0].ms_insert), dst_b.n_bases + 12 * nrec_a,
                            "B class codes read + 12 B per emitted record"),
-        "k3b_split": (float(np.mean(split_ms)), 24 * st_c.n_records_a, "24 B per record (read + write)"),
-        "k3c_range": (float(np.mean(range_ms)), 12 * st_c.n_records_a + 16 * st_c.table_capacity + 8 * st_c.n_rdbg,
-                      "12 B per record + 16 B per bucket + 8 B per rdBG key"),
+        "k3b_split": (mean(lambda r: r[1].ms_split), 24 * dst_c.n_records_a, "24 B per record (read + write)"),
+        "k3c_range": (mean(lambda r: r[1].ms_range), 12 * dst_c.n_records_a + 16 * dst_c.table_capacity +
+                      8 * dst_c.n_rdbg, "12 B per record + 16 B per bucket + 8 B per rdBG key"),
     }
     pmc = {}
     tp = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
@@ -329,28 +461,27 @@ def main():
         "data": "synthetic (splitmix64 pangenome generator, pangenome_amd/synth.py)",
         "config": {"workload": desc, "k": K, "strands": "-c 2 (dBG both strands)",
                    "bases_per_gpu": st_b.n_bases, "fasta_bytes_per_gpu": nbytes[0],
-                   "input": "FASTA resident in HBM when the timed region starts",
+                   "input": ("page-cache-warm mmap of the FASTA file (kmer.seq2bytes); H2D, parse, build and the "
+                             "rdBG count on the host inside the timed region (SURVEY 8(d) window)")
+                   if host_window else "FASTA resident in HBM when the timed region starts (--no-host-window)",
                    "parallelism": "record-sharded, owner all-to-all" if world > 1 else "single GPU"},
         "roofline": {"kernel": dom, "bound": "hbm", "achieved": round(kd["alg_bytes"] / (kd["ms"] * 1e-3) / 1e9, 2),
                      "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": kd["frac"],
                      "traffic": kd["pmc_bytes"], "traffic_frac": kd["pmc_frac"],
                      "traffic_source": "PMC FETCH_SIZE x2 + WRITE_SIZE per build, profiles/traffic_%s.json" % args.config,
                      "alg_bytes_per_launch": kd["alg_bytes"], "alg_model": kd["alg_model"],
-                     "avg_launch_ms": kd["ms"]},
+                     "avg_launch_ms": kd["ms"], "measured_in": "the HBM-resident loop (pg_build_device)"},
         "kernels": kernels,
-        "path": {"alg_bytes_s8d": path_bytes, "frac_of_hbm_s8d": round(path_bytes / (elapsed / args.steps) /
-                                                                         (world * HBM_PEAK), 5),
+        "path": {"device_resident_gbps": round(total_bases_dev / el_dev / 1e9, 4),
+                 "device_resident_ms": round(1e3 * el_dev / args.steps, 3),
+                 "alg_bytes_s8d": path_bytes, "frac_of_hbm_s8d_device_resident":
+                     round(path_bytes / (el_dev / args.steps) / (world * HBM_PEAK), 5),
                  "n_records_a": nrec_a, "n_dbg": n_dbg, "n_rdbg": n_rdbg,
-                 "table_slots": st_b.table_capacity, "exchange_bytes_sent_rank0": sent,
+                 "table_slots": dst_b.table_capacity, "exchange_bytes_sent_rank0": sent,
                  "cold_first_build_ms": round(cold_ms, 3),
                  "cold_first_build_gbps": round(cst[0].n_bases / cold_ms / 1e6, 3)},
     }
-    if host_ms is not None:
-        out["path"]["host_to_rdbg_ms"] = round(host_ms, 3)
-        out["path"]["host_to_rdbg_gbps"] = round(per_batch[0] / host_ms / 1e6, 3)
-        out["path"]["h2d_pinned_gbs"] = round(h2d_gbs, 2)
-        # the PCIe bound of that window: the FASTA's bare pinned H2D time
-        out["path"]["host_to_rdbg_frac_of_pcie_bound"] = round(nbytes[0] / (h2d_gbs * 1e9) / (host_ms * 1e-3), 4)
+    out["path"].update(extra)
     if parity is not None:
         out["parity"] = parity
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

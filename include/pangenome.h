@@ -76,8 +76,10 @@ int pg_parse(pg_ctx* ctx, uint64_t* n_records, uint64_t* n_bases);
 /* pg_set_fasta + pg_parse for host bytes in one call (seq2bytes + seqio_jit_,
  * :117-172): the copy to HBM goes in chunks (PG_TUNE_H2D_CHUNK, 64 MiB) on a
  * side stream and K1 runs on each chunk once it has landed, so the parse of
- * all but the last chunk hides under the PCIe transfer (pinned host memory
- * makes the copies plain DMA).  The bytes are read until the call returns. */
+ * all but the last chunk hides under the PCIe transfer.  Pinned host memory
+ * is DMA'd directly; pageable memory (the np.memmap the reference reads) is
+ * copied by a few host threads into a ring of pinned slots that the DMA
+ * drains (PG_TUNE_HOST_THREADS).  The bytes are read until the call returns. */
 int pg_parse_host(pg_ctx* ctx, const uint8_t* host_bytes, uint64_t nbytes, uint64_t* n_records,
                   uint64_t* n_bases);
 /* pg_parse_host + pg_build of every record (seq2rdbg + dbg2rdbg,
@@ -199,6 +201,10 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 /* PG_TUNE_H2D_CHUNK: bytes per pg_parse_host chunk, rounded down to whole
  * 16 KiB K1 spans (0 = 64 MiB): small values exercise the pipeline. */
 #define PG_TUNE_H2D_CHUNK 4
+/* PG_TUNE_HOST_THREADS: host threads that copy a pageable input (an mmap)
+ * into the pinned staging ring of pg_parse_host / pg_build_host / pg_set_fasta
+ * (1..64, 0 = half the CPUs the process may run on, at most 8). */
+#define PG_TUNE_HOST_THREADS 5
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Timings and counters of the last build (see pg_stats). */

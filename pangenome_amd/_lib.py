@@ -19,6 +19,7 @@ PG_TUNE_K3_CHUNKS = 1
 PG_TUNE_BUCKET_SHIFT = 2
 PG_TUNE_REGION_CAP = 3
 PG_TUNE_H2D_CHUNK = 4
+PG_TUNE_HOST_THREADS = 5
 
 
 class PgStats(C.Structure):

@@ -86,6 +86,8 @@ void pg_destroy(pg_ctx* x) {
                         &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload,
                         &c.dump_cnt};
   for (auto* b : bufs) b->release();
+  pg::pool_destroy(c);
+  c.stage_pin.release();
   c.rec_pack.release();
   c.h_pin.release();
   c.h_out.release();
@@ -111,7 +113,15 @@ int pg_set_fasta(pg_ctx* x, const uint8_t* host, uint64_t n) {
     pg::Ctx& c = x->c;
     PG_HIP(hipSetDevice(c.device));
     c.fasta_own.reserve(n + 64);
-    if (n) PG_HIP(hipMemcpyAsync(c.fasta_own.p, host, n, hipMemcpyHostToDevice, c.stream));
+    {                                          // pageable input through the pinned staging ring
+      pg::Upload up(c, c.fasta_own.as<uint8_t>(), host, n, c.h2d_chunk);
+      for (uint64_t i = 0; i < up.chunks(); ++i) {
+        up.wait_queued(i);
+        PG_HIP(hipStreamWaitEvent(c.stream, c.cev[i & 15], 0));
+        up.consumed(i);
+      }
+      up.finish();
+    }
     c.sync();
     c.d_fasta = c.fasta_own.as<uint8_t>();
     c.n_bytes = n;
@@ -271,6 +281,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
       case PG_TUNE_H2D_CHUNK:
         if (value < 0) throw pg::Error(PG_EINVAL, "pg_tune: H2D chunk must be >= 0");
         x->c.h2d_chunk = value ? (uint64_t)value : (64ull << 20);
+        break;
+      case PG_TUNE_HOST_THREADS:
+        if (value < 0 || value > 64) throw pg::Error(PG_EINVAL, "pg_tune: host threads must be in [0, 64]");
+        x->c.host_threads = (int)value;
         break;
       default:
         throw pg::Error(PG_EINVAL, "pg_tune: unknown parameter " + std::to_string(what));

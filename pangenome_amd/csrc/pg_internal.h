@@ -95,6 +95,8 @@ struct Timer {
   }
 };
 
+struct HostPool;                  // pg_stage.hip: the pinned staging ring's threads
+
 struct Ctx {
   int device = 0;
   int k = 27;
@@ -106,6 +108,9 @@ struct Ctx {
   int n_cu = 256;                 // compute units (persistent-kernel grids)
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
+  int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
+  HostPool* pool = nullptr;       // staging ring threads (created on the first pageable upload)
+  PinBuf stage_pin;               // staging ring slots
   int bb_shift = 0;               // pg_tune: table bits below the sized ones (tests of the overflow paths)
   uint64_t region_cap_force = 0;  // pg_tune: first stage A region size (tests of the re-run path)
 
@@ -218,6 +223,35 @@ struct Ctx {
     PG_HIP(hipStreamSynchronize(stream));
   }
 };
+
+// pg_stage.hip
+// One chunked upload of n host bytes to dst on c.stream3: chunk i's copy is
+// marked by c.cev[i & 15] on stream3 once wait_queued(i) returns.  A
+// pageable source goes through the pinned staging ring (a stager thread and
+// its memcpy pool); a pinned one is DMA'd directly, up to 8 chunks ahead.
+// The source is read until finish() (or the destructor) returns.
+class Upload {
+ public:
+  Upload(Ctx& c, uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t chunk);
+  ~Upload();
+  Upload(const Upload&) = delete;
+  Upload& operator=(const Upload&) = delete;
+  uint64_t chunks() const { return nch_; }
+  void wait_queued(uint64_t i);   // chunk i's copy is queued and c.cev[i & 15] recorded
+  void consumed(uint64_t i);      // the caller has queued its wait on c.cev[i & 15]
+  void finish();                  // every chunk queued; rethrows a stager error
+  bool staged = false;            // through the pinned ring
+
+ private:
+  Ctx& c_;
+  uint8_t* dst_;
+  const uint8_t* src_;
+  uint64_t n_, C_, nch_;
+  HostPool* P_ = nullptr;
+  uint64_t issued_ = 0;
+  bool done_ = false;
+};
+void pool_destroy(Ctx& c);
 
 // pg_parse.hip
 // h_src: host bytes, uploaded in chunks pipelined with K1.  on_chunk (host

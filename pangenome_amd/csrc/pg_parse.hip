@@ -527,20 +527,16 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   bool streaming = on_chunk != nullptr;
   if (h_src) {
     const uint64_t C = std::max<uint64_t>(WSPAN, c.h2d_chunk / WSPAN * WSPAN);
-    const uint64_t nch = (n + C - 1) / C;
-    // copies run up to 8 chunks ahead of K1 on the copy stream (16 events:
-    // an event is recorded again only after K1's wait on it was queued)
-    uint64_t queued = 0;
-    auto queue_copy = [&](uint64_t i) {
-      const uint64_t off = i * C, len = std::min(C, n - off);
-      PG_HIP(hipMemcpyAsync(c.fasta_own.as<uint8_t>() + off, h_src + off, len, hipMemcpyHostToDevice, c.stream3));
-      PG_HIP(hipEventRecord(c.cev[i & 15], c.stream3));
-    };
+    // pinned source: DMA up to 8 chunks ahead; pageable (an mmap): through
+    // the pinned staging ring (pg_stage.hip)
+    Upload up(c, c.fasta_own.as<uint8_t>(), h_src, n, C);
+    const uint64_t nch = up.chunks();
     for (uint64_t i = 0; i < nch; ++i) {
-      while (queued < nch && queued < i + 8) queue_copy(queued++);
+      up.wait_queued(i);
       const uint64_t off = i * C, len = std::min(C, n - off);
       const uint64_t s0 = off / WSPAN, s1 = std::min(nspan, (off + len + WSPAN - 1) / WSPAN);
       PG_HIP(hipStreamWaitEvent(st, c.cev[i & 15], 0));
+      up.consumed(i);
       hipLaunchKernelGGL(k_span_sum, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta,
                          n, s0, s1, fns);
       PG_HIP(hipGetLastError());
@@ -565,6 +561,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
       c.n_records = Rc;
       (*on_chunk)(Rc);
     }
+    up.finish();
   } else {
     hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
     PG_HIP(hipGetLastError());

