@@ -167,6 +167,26 @@ int pg_edges(pg_ctx* ctx, const uint8_t* rec_flags, int rc1, uint64_t* n_edges);
  * of the reference's dump/reload checkpoints (kmer_numba.py:1881-1887). */
 int pg_edges_export(pg_ctx* ctx, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap);
 
+/* The `.xyz` text of the last pg_edges, "%d_%d\t%d_%d\t%d\n" per edge in
+ * first-occurrence order (seq2graph :1893-1904), formatted on the device.
+ * out == NULL: only *n_bytes (the size) is set; otherwise cap >= that size. */
+int pg_edges_format(pg_ctx* ctx, char* out, uint64_t cap, uint64_t* n_bytes);
+
+/* seq2graph's label dictionary (kmer_numba.py:1918-1944) built on the device:
+ * the `.mcl` entries (key, value) -> line index as the host's dict holds them
+ * (a later line wins), then every `.xyz` node - n0_v0, then n1_v1 of each
+ * edge in file order - the .mcl did not label, numbered next_label,
+ * next_label + 1, ... in order of first appearance (next_label = the number
+ * of .mcl lines).  tuples: the edges as the .xyz lists them (n_edges x 4
+ * uint64), or NULL for the last pg_edges in first-occurrence order.  The
+ * table replaces any pg_set_labels table for the following pg_rows. */
+int pg_labels_from_edges(pg_ctx* ctx, const uint64_t* tuples, uint64_t n_edges, const int64_t* mcl_key,
+                         const int64_t* mcl_value, const int64_t* mcl_label, uint64_t n_mcl, int64_t next_label,
+                         uint64_t* n_labels);
+/* The label table in insertion order: the .mcl entries, then the new ones
+ * by label (cap >= n_labels). */
+int pg_labels_export(pg_ctx* ctx, int64_t* key, int64_t* value, int64_t* label, uint64_t cap);
+
 /* ---- region rows: seqs2path_jit_ (kmer_numba.py:1830-1849) -> seq2path_jit_
  *      (:1523-1573).  Labels are the host-built label_dct (:1918-1944):
  *      (key, value) -> label. */
@@ -175,6 +195,12 @@ int pg_rows(pg_ctx* ctx, const uint8_t* rec_flags, int rc1, uint64_t* n_rows);
 /* rows: 5 x int64 per row (record index, start, end, strand +1/-1, label),
  * in print order. */
 int pg_rows_export(pg_ctx* ctx, int64_t* rows5, uint64_t cap);
+/* The text of the last pg_rows, "qid\tstart\tend\t+|-\tlabel\n" per row in
+ * print order (:1946-1949), formatted on the device; qid of record r is
+ * names[name_off[r] .. name_off[r+1]) (n_names >= records, n_names + 1
+ * offsets).  out == NULL: only *n_bytes is set. */
+int pg_rows_format(pg_ctx* ctx, const char* names, const int64_t* name_off, uint64_t n_names, char* out, uint64_t cap,
+                   uint64_t* n_bytes);
 
 /* ---- text output (host only; no context).  The reference formats these in
  *      Python loops (kmer_numba.py:1893-1904, :1946-1949).
@@ -205,6 +231,11 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * into the pinned staging ring of pg_parse_host / pg_build_host / pg_set_fasta
  * (1..64, 0 = half the CPUs the process may run on, at most 8). */
 #define PG_TUNE_HOST_THREADS 5
+/* PG_TUNE_STAGE_PIECE / PG_TUNE_STAGE_SLOTS: bytes per slot of that ring (one
+ * DMA each; 0 = 32 MiB) and its slot count (2..8, 0 = 4); the first pieces
+ * of an upload are smaller (2, 4, 8 ... MiB). */
+#define PG_TUNE_STAGE_PIECE 6
+#define PG_TUNE_STAGE_SLOTS 7
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Timings and counters of the last build (see pg_stats). */

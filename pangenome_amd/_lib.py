@@ -20,6 +20,8 @@ PG_TUNE_BUCKET_SHIFT = 2
 PG_TUNE_REGION_CAP = 3
 PG_TUNE_H2D_CHUNK = 4
 PG_TUNE_HOST_THREADS = 5
+PG_TUNE_STAGE_PIECE = 6
+PG_TUNE_STAGE_SLOTS = 7
 
 
 class PgStats(C.Structure):
@@ -64,6 +66,10 @@ SIGNATURES = {
     "pg_set_labels": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_rows": (C.c_int, [_P, _P, C.c_int, _U64P]),
     "pg_rows_export": (C.c_int, [_P, _P, C.c_uint64]),
+    "pg_edges_format": (C.c_int, [_P, _P, C.c_uint64, _U64P]),
+    "pg_labels_from_edges": (C.c_int, [_P, _P, C.c_uint64, _P, _P, _P, C.c_uint64, C.c_int64, _U64P]),
+    "pg_labels_export": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
+    "pg_rows_format": (C.c_int, [_P, _P, _P, C.c_uint64, _P, C.c_uint64, _U64P]),
     "pg_get_stats": (C.c_int, [_P, _SP]),
     "pg_tune": (C.c_int, [_P, C.c_int, C.c_int64]),
     "pg_dbg_dump": (C.c_int, [_P, _U64P, _P, _P, _P, _U64P]),
@@ -285,6 +291,24 @@ class Context:
                                     int(bool(sentinel))), "pg_dbg_merge")
 
     # -------------------------------------------------------------- walks
+    def edges_count(self, rec_flags=None, rc1: bool = False) -> int:
+        """pg_edges only: the edges stay on the device (edges_text /
+        labels_from_edges / edges_export)."""
+        n = C.c_uint64()
+        f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
+        check(self.lib.pg_edges(self.h, ptr(f), int(bool(rc1)), C.byref(n)), "pg_edges")
+        self.n_edges = n.value
+        return n.value
+
+    def edges_export(self):
+        m = getattr(self, "n_edges", 0)
+        t = np.empty((m, 4), np.uint64)
+        cnt = np.empty(m, np.int64)
+        walk = np.empty(m, np.int64)
+        if m:
+            check(self.lib.pg_edges_export(self.h, ptr(t), ptr(cnt), ptr(walk), m), "pg_edges_export")
+        return t, cnt, walk
+
     def edges(self, rec_flags=None, rc1: bool = False):
         n = C.c_uint64()
         f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
@@ -297,11 +321,66 @@ class Context:
             check(self.lib.pg_edges_export(self.h, ptr(t), ptr(cnt), ptr(walk), m), "pg_edges_export")
         return t, cnt, walk
 
+    def edges_text(self) -> bytes:
+        """The `.xyz` text of the last edges() pass (first-occurrence order),
+        formatted on the device (pg_edges_format)."""
+        n = C.c_uint64()
+        check(self.lib.pg_edges_format(self.h, None, 0, C.byref(n)), "pg_edges_format")
+        buf = np.empty(max(n.value, 1), np.uint8)
+        check(self.lib.pg_edges_format(self.h, ptr(buf), buf.shape[0], C.byref(n)), "pg_edges_format")
+        return buf[:n.value].tobytes()
+
+    def labels_from_edges(self, tuples=None, mcl_keys=None, mcl_vals=None, mcl_ids=None, next_label: int = 0):
+        """seq2graph's label table on the device (pg_labels_from_edges): the
+        .mcl entries, then the .xyz nodes in first-appearance order.  tuples
+        None: the last edges() pass."""
+        n = C.c_uint64()
+        t = None if tuples is None else np.ascontiguousarray(tuples, dtype=np.uint64).reshape(-1, 4)
+        mk = np.ascontiguousarray(mcl_keys if mcl_keys is not None else np.zeros(0), dtype=np.int64)
+        mv = np.ascontiguousarray(mcl_vals if mcl_vals is not None else np.zeros(0), dtype=np.int64)
+        mi = np.ascontiguousarray(mcl_ids if mcl_ids is not None else np.zeros(0), dtype=np.int64)
+        check(self.lib.pg_labels_from_edges(self.h, ptr(t), 0 if t is None else t.shape[0], ptr(mk), ptr(mv),
+                                            ptr(mi), mk.shape[0], int(next_label), C.byref(n)),
+              "pg_labels_from_edges")
+        self.n_labels = n.value
+        return n.value
+
+    def labels(self):
+        """(keys, vals, ids) of the device label table, in insertion order."""
+        n = getattr(self, "n_labels", 0)
+        out = [np.empty(n, np.int64) for _ in range(3)]
+        if n:
+            check(self.lib.pg_labels_export(self.h, *[ptr(a) for a in out], n), "pg_labels_export")
+        return tuple(out)
+
     def set_labels(self, keys, vals, ids):
         keys = np.ascontiguousarray(keys, np.int64)
         vals = np.ascontiguousarray(vals, np.int64)
         ids = np.ascontiguousarray(ids, np.int64)
         check(self.lib.pg_set_labels(self.h, ptr(keys), ptr(vals), ptr(ids), keys.shape[0]), "pg_set_labels")
+        self.n_labels = keys.shape[0]
+
+    def rows_count(self, rec_flags=None, rc1: bool = False) -> int:
+        """pg_rows only: the rows stay on the device (rows_text / rows())."""
+        n = C.c_uint64()
+        f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
+        check(self.lib.pg_rows(self.h, ptr(f), int(bool(rc1)), C.byref(n)), "pg_rows")
+        return n.value
+
+    def rows_text(self, names: list) -> bytes:
+        """The region rows' text of the last pg_rows, formatted on the device
+        (pg_rows_format); names[r] = record r's qid."""
+        blob = b"".join(names)
+        off = np.zeros(len(names) + 1, np.int64)
+        if names:
+            off[1:] = np.cumsum([len(x) for x in names])
+        nb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
+        n = C.c_uint64()
+        check(self.lib.pg_rows_format(self.h, ptr(nb), ptr(off), len(names), None, 0, C.byref(n)), "pg_rows_format")
+        buf = np.empty(max(n.value, 1), np.uint8)
+        check(self.lib.pg_rows_format(self.h, ptr(nb), ptr(off), len(names), ptr(buf), buf.shape[0], C.byref(n)),
+              "pg_rows_format")
+        return buf[:n.value].tobytes()
 
     def rows(self, rec_flags=None, rc1: bool = False):
         n = C.c_uint64()

@@ -83,7 +83,8 @@ void pg_destroy(pg_ctx* x) {
                         &c.recA_key, &c.recA_mw, &c.ctrA, &c.recS_key[0], &c.recS_key[1], &c.recS_mw[0],
                         &c.recS_mw[1], &c.ctrS, &c.rseg, &c.k5_ctr, &c.tile_sched, &c.tile_desc, &c.k3_queue,
                         &c.k3_hint, &c.part_cnt, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
-                        &c.edge_out, &c.lab_tab, &c.walk_hits_off, &c.rows_buf, &c.rows_cnt, &c.preload,
+                        &c.edge_out, &c.edge_exp, &c.lab_tab, &c.lab_list, &c.rows_buf, &c.text_len, &c.text_off,
+                        &c.text_buf, &c.text_names, &c.preload,
                         &c.dump_cnt};
   for (auto* b : bufs) b->release();
   pg::pool_destroy(c);
@@ -286,6 +287,14 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || value > 64) throw pg::Error(PG_EINVAL, "pg_tune: host threads must be in [0, 64]");
         x->c.host_threads = (int)value;
         break;
+      case PG_TUNE_STAGE_PIECE:
+        if (value < 0 || (value && value < 4096)) throw pg::Error(PG_EINVAL, "pg_tune: staging piece must be 0 or >= 4096");
+        x->c.stage_piece = value ? (uint64_t)value : (32ull << 20);
+        break;
+      case PG_TUNE_STAGE_SLOTS:
+        if (value < 0 || value == 1 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: staging slots must be 0 or 2..8");
+        x->c.stage_slots = value ? (uint64_t)value : 4;
+        break;
       default:
         throw pg::Error(PG_EINVAL, "pg_tune: unknown parameter " + std::to_string(what));
     }
@@ -409,7 +418,46 @@ int pg_rows_export(pg_ctx* x, int64_t* rows5, uint64_t cap) {
   return guard([&] {
     if (!x || !rows5) throw pg::Error(PG_EINVAL, "pg_rows_export: bad arguments");
     if (cap < x->c.n_rows) throw pg::Error(PG_ERANGE, "pg_rows_export: buffer too small");
-    if (x->c.n_rows) std::memcpy(rows5, x->c.h_rows.data(), 8 * 5 * x->c.n_rows);
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::export_rows(x->c, rows5, cap);
+  });
+}
+
+int pg_edges_format(pg_ctx* x, char* out, uint64_t cap, uint64_t* n_bytes) {
+  return guard([&] {
+    if (!x || !n_bytes) throw pg::Error(PG_EINVAL, "pg_edges_format: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    *n_bytes = pg::format_edges(x->c, out, cap);
+  });
+}
+
+int pg_labels_from_edges(pg_ctx* x, const uint64_t* tuples, uint64_t n_edges, const int64_t* mcl_key,
+                         const int64_t* mcl_value, const int64_t* mcl_label, uint64_t n_mcl, int64_t next_label,
+                         uint64_t* n_labels) {
+  return guard([&] {
+    if (!x || (n_mcl && (!mcl_key || !mcl_value || !mcl_label)) || (tuples == nullptr && n_edges))
+      throw pg::Error(PG_EINVAL, "pg_labels_from_edges: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    const uint64_t n = pg::labels_from_edges(x->c, tuples, n_edges, mcl_key, mcl_value, mcl_label, n_mcl, next_label);
+    if (n_labels) *n_labels = n;
+  });
+}
+
+int pg_labels_export(pg_ctx* x, int64_t* key, int64_t* value, int64_t* label, uint64_t cap) {
+  return guard([&] {
+    if (!x || !key || !value || !label) throw pg::Error(PG_EINVAL, "pg_labels_export: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::export_labels(x->c, key, value, label, cap);
+  });
+}
+
+int pg_rows_format(pg_ctx* x, const char* names, const int64_t* name_off, uint64_t n_names, char* out, uint64_t cap,
+                   uint64_t* n_bytes) {
+  return guard([&] {
+    if (!x || !n_bytes || !name_off) throw pg::Error(PG_EINVAL, "pg_rows_format: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    if (n_names < x->c.n_records) throw pg::Error(PG_EINVAL, "pg_rows_format: fewer names than records");
+    *n_bytes = pg::format_rows_text(x->c, names, name_off, n_names, out, cap);
   });
 }
 

@@ -109,6 +109,8 @@ struct Ctx {
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
   int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
+  uint64_t stage_piece = 32ull << 20;  // pg_tune: bytes per staging-ring slot (one DMA)
+  uint64_t stage_slots = 4;       // pg_tune: staging-ring slots (2..8)
   HostPool* pool = nullptr;       // staging ring threads (created on the first pageable upload)
   PinBuf stage_pin;               // staging ring slots
   int bb_shift = 0;               // pg_tune: table bits below the sized ones (tests of the overflow paths)
@@ -186,13 +188,19 @@ struct Ctx {
   DevBuf tile_cnt, tile_off;      // per tile x strand counts / offsets
   DevBuf occ;                     // member / hit occurrences, walk ordered
   DevBuf edge_tab, pair_tab;      // edge table and (edge, walk) dedup set
-  DevBuf edge_out;
+  DevBuf edge_out;                // compacted edge slots
+  DevBuf edge_exp;                // edges in first-occurrence order: [n][4] tuple, [n] count, [n] first walk
   uint64_t edge_cap = 0, pair_cap = 0, n_edges = 0;
-  DevBuf lab_tab;                 // label table
+  DevBuf lab_tab;                 // label table (hash of (key, value) -> label)
   uint64_t lab_cap = 0;
-  DevBuf walk_hits_off, rows_buf, rows_cnt;
+  DevBuf lab_list;                // the labels in order: [n] key, [n] value, [n] label
+  uint64_t n_labels = 0;
+  DevBuf rows_buf;                // rows of the last row pass: [n][5] int64
   uint64_t n_rows = 0;
-  std::vector<int64_t> h_rows;    // rec, start, end, strand, label
+  // text of the last edge or row pass (pg_edges_format / pg_rows_format)
+  DevBuf text_len, text_off, text_buf, text_names;
+  uint64_t text_total = 0;
+  bool text_xyz = false, text_rows = false;
 
   // ---- npz persistence (pg_persist.hip)
   DevBuf preload;                 // staged PreEnt pairs, OR-merged by every build
@@ -282,6 +290,13 @@ uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1);
 void export_edges(Ctx& c, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap);
 void set_labels(Ctx& c, const int64_t* key, const int64_t* val, const int64_t* id, uint64_t n);
 uint64_t walk_rows(Ctx& c, const uint8_t* h_rec_flag, int rc1);
+void export_rows(Ctx& c, int64_t* rows5, uint64_t cap);
+uint64_t format_edges(Ctx& c, char* out, uint64_t cap);
+uint64_t labels_from_edges(Ctx& c, const uint64_t* h_tuples, uint64_t n_edges, const int64_t* mk, const int64_t* mv,
+                           const int64_t* mi, uint64_t n_mcl, int64_t next_id);
+void export_labels(Ctx& c, int64_t* key, int64_t* val, int64_t* id, uint64_t cap);
+uint64_t format_rows_text(Ctx& c, const char* names, const int64_t* name_off, uint64_t n_names, char* out,
+                          uint64_t cap);
 
 // helpers
 inline uint64_t next_pow2(uint64_t x) {

@@ -22,8 +22,7 @@
 
 namespace pg {
 
-constexpr uint64_t NSLOT = 6;            // pinned slots of the ring
-constexpr uint64_t SLOT_BYTES = 8ull << 20;
+constexpr uint64_t NSLOT = 8;            // pinned slots of the ring (at most)
 
 struct HostPool {
   int device = 0;
@@ -123,8 +122,10 @@ struct HostPool {
           // soon as it is in pinned memory, so the ring fills in one piece's
           // copy time and the link never waits for a whole chunk
           const uint64_t off = i * C, len = std::min(C, n - off);
-          for (uint64_t po = 0; po < len; po += S, ++piece) {
-            const uint64_t pl = std::min(S, len - po);
+          for (uint64_t po = 0, pl; po < len; po += pl, ++piece) {
+            // the first pieces small (2, 4, 8 ... MiB up to a slot): the link
+            // starts after one small copy instead of a whole slot's
+            pl = std::min<uint64_t>(std::min<uint64_t>(S, len - po), piece < 8 ? (uint64_t)(2ull << 20) << piece : S);
             const uint64_t slot = piece % nslots;
             if (piece >= nslots) PG_HIP(hipEventSynchronize(slot_ev[slot]));   // the slot's last DMA
             par_copy(slots + slot * S, src + off + po, pl);
@@ -201,8 +202,9 @@ Upload::Upload(Ctx& c, uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t ch
     : c_(c), dst_(dst), src_(src), n_(n), C_(chunk), nch_(n ? (n + chunk - 1) / chunk : 0) {
   staged = nch_ && !(is_pinned(src) && is_pinned(src + n - 1));
   if (!staged) return;
-  const uint64_t S = std::min(SLOT_BYTES, n);
-  const uint64_t nslots = std::min<uint64_t>(NSLOT, (n + S - 1) / S);
+  const uint64_t S = std::min(c.stage_piece, n);
+  const uint64_t nslots = std::min<uint64_t>(std::min<uint64_t>(NSLOT, c.stage_slots),
+                                             (n + S - 1) / S);
   c.stage_pin.reserve(nslots * S);
   P_ = pool_of(c);
   std::lock_guard<std::mutex> g(P_->mu);

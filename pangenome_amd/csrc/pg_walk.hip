@@ -240,12 +240,16 @@ __device__ __forceinline__ unsigned atomic_read32(unsigned* p) { return atomicCA
 // published when it ends).  Spinning instead deadlocks: the compiler lays the
 // winner's publish out after the loop, behind its waiting wave-mates.
 constexpr uint64_t EDGE_RETRY = ~0ull - 1;
+constexpr uint64_t EDGE_PROBES = 4096;
 __device__ uint64_t edge_find_or_insert(EdgeSlot* __restrict__ tab, uint64_t capmask, uint64_t n0, uint32_t v0,
                                         uint64_t n1, uint32_t v1, unsigned* err) {
   const unsigned long long a = n0 + 1ull, bkey = n1 + 1ull;
   const unsigned vv = v0 | (v1 << 16) | 0x80000000u;
   uint64_t slot = fmix64(n0 * 0x9e3779b97f4a7c15ull ^ fmix64(n1 ^ ((uint64_t)vv << 40))) & capmask;
-  for (uint64_t probe = 0; probe <= capmask; ++probe) {
+  // (the table is sized from the rdBG; a long probe sequence means it is too
+  // small for this input: the error bit makes the host re-run with more slots)
+  const uint64_t limit = capmask < EDGE_PROBES ? capmask : EDGE_PROBES;
+  for (uint64_t probe = 0; probe <= limit; ++probe) {
     EdgeSlot* s = tab + slot;
     unsigned long long w0 = s->n0p1;          // a stale plain read can only show 0
     if (w0 == 0ull) {
@@ -312,7 +316,8 @@ __global__ void k_edges(const Occ* __restrict__ occ, uint64_t m, const unsigned 
 struct EdgeOut { unsigned long long n0, n1; unsigned v0, v1; unsigned long long count, first, walk; };
 
 __global__ void k_edges_compact(const EdgeSlot* __restrict__ tab, uint64_t cap, const Occ* __restrict__ occ,
-                                EdgeOut* __restrict__ out, unsigned long long* __restrict__ counter) {
+                                EdgeOut* __restrict__ out, unsigned long long* __restrict__ first_key,
+                                unsigned* __restrict__ iota, unsigned long long* __restrict__ counter) {
   const int lane = threadIdx.x & 63;
   const unsigned long long lt = (1ull << lane) - 1ull;
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < cap;
@@ -325,10 +330,26 @@ __global__ void k_edges_compact(const EdgeSlot* __restrict__ tab, uint64_t cap, 
     unsigned long long base = 0;
     if (lane == leader) base = atomicAdd(counter, (unsigned long long)__builtin_popcountll(bal));
     base = __shfl(base, leader, 64);
-    if (used)
-      out[base + __builtin_popcountll(bal & lt)] =
-          EdgeOut{s.n0p1 - 1ull, s.n1p1 - 1ull, s.vv & 0xFFFFu, (s.vv >> 16) & 0x7FFFu, s.count, ~s.first,
-                  occ[~s.first].walk};
+    if (used) {
+      const unsigned long long o = base + __builtin_popcountll(bal & lt);
+      out[o] = EdgeOut{s.n0p1 - 1ull, s.n1p1 - 1ull, s.vv & 0xFFFFu, (s.vv >> 16) & 0x7FFFu, s.count, ~s.first,
+                       occ[~s.first].walk};
+      first_key[o] = ~s.first;
+      iota[o] = (unsigned)o;
+    }
+  }
+}
+
+// The edges in first-occurrence order (typed-Dict insertion order,
+// :1479-1484) as the export layout: 4 x uint64 tuple, int64 count, int64 walk.
+__global__ void k_edges_order(const EdgeOut* __restrict__ e, const unsigned* __restrict__ order, uint64_t n,
+                              unsigned long long* __restrict__ tup, long long* __restrict__ cnt,
+                              long long* __restrict__ walk) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    const EdgeOut x = e[order[j]];
+    tup[4 * j] = x.n0; tup[4 * j + 1] = x.v0; tup[4 * j + 2] = x.n1; tup[4 * j + 3] = x.v1;
+    cnt[j] = (long long)x.count;
+    walk[j] = (long long)x.walk;
   }
 }
 
@@ -348,41 +369,201 @@ __global__ void k_lab_insert(const long long* __restrict__ key, const long long*
   }
 }
 
-// seq2path_jit_'s greedy merge (:1546-1560) for one walk per thread.  State is
-// (starts[-1], labels[-1]); rows (starts[i-1], starts[i], labels[i]) leave as
-// int32 (:1533) and reverse-strand rows are mirrored to (n-end, n-start) (:1843).
-__global__ void k_regions(const Hit* __restrict__ hits, const unsigned long long* __restrict__ seg_off,
-                          const unsigned long long* __restrict__ seg_cnt, const long long* __restrict__ seg_len,
-                          uint64_t nseg, int k, long long* __restrict__ rows, unsigned long long* __restrict__ nrows) {
-  for (uint64_t w = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; w < nseg; w += (uint64_t)gridDim.x * blockDim.x) {
-    const unsigned long long off = seg_off[w], cnt = seg_cnt[w];
-    const long long lseq = seg_len[w >> 1];
-    const bool rc = w & 1;
-    long long last = 0, last_label = -1;
-    unsigned long long nr = 0;
-    long long* out = rows + 3 * off;
-    for (unsigned long long j = 0; j < cnt; ++j) {
-      const Hit h = hits[off + j];
-      if (last < (long long)h.idx) {
-        const long long pos = (long long)h.idx + k;
-        if (last_label != h.label) {
-          out[3 * nr] = last; out[3 * nr + 1] = pos; out[3 * nr + 2] = h.label;
-          ++nr;
-          last_label = h.label;
-        } else if (nr > 0) {
-          out[3 * (nr - 1) + 1] = pos;
-        }
-        last = pos;
-      }
+// ------------------------------------------------------------ regions
+// seq2path_jit_'s greedy merge (:1546-1560), in parallel.  Per walk, with
+// last = 0 and last_label = -1 at its start, a hit (idx, label) is taken iff
+// idx > last (then last = idx + k); a taken hit whose label differs from the
+// previous taken one opens a row (start = last before it, end = its idx + k),
+// an equal label extends the open row's end.
+//
+// Taken hits: a hit more than k past its walk predecessor is always taken
+// (last <= that predecessor's idx + k), so a walk splits into runs at such
+// hits (and at the walk's first hit, entered with last = 0); one thread
+// resolves each run sequentially.  Rows: the taken hits compacted in walk
+// order; a row starts at a taken hit that is its walk's first or changes the
+// label, and ends at the taken hit before the next row's start.
+
+// walk of hit j: the last w with seg_off[w] <= j (seg_off: nseg + 1 bounds)
+__device__ __forceinline__ uint32_t walk_of(const unsigned long long* __restrict__ seg_off, uint32_t nseg,
+                                            unsigned long long j) {
+  uint32_t lo = 0, hi = nseg;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (seg_off[mid] <= j) lo = mid + 1; else hi = mid;
+  }
+  return lo - 1;
+}
+
+__global__ void k_taken(const Hit* __restrict__ hits, uint64_t m, const unsigned long long* __restrict__ seg_off,
+                        uint32_t nseg, int k, uint8_t* __restrict__ taken) {
+  for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < m; j += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t w = walk_of(seg_off, nseg, j);
+    const unsigned long long w0 = seg_off[w], w1 = seg_off[w + 1];
+    const long long idx = (long long)hits[j].idx;
+    const bool first = j == w0;
+    if (!first && idx <= (long long)hits[j - 1].idx + k) continue;       // inside a run
+    long long last = first ? 0 : idx - 1;
+    long long prev = idx;
+    for (unsigned long long t = j; t < w1; ++t) {
+      const long long x = t == j ? idx : (long long)hits[t].idx;
+      if (t > j && x > prev + k) break;                                   // the next run
+      const bool tk = last < x;
+      taken[t] = tk;
+      if (tk) last = x + k;
+      prev = x;
     }
-    for (unsigned long long i = 0; i < nr; ++i) {
-      const int st = (int)out[3 * i], ed = (int)out[3 * i + 1];
-      const int lb = (int)out[3 * i + 2];
-      if (rc) { out[3 * i] = (int)(lseq - ed); out[3 * i + 1] = (int)(lseq - st); }
-      else { out[3 * i] = st; out[3 * i + 1] = ed; }
-      out[3 * i + 2] = lb;
+  }
+}
+
+__global__ void k_row_heads(const Hit* __restrict__ hits, const unsigned long long* __restrict__ acc, uint64_t na,
+                            const unsigned long long* __restrict__ seg_off, uint32_t nseg,
+                            uint8_t* __restrict__ head) {
+  for (uint64_t a = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; a < na; a += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long j = acc[a];
+    bool h = a == 0;
+    if (!h) {
+      const unsigned long long jp = acc[a - 1];
+      h = walk_of(seg_off, nseg, jp) != walk_of(seg_off, nseg, j) || hits[jp].label != hits[j].label;
     }
-    nrows[w] = nr;
+    head[a] = h;
+  }
+}
+
+// rows in print order (walk order = record, forward then reverse strand,
+// :1836-1844): (record, start, end, strand +1/-1, label) as int64, the
+// values through int32 (:1533) and reverse-strand rows mirrored (:1843)
+__global__ void k_rows(const Hit* __restrict__ hits, const unsigned long long* __restrict__ acc, uint64_t na,
+                       const unsigned long long* __restrict__ starts, uint64_t nrows,
+                       const unsigned long long* __restrict__ seg_off, uint32_t nseg, const int* __restrict__ walk_rec,
+                       const long long* __restrict__ rec_len, int k, long long* __restrict__ rows) {
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nrows;
+       r += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long s = starts[r], e = (r + 1 < nrows ? starts[r + 1] : na) - 1;
+    const unsigned long long js = acc[s], je = acc[e];
+    const uint32_t w = walk_of(seg_off, nseg, js);
+    long long start = 0;
+    if (s > 0) {
+      const unsigned long long jp = acc[s - 1];
+      if (walk_of(seg_off, nseg, jp) == w) start = (long long)hits[jp].idx + k;
+    }
+    const long long end = (long long)hits[je].idx + k;
+    const int rec = walk_rec[w >> 1];
+    const int st = (int)start, ed = (int)end, lb = (int)hits[js].label;
+    long long* o = rows + 5 * r;
+    o[0] = rec;
+    if (w & 1) {
+      const long long lseq = rec_len[rec];
+      o[1] = (int)(lseq - ed);
+      o[2] = (int)(lseq - st);
+      o[3] = -1;
+    } else {
+      o[1] = st;
+      o[2] = ed;
+      o[3] = 1;
+    }
+    o[4] = lb;
+  }
+}
+
+// ------------------------------------------------------------ text
+// decimal digits of v (v >= 0)
+__host__ __device__ __forceinline__ uint32_t ndig(unsigned long long v) {
+  uint32_t d = 1;
+  while (v >= 10ull) { v /= 10ull; ++d; }
+  return d;
+}
+__device__ __forceinline__ uint32_t ndig_i(long long v) {
+  return v < 0 ? 1 + ndig((unsigned long long)0 - (unsigned long long)v) : ndig((unsigned long long)v);
+}
+__device__ __forceinline__ char* put_dec(char* o, unsigned long long v) {
+  const uint32_t d = ndig(v);
+  for (uint32_t i = d; i-- > 0;) { o[i] = (char)('0' + v % 10ull); v /= 10ull; }
+  return o + d;
+}
+__device__ __forceinline__ char* put_dec_i(char* o, long long v) {
+  if (v < 0) { *o++ = '-'; return put_dec(o, (unsigned long long)0 - (unsigned long long)v); }
+  return put_dec(o, (unsigned long long)v);
+}
+
+// `.xyz` lines "%d_%d\t%d_%d\t%d\n" (:1901), keys printed as unsigned
+__global__ void k_xyz_len(const unsigned long long* __restrict__ tup, const long long* __restrict__ cnt, uint64_t n,
+                          unsigned long long* __restrict__ len) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    len[i] = ndig(tup[4 * i]) + ndig(tup[4 * i + 1]) + ndig(tup[4 * i + 2]) + ndig(tup[4 * i + 3]) +
+             ndig_i(cnt[i]) + 5;
+}
+__global__ void k_xyz_write(const unsigned long long* __restrict__ tup, const long long* __restrict__ cnt, uint64_t n,
+                            const unsigned long long* __restrict__ off, char* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    char* o = out + off[i];
+    o = put_dec(o, tup[4 * i]); *o++ = '_'; o = put_dec(o, tup[4 * i + 1]); *o++ = '\t';
+    o = put_dec(o, tup[4 * i + 2]); *o++ = '_'; o = put_dec(o, tup[4 * i + 3]); *o++ = '\t';
+    o = put_dec_i(o, cnt[i]); *o = '\n';
+  }
+}
+
+// region rows "%s\t%d\t%d\t%s\t%d\n" (:1947-1949); qid of record r is
+// names[name_off[r] .. name_off[r+1])
+__global__ void k_rowtxt_len(const long long* __restrict__ rows, uint64_t n, const long long* __restrict__ name_off,
+                             unsigned long long* __restrict__ len) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const long long* w = rows + 5 * i;
+    len[i] = (unsigned long long)(name_off[w[0] + 1] - name_off[w[0]]) + ndig_i(w[1]) + ndig_i(w[2]) +
+             ndig_i(w[4]) + 6;
+  }
+}
+__global__ void k_rowtxt_write(const long long* __restrict__ rows, uint64_t n, const char* __restrict__ names,
+                               const long long* __restrict__ name_off, const unsigned long long* __restrict__ off,
+                               char* __restrict__ out) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const long long* w = rows + 5 * i;
+    char* o = out + off[i];
+    for (long long b = name_off[w[0]]; b < name_off[w[0] + 1]; ++b) *o++ = names[b];
+    *o++ = '\t'; o = put_dec_i(o, w[1]); *o++ = '\t'; o = put_dec_i(o, w[2]);
+    *o++ = '\t'; *o++ = w[3] == 1 ? '+' : '-'; *o++ = '\t'; o = put_dec_i(o, w[4]); *o = '\n';
+  }
+}
+
+// ------------------------------------------------------------ labels from edges
+// seq2graph :1932-1944: every `.xyz` node (n0_v0, then n1_v1 of each edge, in
+// file order) that the `.mcl` did not label gets the next label, in order of
+// first appearance.  Nodes sorted by (key, value) with their positions
+// (stable radix sorts: each group's first element is its first appearance).
+__global__ void k_nodes(const unsigned long long* __restrict__ tup, uint64_t nn, unsigned long long* __restrict__ key,
+                        unsigned* __restrict__ val, unsigned long long* __restrict__ pos) {
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < nn; t += (uint64_t)gridDim.x * blockDim.x) {
+    key[t] = tup[2 * t];                       // (n0, v0, n1, v1): node t is words 2t, 2t+1
+    val[t] = (unsigned)tup[2 * t + 1];
+    pos[t] = t;
+  }
+}
+__global__ void k_gather_key(const unsigned long long* __restrict__ src, const unsigned long long* __restrict__ pos,
+                             uint64_t n, unsigned long long* __restrict__ dst) {
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x)
+    dst[t] = src[pos[t]];
+}
+// first appearances not in the .mcl table: flag the group heads
+__global__ void k_node_heads(const unsigned long long* __restrict__ skey, const unsigned long long* __restrict__ pos,
+                             const unsigned* __restrict__ val0, uint64_t n, const LabSlot* __restrict__ lab,
+                             uint64_t lab_capmask, int have_mcl, uint8_t* __restrict__ head) {
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long kk = skey[t];
+    const unsigned v = val0[pos[t]];
+    bool h = t == 0 || skey[t - 1] != kk || val0[pos[t - 1]] != v;
+    long long id;
+    if (h && have_mcl && label_get(lab, lab_capmask, (long long)kk, (long long)v, id)) h = false;
+    head[t] = h;
+  }
+}
+__global__ void k_lab_new(const unsigned long long* __restrict__ first, uint64_t nu,
+                          const unsigned long long* __restrict__ tup, long long next_id,
+                          long long* __restrict__ out_key, long long* __restrict__ out_val,
+                          long long* __restrict__ out_id) {
+  for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < nu; r += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long t = first[r];
+    out_key[r] = (long long)tup[2 * t];
+    out_val[r] = (long long)tup[2 * t + 1];
+    out_id[r] = next_id + (long long)r;
   }
 }
 
@@ -393,6 +574,11 @@ __global__ void k_gather_bounds(const unsigned long long* __restrict__ sf, const
     out[2 * i] = sf[run_off[i]];
     out[2 * i + 1] = sr[run_off[i]];
   }
+}
+
+__global__ void k_iota64(unsigned long long* __restrict__ out, uint64_t n) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    out[i] = i;
 }
 
 // ------------------------------------------------------------------ host
@@ -507,6 +693,42 @@ static uint64_t walk_collect(Ctx& c, WalkPlan& P, WalkArgs& a, DevBuf& out, size
   return total;
 }
 
+// rocPRIM helpers on the context's stream and scratch
+template <class K, class V>
+static void sort_pairs(Ctx& c, const K* kin, K* kout, const V* vin, V* vout, uint64_t n, int end_bit) {
+  with_temp(c, [&](void* tmp, size_t& bytes) {
+    return rocprim::radix_sort_pairs(tmp, bytes, kin, kout, vin, vout, (size_t)n, 0, end_bit, c.stream);
+  });
+}
+template <class T>
+static uint64_t select_flagged(Ctx& c, const T* in, const uint8_t* flags, T* out, uint64_t n, DevBuf& cnt) {
+  cnt.reserve(16);
+  with_temp(c, [&](void* tmp, size_t& bytes) {
+    return rocprim::select(tmp, bytes, in, flags, out, cnt.as<unsigned long long>(), (size_t)n, c.stream);
+  });
+  unsigned long long h = 0;
+  PG_HIP(hipMemcpyAsync(&h, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  return h;
+}
+static uint64_t excl_scan_total(Ctx& c, const unsigned long long* len, unsigned long long* off, uint64_t n) {
+  // off[0..n]: exclusive prefix sums, off[n] = total
+  PG_HIP(hipMemsetAsync(const_cast<unsigned long long*>(len) + n, 0, 8, c.stream));
+  with_temp(c, [&](void* tmp, size_t& bytes) {
+    return rocprim::exclusive_scan(tmp, bytes, len, off, 0ull, (size_t)n + 1, rocprim::plus<unsigned long long>(),
+                                   c.stream);
+  });
+  unsigned long long h = 0;
+  PG_HIP(hipMemcpyAsync(&h, off + n, 8, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  return h;
+}
+static int bits_for(uint64_t maxv) {
+  int b = 1;
+  while (b < 64 && (maxv >> b)) ++b;
+  return b;
+}
+
 uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1) {
   if (!c.reduced) throw Error(-22, "pg_edges: no rdBG (call pg_build_rdbg first)");
   WalkPlan P;
@@ -515,101 +737,264 @@ uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1) {
   std::vector<unsigned long long> so, sc;
   const uint64_t m = walk_collect<0>(c, P, a, c.occ, sizeof(Occ), so, sc);
   c.n_edges = 0;
-  const uint64_t ecap = next_pow2(std::max<uint64_t>(1024, 2 * m));
-  c.edge_cap = ecap;
-  c.pair_cap = ecap;
-  c.edge_tab.reserve(sizeof(EdgeSlot) * ecap);
-  c.pair_tab.reserve(8 * ecap);
-  PG_HIP(hipMemsetAsync(c.edge_tab.p, 0, sizeof(EdgeSlot) * ecap, c.stream));
-  PG_HIP(hipMemsetAsync(c.pair_tab.p, 0, 8 * ecap, c.stream));
+  c.text_xyz = false;
+  // Distinct edges join rdBG members: the edge table starts at 4 slots per
+  // rdBG key (C3: 1.93 M keys, 2.5 M edges among 1e8 member occurrences) and
+  // grows (x4, up to 2 per occurrence) when a probe sequence runs long.  The
+  // (edge, walk) set holds one entry per occurrence at most.
+  const uint64_t emax = next_pow2(std::max<uint64_t>(1024, 2 * m));
+  uint64_t ecap = std::min(emax, next_pow2(std::max<uint64_t>(1024, 4 * (c.n_rdbg + 1))));
+  const uint64_t pcap = emax;
+  c.pair_cap = pcap;
+  c.pair_tab.reserve(8 * pcap);
   DevBuf err;
   err.reserve(16);
-  PG_HIP(hipMemsetAsync(err.p, 0, 16, c.stream));
-  c.edge_out.reserve(sizeof(EdgeOut) * (m + 1));
   unsigned long long n_out = 0;
-  if (m > 1) {
-    DevBuf rb;
-    rb.reserve(8 * 2 * (m + 2));
-    unsigned long long* lists[2] = {rb.as<unsigned long long>(), rb.as<unsigned long long>() + (m + 1)};
-    DevBuf nr;
-    nr.reserve(16);
-    const unsigned long long* cur = nullptr;
-    uint64_t ncur = m;
-    for (int round = 0; ncur && round < 64; ++round) {
-      unsigned long long* out = lists[round & 1];
-      PG_HIP(hipMemsetAsync(nr.p, 0, 8, c.stream));
-      hipLaunchKernelGGL(k_edges, dim3(grid_for(ncur, 256, 16384)), dim3(256), 0, c.stream, c.occ.as<Occ>(), m,
-                         cur, ncur, c.edge_tab.as<EdgeSlot>(), ecap - 1, c.pair_tab.as<unsigned long long>(),
-                         ecap - 1, out, nr.as<unsigned long long>(), err.as<unsigned>());
-      PG_HIP(hipGetLastError());
-      unsigned long long nn = 0;
-      PG_HIP(hipMemcpyAsync(&nn, nr.p, 8, hipMemcpyDeviceToHost, c.stream));
-      c.sync();
-      cur = out;
-      ncur = nn;
+  for (;;) {
+    c.edge_cap = ecap;
+    c.edge_tab.reserve(sizeof(EdgeSlot) * ecap);
+    PG_HIP(hipMemsetAsync(c.edge_tab.p, 0, sizeof(EdgeSlot) * ecap, c.stream));
+    PG_HIP(hipMemsetAsync(c.pair_tab.p, 0, 8 * pcap, c.stream));
+    PG_HIP(hipMemsetAsync(err.p, 0, 16, c.stream));
+    if (m > 1) {
+      DevBuf rb;
+      rb.reserve(8 * 2 * (m + 2));
+      unsigned long long* lists[2] = {rb.as<unsigned long long>(), rb.as<unsigned long long>() + (m + 1)};
+      DevBuf nr;
+      nr.reserve(16);
+      const unsigned long long* cur = nullptr;
+      uint64_t ncur = m;
+      for (int round = 0; ncur && round < 64; ++round) {
+        unsigned long long* out = lists[round & 1];
+        PG_HIP(hipMemsetAsync(nr.p, 0, 8, c.stream));
+        hipLaunchKernelGGL(k_edges, dim3(grid_for(ncur, 256, 16384)), dim3(256), 0, c.stream, c.occ.as<Occ>(), m,
+                           cur, ncur, c.edge_tab.as<EdgeSlot>(), ecap - 1, c.pair_tab.as<unsigned long long>(),
+                           pcap - 1, out, nr.as<unsigned long long>(), err.as<unsigned>());
+        PG_HIP(hipGetLastError());
+        unsigned long long nn = 0;
+        PG_HIP(hipMemcpyAsync(&nn, nr.p, 8, hipMemcpyDeviceToHost, c.stream));
+        c.sync();
+        cur = out;
+        ncur = nn;
+      }
+      if (ncur) throw Error(-5, "pg_edges: edge insert did not converge");
     }
-    if (ncur) throw Error(-5, "pg_edges: edge insert did not converge");
-    rb.release();
-    nr.release();
+    unsigned e = 0;
+    // (c.stream is non-blocking: a null-stream hipMemcpy would not wait for the
+    // memset above when m <= 1 queued nothing that synced)
+    PG_HIP(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    if ((e & 2u) && ecap < emax) {                              // the edge table was too small: again, larger
+      ecap = std::min(emax, ecap * 4);
+      continue;
+    }
+    if (e) throw Error(-5, "pg_edges: edge table error " + std::to_string(e));
+    break;
+  }
+  if (m > 1) {
+    // compact, then order by first occurrence on the device
     DevBuf cnt;
     cnt.reserve(8);
     PG_HIP(hipMemsetAsync(cnt.p, 0, 8, c.stream));
+    c.edge_out.reserve(sizeof(EdgeOut) * std::max<uint64_t>(m, 1));
+    DevBuf kv;
+    kv.reserve((8 + 8 + 4 + 4) * std::min<uint64_t>(m, ecap) + 64);
+    auto* k0 = kv.as<unsigned long long>();
+    auto* k1 = k0 + std::min<uint64_t>(m, ecap);
+    auto* v0 = reinterpret_cast<unsigned*>(k1 + std::min<uint64_t>(m, ecap));
+    auto* v1 = v0 + std::min<uint64_t>(m, ecap);
     hipLaunchKernelGGL(k_edges_compact, dim3(grid_for(ecap, 256, 8192)), dim3(256), 0, c.stream,
-                       c.edge_tab.as<EdgeSlot>(), ecap, c.occ.as<Occ>(), c.edge_out.as<EdgeOut>(),
+                       c.edge_tab.as<EdgeSlot>(), ecap, c.occ.as<Occ>(), c.edge_out.as<EdgeOut>(), k0, v0,
                        cnt.as<unsigned long long>());
     PG_HIP(hipGetLastError());
     PG_HIP(hipMemcpyAsync(&n_out, cnt.p, 8, hipMemcpyDeviceToHost, c.stream));
     c.sync();
-    cnt.release();
+    if (n_out) {
+      sort_pairs(c, k0, k1, v0, v1, n_out, bits_for(m));
+      c.edge_exp.reserve((8 * 4 + 8 + 8) * n_out);
+      auto* tup = c.edge_exp.as<unsigned long long>();
+      auto* ecnt = reinterpret_cast<long long*>(tup + 4 * n_out);
+      auto* ewalk = ecnt + n_out;
+      hipLaunchKernelGGL(k_edges_order, dim3(grid_for(n_out, 256, 8192)), dim3(256), 0, c.stream,
+                         c.edge_out.as<EdgeOut>(), v1, n_out, tup, ecnt, ewalk);
+      PG_HIP(hipGetLastError());
+      c.sync();
+    }
   }
-  unsigned e = 0;
-  // (c.stream is non-blocking: a null-stream hipMemcpy would not wait for the
-  // memset above when m <= 1 queued nothing that synced)
-  PG_HIP(hipMemcpyAsync(&e, err.p, 4, hipMemcpyDeviceToHost, c.stream));
-  c.sync();
-  err.release();
-  if (e) throw Error(-5, "pg_edges: edge table error " + std::to_string(e));
   c.n_edges = n_out;
   return n_out;
 }
 
 void export_edges(Ctx& c, uint64_t* tuples, int64_t* counts, int64_t* first_walk, uint64_t cap) {
   const uint64_t n = std::min<uint64_t>(cap, c.n_edges);
-  std::vector<EdgeOut> h(n);
-  if (n) {
-    PG_HIP(hipMemcpyAsync(h.data(), c.edge_out.p, sizeof(EdgeOut) * n, hipMemcpyDeviceToHost, c.stream));
-    c.sync();
-  }
-  // order by first occurrence (typed-Dict insertion order, :1479-1484)
-  std::vector<uint64_t> idx(n);
-  for (uint64_t i = 0; i < n; ++i) idx[i] = i;
-  std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return h[a].first < h[b].first; });
-  for (uint64_t j = 0; j < n; ++j) {
-    const EdgeOut& e = h[idx[j]];
-    tuples[4 * j] = e.n0; tuples[4 * j + 1] = e.v0; tuples[4 * j + 2] = e.n1; tuples[4 * j + 3] = e.v1;
-    counts[j] = (int64_t)e.count;
-    first_walk[j] = (int64_t)e.walk;
-  }
+  if (!n) return;
+  const auto* tup = c.edge_exp.as<unsigned long long>();
+  const auto* ecnt = reinterpret_cast<const long long*>(tup + 4 * c.n_edges);
+  const auto* ewalk = ecnt + c.n_edges;
+  PG_HIP(hipMemcpyAsync(tuples, tup, 32 * n, hipMemcpyDeviceToHost, c.stream));
+  PG_HIP(hipMemcpyAsync(counts, ecnt, 8 * n, hipMemcpyDeviceToHost, c.stream));
+  PG_HIP(hipMemcpyAsync(first_walk, ewalk, 8 * n, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
 }
 
-void set_labels(Ctx& c, const int64_t* key, const int64_t* val, const int64_t* id, uint64_t n) {
+// the .xyz text of the last edge pass, in first-occurrence order
+uint64_t format_edges(Ctx& c, char* out, uint64_t cap) {
+  const uint64_t n = c.n_edges;
+  if (!c.text_xyz) {
+    c.text_len.reserve(8 * (n + 1));
+    c.text_off.reserve(8 * (n + 1));
+    const auto* tup = c.edge_exp.as<unsigned long long>();
+    const auto* ecnt = reinterpret_cast<const long long*>(tup + 4 * n);
+    if (n) {
+      hipLaunchKernelGGL(k_xyz_len, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c.stream, tup, ecnt, n,
+                         c.text_len.as<unsigned long long>());
+      PG_HIP(hipGetLastError());
+    }
+    c.text_total = excl_scan_total(c, c.text_len.as<unsigned long long>(), c.text_off.as<unsigned long long>(), n);
+    c.text_xyz = true;
+    c.text_rows = false;
+  }
+  if (!out) return c.text_total;
+  if (cap < c.text_total) throw Error(-34, "pg_edges_format: buffer too small");
+  if (n) {
+    c.text_buf.reserve(c.text_total + 16);
+    const auto* tup = c.edge_exp.as<unsigned long long>();
+    const auto* ecnt = reinterpret_cast<const long long*>(tup + 4 * n);
+    hipLaunchKernelGGL(k_xyz_write, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c.stream, tup, ecnt, n,
+                       c.text_off.as<unsigned long long>(), c.text_buf.as<char>());
+    PG_HIP(hipGetLastError());
+    PG_HIP(hipMemcpyAsync(out, c.text_buf.p, c.text_total, hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+  }
+  return c.text_total;
+}
+
+static void lab_build(Ctx& c, const long long* d_key, const long long* d_val, const long long* d_id, uint64_t n) {
   const uint64_t cap = next_pow2(std::max<uint64_t>(1024, 2 * n + 16));
   c.lab_cap = cap;
   c.lab_tab.reserve(sizeof(LabSlot) * cap);
   PG_HIP(hipMemsetAsync(c.lab_tab.p, 0, sizeof(LabSlot) * cap, c.stream));
   if (n) {
-    DevBuf tmp;
-    tmp.reserve(24 * n);
-    long long* dk = tmp.as<long long>();
+    hipLaunchKernelGGL(k_lab_insert, dim3(grid_for(n, 256, 4096)), dim3(256), 0, c.stream, d_key, d_val, d_id, n,
+                       c.lab_tab.as<LabSlot>(), cap - 1);
+    PG_HIP(hipGetLastError());
+  }
+}
+
+void set_labels(Ctx& c, const int64_t* key, const int64_t* val, const int64_t* id, uint64_t n) {
+  c.lab_list.reserve(24 * (n + 1));
+  long long* dk = c.lab_list.as<long long>();
+  if (n) {
     PG_HIP(hipMemcpyAsync(dk, key, 8 * n, hipMemcpyHostToDevice, c.stream));
     PG_HIP(hipMemcpyAsync(dk + n, val, 8 * n, hipMemcpyHostToDevice, c.stream));
     PG_HIP(hipMemcpyAsync(dk + 2 * n, id, 8 * n, hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_lab_insert, dim3(grid_for(n, 256, 4096)), dim3(256), 0, c.stream, dk, dk + n, dk + 2 * n,
-                       n, c.lab_tab.as<LabSlot>(), cap - 1);
-    PG_HIP(hipGetLastError());
-    c.sync();
-    tmp.release();
   }
+  lab_build(c, dk, dk + n, dk + 2 * n, n);
+  c.n_labels = n;
+  c.sync();
+}
+
+// seq2graph's label dictionary (:1918-1944) built on the device: the `.mcl`
+// entries (the host's dict of line indices, a later line winning), then the
+// `.xyz` nodes the .mcl did not label, numbered next_id, next_id + 1, ... in
+// order of first appearance.  Edges: h_tuples (n x 4, file order) or, when
+// NULL, the last edge pass in first-occurrence order.
+uint64_t labels_from_edges(Ctx& c, const uint64_t* h_tuples, uint64_t n_edges, const int64_t* mk, const int64_t* mv,
+                           const int64_t* mi, uint64_t n_mcl, int64_t next_id) {
+  DevBuf up;
+  const unsigned long long* tup;
+  if (h_tuples) {
+    up.reserve(32 * (n_edges + 1));
+    if (n_edges) PG_HIP(hipMemcpyAsync(up.p, h_tuples, 32 * n_edges, hipMemcpyHostToDevice, c.stream));
+    tup = up.as<unsigned long long>();
+  } else {
+    n_edges = c.n_edges;
+    tup = c.edge_exp.as<unsigned long long>();
+  }
+  // the .mcl entries first (their table answers "labelled by the .mcl?")
+  DevBuf mcl;
+  mcl.reserve(24 * (n_mcl + 1));
+  long long* dk = mcl.as<long long>();
+  if (n_mcl) {
+    PG_HIP(hipMemcpyAsync(dk, mk, 8 * n_mcl, hipMemcpyHostToDevice, c.stream));
+    PG_HIP(hipMemcpyAsync(dk + n_mcl, mv, 8 * n_mcl, hipMemcpyHostToDevice, c.stream));
+    PG_HIP(hipMemcpyAsync(dk + 2 * n_mcl, mi, 8 * n_mcl, hipMemcpyHostToDevice, c.stream));
+  }
+  lab_build(c, dk, dk + n_mcl, dk + 2 * n_mcl, n_mcl);
+  const uint64_t nn = 2 * n_edges;
+  uint64_t nu = 0;
+  DevBuf firsts;
+  if (nn) {
+    // nodes -> sorted by value, then stably by key, positions carried
+    DevBuf w;
+    w.reserve((8 + 8 + 4 + 4 + 8 + 8 + 8) * nn + 64);
+    auto* key = w.as<unsigned long long>();
+    auto* skey = key + nn;
+    auto* pos = skey + nn;
+    auto* pos2 = pos + nn;
+    auto* tmpk = pos2 + nn;
+    auto* val = reinterpret_cast<unsigned*>(tmpk + nn);
+    auto* sval = val + nn;
+    hipLaunchKernelGGL(k_nodes, dim3(grid_for(nn, 256, 8192)), dim3(256), 0, c.stream, tup, nn, key, val, pos);
+    PG_HIP(hipGetLastError());
+    uint64_t maxv = 0xFFFFu, maxk = ~0ull;
+    if (h_tuples) {
+      maxv = 0;
+      for (uint64_t i = 0; i < nn; ++i) maxv = std::max<uint64_t>(maxv, h_tuples[2 * i + 1]);
+    }
+    if (maxv > 0xFFFFFFFFull) throw Error(-22, "pg_labels_from_edges: node value above 2^32");
+    sort_pairs(c, val, sval, pos, pos2, nn, bits_for(maxv));          // by value
+    hipLaunchKernelGGL(k_gather_key, dim3(grid_for(nn, 256, 8192)), dim3(256), 0, c.stream, key, pos2, nn, tmpk);
+    PG_HIP(hipGetLastError());
+    sort_pairs(c, tmpk, skey, pos2, pos, nn, bits_for(maxk));           // then stably by key
+    DevBuf flag, cnt;
+    flag.reserve(nn + 16);
+    hipLaunchKernelGGL(k_node_heads, dim3(grid_for(nn, 256, 8192)), dim3(256), 0, c.stream, skey, pos, val, nn,
+                       c.lab_tab.as<LabSlot>(), c.lab_cap - 1, (int)(n_mcl != 0), flag.as<uint8_t>());
+    PG_HIP(hipGetLastError());
+    firsts.reserve(16 * nn + 16);
+    auto* f0 = firsts.as<unsigned long long>();
+    nu = select_flagged(c, pos, flag.as<uint8_t>(), f0, nn, cnt);
+    if (nu) {
+      with_temp(c, [&](void* tmp, size_t& bytes) {
+        return rocprim::radix_sort_keys(tmp, bytes, f0, f0 + nn, (size_t)nu, 0, bits_for(nn), c.stream);
+      });
+    }
+    // the label list: .mcl entries, then the new ones in order
+    c.lab_list.reserve(24 * (n_mcl + nu + 1));
+    long long* L = c.lab_list.as<long long>();
+    const uint64_t nl = n_mcl + nu;
+    if (n_mcl) {
+      PG_HIP(hipMemcpyAsync(L, dk, 8 * n_mcl, hipMemcpyDeviceToDevice, c.stream));
+      PG_HIP(hipMemcpyAsync(L + nl, dk + n_mcl, 8 * n_mcl, hipMemcpyDeviceToDevice, c.stream));
+      PG_HIP(hipMemcpyAsync(L + 2 * nl, dk + 2 * n_mcl, 8 * n_mcl, hipMemcpyDeviceToDevice, c.stream));
+    }
+    if (nu) {
+      hipLaunchKernelGGL(k_lab_new, dim3(grid_for(nu, 256, 8192)), dim3(256), 0, c.stream, f0 + nn, nu, tup,
+                         (long long)next_id, L + n_mcl, L + nl + n_mcl, L + 2 * nl + n_mcl);
+      PG_HIP(hipGetLastError());
+    }
+    lab_build(c, L, L + nl, L + 2 * nl, nl);
+    c.n_labels = nl;
+  } else {
+    c.lab_list.reserve(24 * (n_mcl + 1));
+    long long* L = c.lab_list.as<long long>();
+    if (n_mcl) PG_HIP(hipMemcpyAsync(L, dk, 24 * n_mcl, hipMemcpyDeviceToDevice, c.stream));
+    c.n_labels = n_mcl;
+  }
+  c.sync();
+  return c.n_labels;
+}
+
+void export_labels(Ctx& c, int64_t* key, int64_t* val, int64_t* id, uint64_t cap) {
+  const uint64_t n = c.n_labels;
+  if (cap < n) throw Error(-34, "pg_labels_export: buffer too small");
+  if (!n) return;
+  const long long* L = c.lab_list.as<long long>();
+  PG_HIP(hipMemcpyAsync(key, L, 8 * n, hipMemcpyDeviceToHost, c.stream));
+  PG_HIP(hipMemcpyAsync(val, L + n, 8 * n, hipMemcpyDeviceToHost, c.stream));
+  PG_HIP(hipMemcpyAsync(id, L + 2 * n, 8 * n, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
 }
 
 uint64_t walk_rows(Ctx& c, const uint8_t* h_rec_flag, int rc1) {
@@ -622,47 +1007,94 @@ uint64_t walk_rows(Ctx& c, const uint8_t* h_rec_flag, int rc1) {
   DevBuf hits;
   const uint64_t m = walk_collect<1>(c, P, a, hits, sizeof(Hit), so, sc);
   const uint64_t nseg = so.size();
-  c.h_rows.clear();
   c.n_rows = 0;
-  if (nseg == 0) return 0;
+  c.text_rows = false;
+  if (nseg == 0 || m == 0) return 0;
+  // walk bounds (segments are contiguous in walk order)
   DevBuf meta;
-  meta.reserve(8 * 4 * nseg);
-  auto* d_so = meta.as<unsigned long long>();
-  auto* d_sc = d_so + nseg;
-  auto* d_len = reinterpret_cast<long long*>(d_sc + nseg);
-  auto* d_nr = reinterpret_cast<unsigned long long*>(d_len + nseg);
-  std::vector<long long> lens(nseg / 2);
-  for (size_t i = 0; i < P.recs.size(); ++i) lens[i] = c.h_rec_len[P.recs[i]];
-  PG_HIP(hipMemcpyAsync(d_so, so.data(), 8 * nseg, hipMemcpyHostToDevice, c.stream));
-  PG_HIP(hipMemcpyAsync(d_sc, sc.data(), 8 * nseg, hipMemcpyHostToDevice, c.stream));
-  PG_HIP(hipMemcpyAsync(d_len, lens.data(), 8 * lens.size(), hipMemcpyHostToDevice, c.stream));
-  c.rows_buf.reserve(24 * (m + 1));
-  hipLaunchKernelGGL(k_regions, dim3(grid_for(nseg, 64, 4096)), dim3(64), 0, c.stream, hits.as<Hit>(), d_so, d_sc,
-                     d_len, nseg, c.k, c.rows_buf.as<long long>(), d_nr);
+  meta.reserve(8 * (nseg + 2));
+  std::vector<unsigned long long> bounds(nseg + 1);
+  for (size_t w = 0; w < nseg; ++w) bounds[w] = so[w];
+  bounds[nseg] = m;
+  PG_HIP(hipMemcpyAsync(meta.p, bounds.data(), 8 * (nseg + 1), hipMemcpyHostToDevice, c.stream));
+  const auto* d_bounds = meta.as<unsigned long long>();
+  DevBuf flag, cnt, acc;
+  flag.reserve(m + 16);
+  acc.reserve(8 * (m + 1));
+  hipLaunchKernelGGL(k_taken, dim3(grid_for(m, 256, 16384)), dim3(256), 0, c.stream, hits.as<Hit>(), m, d_bounds,
+                     (uint32_t)nseg, c.k, flag.as<uint8_t>());
   PG_HIP(hipGetLastError());
-  std::vector<unsigned long long> nr(nseg);
-  PG_HIP(hipMemcpyAsync(nr.data(), d_nr, 8 * nseg, hipMemcpyDeviceToHost, c.stream));
-  std::vector<long long> rows(3 * (m + 1));
-  if (m) PG_HIP(hipMemcpyAsync(rows.data(), c.rows_buf.p, 24 * m, hipMemcpyDeviceToHost, c.stream));
+  // indices of the taken hits (a counting iterator through rocprim::select)
+  DevBuf idx;
+  idx.reserve(8 * (m + 1));
+  hipLaunchKernelGGL(k_iota64, dim3(grid_for(m, 256, 16384)), dim3(256), 0, c.stream, idx.as<unsigned long long>(), m);
+  PG_HIP(hipGetLastError());
+  const uint64_t na = select_flagged(c, idx.as<unsigned long long>(), flag.as<uint8_t>(),
+                                     acc.as<unsigned long long>(), m, cnt);
+  if (na == 0) return 0;
+  hipLaunchKernelGGL(k_row_heads, dim3(grid_for(na, 256, 16384)), dim3(256), 0, c.stream, hits.as<Hit>(),
+                     acc.as<unsigned long long>(), na, d_bounds, (uint32_t)nseg, flag.as<uint8_t>());
+  PG_HIP(hipGetLastError());
+  hipLaunchKernelGGL(k_iota64, dim3(grid_for(na, 256, 16384)), dim3(256), 0, c.stream, idx.as<unsigned long long>(), na);
+  PG_HIP(hipGetLastError());
+  DevBuf starts;
+  starts.reserve(8 * (na + 1));
+  const uint64_t nrows = select_flagged(c, idx.as<unsigned long long>(), flag.as<uint8_t>(),
+                                        starts.as<unsigned long long>(), na, cnt);
+  c.rows_buf.reserve(40 * (nrows + 1));
+  hipLaunchKernelGGL(k_rows, dim3(grid_for(nrows, 256, 16384)), dim3(256), 0, c.stream, hits.as<Hit>(),
+                     acc.as<unsigned long long>(), na, starts.as<unsigned long long>(), nrows, d_bounds,
+                     (uint32_t)nseg, P.d_recs.as<int>(), c.rec_len.as<long long>(), c.k, c.rows_buf.as<long long>());
+  PG_HIP(hipGetLastError());
   c.sync();
-  // rows in reference order: record, forward rows then reverse rows (:1836-1844)
-  for (size_t i = 0; i < P.recs.size(); ++i) {
-    for (int s = 0; s < 2; ++s) {
-      const size_t w = 2 * i + s;
-      for (unsigned long long j = 0; j < nr[w]; ++j) {
-        const long long* rw = &rows[3 * (so[w] + j)];
-        c.h_rows.push_back(P.recs[i]);
-        c.h_rows.push_back(rw[0]);
-        c.h_rows.push_back(rw[1]);
-        c.h_rows.push_back(s == 0 ? 1 : -1);
-        c.h_rows.push_back(rw[2]);
-      }
+  c.n_rows = nrows;
+  return nrows;
+}
+
+void export_rows(Ctx& c, int64_t* rows5, uint64_t cap) {
+  if (cap < c.n_rows) throw Error(-34, "pg_rows_export: buffer too small");
+  if (!c.n_rows) return;
+  PG_HIP(hipMemcpyAsync(rows5, c.rows_buf.p, 40 * c.n_rows, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+}
+
+// the region rows' text of the last row pass; names[name_off[r] ..
+// name_off[r+1]) is record r's qid (R + 1 offsets)
+uint64_t format_rows_text(Ctx& c, const char* names, const int64_t* name_off, uint64_t n_names, char* out,
+                          uint64_t cap) {
+  const uint64_t n = c.n_rows;
+  if (!c.text_rows) {
+    c.text_names.reserve(8 * (n_names + 1) + (uint64_t)std::max<int64_t>(name_off[n_names], 0) + 16);
+    long long* d_off = c.text_names.as<long long>();
+    char* d_names = reinterpret_cast<char*>(d_off + n_names + 1);
+    PG_HIP(hipMemcpyAsync(d_off, name_off, 8 * (n_names + 1), hipMemcpyHostToDevice, c.stream));
+    if (name_off[n_names])
+      PG_HIP(hipMemcpyAsync(d_names, names, (size_t)name_off[n_names], hipMemcpyHostToDevice, c.stream));
+    c.text_len.reserve(8 * (n + 1));
+    c.text_off.reserve(8 * (n + 1));
+    if (n) {
+      hipLaunchKernelGGL(k_rowtxt_len, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c.stream,
+                         c.rows_buf.as<long long>(), n, d_off, c.text_len.as<unsigned long long>());
+      PG_HIP(hipGetLastError());
     }
+    c.text_total = excl_scan_total(c, c.text_len.as<unsigned long long>(), c.text_off.as<unsigned long long>(), n);
+    c.text_rows = true;
+    c.text_xyz = false;
   }
-  c.n_rows = c.h_rows.size() / 5;
-  meta.release();
-  hits.release();
-  return c.n_rows;
+  if (!out) return c.text_total;
+  if (cap < c.text_total) throw Error(-34, "pg_rows_format: buffer too small");
+  if (n) {
+    const long long* d_off = c.text_names.as<long long>();
+    const char* d_names = reinterpret_cast<const char*>(d_off + n_names + 1);
+    c.text_buf.reserve(c.text_total + 16);
+    hipLaunchKernelGGL(k_rowtxt_write, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c.stream,
+                       c.rows_buf.as<long long>(), n, d_names, d_off, c.text_off.as<unsigned long long>(),
+                       c.text_buf.as<char>());
+    PG_HIP(hipGetLastError());
+    PG_HIP(hipMemcpyAsync(out, c.text_buf.p, c.text_total, hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+  }
+  return c.text_total;
 }
 
 }  // namespace pg

@@ -430,9 +430,9 @@ class GpuShard:
         return self.ctx.edges(flags, bool(rc1))
 
     def rows_text(self, labels, flags, rc1, names):
-        from ._lib import format_rows
         self.ctx.set_labels(*labels)
-        return format_rows(self.ctx.rows(flags, bool(rc1)), names)
+        self.ctx.rows_count(flags, bool(rc1))
+        return self.ctx.rows_text(names)
 
     def dump_global(self, keys, masks, counts, k, device):
         from ._lib import Context

@@ -237,6 +237,24 @@ def label_dict(mcl_text: str, xyz_lines) -> dict:
     return lab
 
 
+def mcl_labels(mcl_text: str):
+    """The `.mcl` part of seq2graph's label dictionary (:1918-1929): every
+    token's line index, a later line winning as dict assignment does.
+    Returns (keys, vals, ids) as int64 (keys carry the uint64 key's bits) and
+    the number of lines (the next label)."""
+    seen = {}
+    flag = 0
+    for line in mcl_text.splitlines(keepends=True):
+        for tok in line[:-1].split("\t"):
+            p = tok.split("_")[:2]
+            seen[(int(p[0]), int(p[1]))] = flag
+        flag += 1
+    mk = np.array([k for k, _ in seen.keys()], dtype=np.uint64).view(np.int64)
+    mv = np.array([v for _, v in seen.keys()], dtype=np.uint64).view(np.int64)
+    mi = np.fromiter(seen.values(), dtype=np.int64, count=len(seen))
+    return mk, mv, mi, flag
+
+
 def label_table(mcl_text: str, tuples: np.ndarray):
     """label_dict + label_arrays without the text round trip: the `.mcl` line
     index of every token (a later line wins, as dict assignment does), then

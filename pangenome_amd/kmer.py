@@ -24,16 +24,36 @@ import numpy as np
 from collections.abc import Mapping
 
 from . import host
-from ._lib import Context, format_rows, format_xyz
+from ._lib import Context, format_xyz
 
 
 class LabelTable(Mapping):
     """seq2graph's label dictionary {(key, value): label} (:1918-1944), kept as
-    arrays; the Python dict is built only if it is looked into."""
+    arrays (or on the device, fetched by `loader` when first needed); the
+    Python dict is built only if it is looked into."""
 
-    def __init__(self, keys, vals, ids):
-        self.keys_, self.vals_, self.ids_ = keys, vals, ids
+    def __init__(self, keys=None, vals=None, ids=None, loader=None):
+        self._arrays = None if loader is not None else (keys, vals, ids)
+        self._loader = loader
         self._d = None
+
+    @property
+    def keys_(self):
+        return self._get()[0]
+
+    @property
+    def vals_(self):
+        return self._get()[1]
+
+    @property
+    def ids_(self):
+        return self._get()[2]
+
+    def _get(self):
+        if self._arrays is None:
+            self._arrays = self._loader()
+            self._loader = None
+        return self._arrays
 
     def _dict(self):
         if self._d is None:
@@ -169,15 +189,21 @@ def dbg2rdbg(kmer_dict):
     return kmer_dict
 
 
-def rdbg_edges(g: DeviceGraph, Ns, chunk, rc, brkpt=""):
+def rdbg_edges(g: DeviceGraph, Ns, chunk, rc, brkpt="", keep_on_device=False):
     """Edge Dict of rdbg_edge_weight_jit_ (:1808-1827) in its iteration order;
-    an existing `brkpt` (-R) is the Dict so far and the offset to resume at."""
+    an existing `brkpt` (-R) is the Dict so far and the offset to resume at.
+    With keep_on_device and neither a -R resume nor a checkpoint (the order is
+    then the device's first-occurrence order), the edges stay on the device
+    and None is returned."""
     loaded, resume = None, None
     if brkpt and os.path.isfile(brkpt):
         offset, lt, lc = host.read_edge_npz(brkpt)
         loaded, resume = (lt, lc), host.resume_position(offset, g.rec_ptr)
     flags, segment, ncp, ckpt = host.plan_edges(g.seq_len, g.shape, int(Ns), int(chunk), resume=resume,
                                                 checkpoint=True)
+    if keep_on_device and loaded is None and ncp == 0:
+        g.ctx.edges_count(flags, bool(rc))
+        return None
 
     def state(fl, upto):                          # the Dict after segments 0..upto, in iteration order
         tuples, counts, walk_first = g.ctx.edges(fl, bool(rc))
@@ -197,13 +223,15 @@ def rdbg_edges(g: DeviceGraph, Ns, chunk, rc, brkpt=""):
 def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_dict=None, saved=None,
               hashfunc=None, jit=True, chunk=2 ** 33, rc=False, cluster=True, out=None):
     """:1853-1951: edge weights -> `<qry>_rdbg_weight.xyz` -> mcl (or reuse)
-    -> label dictionary -> print the region rows."""
+    -> label dictionary -> print the region rows.  The edges, the label
+    table, the rows and both texts are made on the device; the host writes
+    the files and runs (or reuses) mcl."""
     out = out or sys.stdout
     g = rdbg_dict
-    tuples, counts = rdbg_edges(g, Ns, chunk, rc, brkpt=brkpt)
+    res = rdbg_edges(g, Ns, chunk, rc, brkpt=brkpt, keep_on_device=True)
     oname = qry + "_rdbg_weight.xyz"
     with open(oname, "wb") as f:                      # "%d_%d\t%d_%d\t%d\n" (:1893-1904)
-        f.write(format_xyz(tuples, counts))
+        f.write(g.ctx.edges_text() if res is None else format_xyz(*res))
     if cluster:
         if os.path.isfile("%s.mcl" % oname):
             print("# the mcl has been ran", file=out)
@@ -212,12 +240,12 @@ def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_
             os.system("mcl %s --abc -I 1.5 -te 8 -o %s.mcl -q x -V all" % (oname, oname))
     with open(oname + ".mcl", "r") as f:
         mcl_text = f.read()
-    keys, vals, ids = host.label_table(mcl_text, tuples)     # :1918-1944
-    g.ctx.set_labels(keys, vals, ids)
+    mk, mv, mi, nxt = host.mcl_labels(mcl_text)              # :1918-1929
+    g.ctx.labels_from_edges(None if res is None else res[0], mk, mv, mi, nxt)     # :1932-1944
     flags = host.plan_rows(g.seq_len, g.shape, g.buf, int(Ns))
-    rows = g.ctx.rows(flags, bool(rc))
+    g.ctx.rows_count(flags, bool(rc))
     names = [bytes(g.buf[int(hs) + 1:int(hs) + int(hl)]) for hs, hl in zip(g.hdr_start, g.hdr_len)]
-    text = format_rows(rows, names)                   # print('%s\t%d\t%d\t%s\t%d') (:1946-1949)
+    text = g.ctx.rows_text(names)                     # print('%s\t%d\t%d\t%s\t%d') (:1946-1949)
     if text:
         if hasattr(out, "buffer"):
             out.flush()
@@ -225,7 +253,7 @@ def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_
             out.buffer.flush()
         else:
             out.write(text.decode())
-    return LabelTable(keys, vals, ids)
+    return LabelTable(loader=g.ctx.labels)
 
 
 # ---------------------------------------------------------------------- CLI

@@ -116,3 +116,63 @@ def test_c2_pipeline_vs_oracle_digest(tmp_path):
     rows = [ln for ln in out.getvalue().split("\n") if ln.count("\t") == 4]
     assert len(rows) == dg["n_rows"]
     assert text_digest("".join(x + "\n" for x in rows)) == dg["rows_sha256"]
+
+
+class _Out:
+    """stdout stand-in: `#` lines through write(), row text through .buffer."""
+
+    def __init__(self):
+        import io
+        self.buffer = io.BytesIO()
+        self.lines = []
+
+    def write(self, s):
+        self.lines.append(s)
+        self.buffer.write(s.encode())
+
+    def flush(self):
+        pass
+
+
+@pytest.mark.parametrize("name", ["c3a_c2", "c3a_c3"])
+def test_c3_cli_region_table_vs_oracle_digest(tmp_path, name):
+    """The whole CLI (kmer.entry_point: dBG, `<in>_db.npz`, rdBG, edges, `.xyz`,
+    labels from an empty `.mcl`, region rows) on C3 batch A at -c 2 and -c 3,
+    against the oracle's digests of the `.xyz` text and the region rows
+    (seq2graph :1853-1951, rdbg_edge_weight :1446-1518, seq2path_jit_
+    :1523-1573 on 100 records and 1.93 M rdBG keys).  The stage times the CLI
+    prints go to $PG_TIMING_LOG when set."""
+    import json
+    import time
+    from pangenome_amd import kmer
+    dg = load_digest(name)
+    assert dg is not None, "tests/golden/scale/%s.json missing (make_scale_digests.py)" % name
+    fasta = _input("c3a")
+    assert len(fasta) == dg["fasta_bytes"]
+    q = tmp_path / "c3.fa"
+    q.write_bytes(fasta)
+    (tmp_path / "c3.fa_rdbg_weight.xyz.mcl").write_text("")
+    out = _Out()
+    t0 = time.time()
+    kmer.entry_point(["kmer_numba.py", "-i", str(q), "-k", "27", "-c", str(dg["c"])], out=out)
+    wall = time.time() - t0
+    text = out.buffer.getvalue()
+    lines = text.split(b"\n")
+    rows = [ln for ln in lines if ln.count(b"\t") == 4]
+    assert len(rows) == dg["n_rows"]
+    assert text_digest(b"".join(x + b"\n" for x in rows)) == dg["rows_sha256"]
+    xyz = (tmp_path / "c3.fa_rdbg_weight.xyz").read_bytes()
+    assert xyz.count(b"\n") == dg["n_edges"]
+    assert text_digest(xyz) == dg["xyz_sha256"]
+    # stage times: each "# finished in X seconds" follows its stage's name
+    stages, cur = {}, None
+    for ln in lines:
+        if ln.startswith(b"# finished in"):
+            stages[cur] = float(ln.split()[3])
+        elif ln.startswith(b"#"):
+            cur = ln[2:].decode()
+    log = os.environ.get("PG_TIMING_LOG")
+    if log:
+        with open(log, "a") as f:
+            f.write(json.dumps({"test": name, "stages_s": stages, "cli_wall_s": round(wall, 3),
+                                "n_edges": dg["n_edges"], "n_rows": dg["n_rows"]}) + "\n")
