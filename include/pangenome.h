@@ -120,10 +120,10 @@ int pg_build_rdbg(pg_ctx* ctx, uint64_t* n_rdbg, pg_stats* stats);
  * pg_build_dbg + pg_build_rdbg. */
 int pg_build(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0, uint64_t* n_rdbg, pg_stats* stats);
 
-/* dump()'s keys/values (kmer_numba.py:243-261) of the dBG, unordered.
- * keys == NULL: only *n is set. */
+/* dump()'s keys/values (kmer_numba.py:243-261) of the dBG, sorted by key
+ * (on the device).  keys == NULL: only *n is set. */
 int pg_dbg_export(pg_ctx* ctx, uint64_t* keys, uint16_t* masks, uint64_t cap, uint64_t* n);
-/* rdBG keys, unordered. keys == NULL: only *n is set. */
+/* rdBG keys, sorted. keys == NULL: only *n is set. */
 int pg_rdbg_export(pg_ctx* ctx, uint64_t* keys, uint64_t cap, uint64_t* n);
 
 /* ---- npz persistence: dump() / load_on_disk() (kmer_numba.py:243-335).

@@ -249,15 +249,14 @@ class Context:
         keys = np.empty(n.value, np.uint64)
         masks = np.empty(n.value, np.uint16)
         check(self.lib.pg_dbg_export(self.h, ptr(keys), ptr(masks), n.value, C.byref(n)), "pg_dbg_export")
-        o = np.argsort(keys, kind="stable")
-        return keys[o], masks[o]
+        return keys, masks                        # (sorted by key on the device)
 
     def rdbg(self):
         n = C.c_uint64()
         check(self.lib.pg_rdbg_export(self.h, None, 0, C.byref(n)), "pg_rdbg_export")
         keys = np.empty(n.value, np.uint64)
         check(self.lib.pg_rdbg_export(self.h, ptr(keys), n.value, C.byref(n)), "pg_rdbg_export")
-        return np.sort(keys)
+        return keys                               # (sorted on the device)
 
     # ----------------------------------------------------- npz persistence
     def dbg_dump(self, capacity: int = 0):

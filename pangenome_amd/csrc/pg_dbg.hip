@@ -35,6 +35,8 @@
 #include <cstdlib>
 #include <cstring>
 
+#include <rocprim/rocprim.hpp>
+
 #include "pg_internal.h"
 
 // Development experiments (tools/exp_build.sh builds variants with
@@ -1874,8 +1876,21 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap) {
   }
   const uint64_t total = n + (c.sentinel ? 1 : 0);
   if (h_keys && cap >= total) {
-    PG_HIP(hipMemcpyAsync(h_keys, keys.p, 8 * n, hipMemcpyDeviceToHost, c.stream));
-    PG_HIP(hipMemcpyAsync(h_masks, masks.p, 2 * n, hipMemcpyDeviceToHost, c.stream));
+    // sorted by key on the device (the sentinel, 2^64 - 1, last)
+    DevBuf k2, m2, tmp;
+    k2.reserve(8 * (n + 1));
+    m2.reserve(2 * (n + 1));
+    size_t bytes = 0;
+    PG_HIP(rocprim::radix_sort_pairs(nullptr, bytes, keys.as<unsigned long long>(), k2.as<unsigned long long>(),
+                                     masks.as<unsigned short>(), m2.as<unsigned short>(), (size_t)n, 0, c.kb,
+                                     c.stream));
+    tmp.reserve(bytes + 16);
+    bytes = tmp.cap;
+    PG_HIP(rocprim::radix_sort_pairs(tmp.p, bytes, keys.as<unsigned long long>(), k2.as<unsigned long long>(),
+                                     masks.as<unsigned short>(), m2.as<unsigned short>(), (size_t)n, 0, c.kb,
+                                     c.stream));
+    PG_HIP(hipMemcpyAsync(h_keys, k2.p, 8 * n, hipMemcpyDeviceToHost, c.stream));
+    PG_HIP(hipMemcpyAsync(h_masks, m2.p, 2 * n, hipMemcpyDeviceToHost, c.stream));
     c.sync();
     if (c.sentinel) { h_keys[n] = SENTINEL; h_masks[n] = 32; }
   }
@@ -1900,7 +1915,17 @@ uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap) {
       hipLaunchKernelGGL(k_gather_segs, dim3((unsigned)nseg), dim3(256), 0, c.stream, c.rseg.as<unsigned long long>(),
                          c.rseg_cap, d_off.as<unsigned long long>(), out.as<unsigned long long>());
       PG_HIP(hipGetLastError());
-      PG_HIP(hipMemcpyAsync(h_keys, out.p, 8 * n, hipMemcpyDeviceToHost, c.stream));
+      DevBuf k2, tmp;                                   // sorted on the device
+      k2.reserve(8 * n);
+      size_t bytes = 0;
+      PG_HIP(rocprim::radix_sort_keys(nullptr, bytes, out.as<unsigned long long>(), k2.as<unsigned long long>(),
+                                      (size_t)n, 0, c.kb, c.stream));
+      tmp.reserve(bytes + 16);
+      bytes = tmp.cap;
+      PG_HIP(rocprim::radix_sort_keys(tmp.p, bytes, out.as<unsigned long long>(), k2.as<unsigned long long>(),
+                                      (size_t)n, 0, c.kb, c.stream));
+      PG_HIP(hipMemcpyAsync(h_keys, k2.p, 8 * n, hipMemcpyDeviceToHost, c.stream));
+      c.sync();
     }
     c.sync();
     d_off.release();

@@ -113,6 +113,51 @@ def pangenome(n_genomes: int, genome_len: int, snp: float = 1e-3, indel: float =
     return b"".join(parts)
 
 
+_BASE = {}
+
+
+def _genome_fasta(args) -> bytes:
+    """One genome of pangenome() as FASTA bytes (a pool worker; the base
+    genome is made once per worker)."""
+    gi, genome_len, snp, indel, seed, width = args
+    key = (genome_len, seed)
+    if key not in _BASE:
+        _BASE.clear()
+        _BASE[key] = base_genome(genome_len, seed)
+    return to_fasta_lines(b"g%d" % gi, variant(_BASE[key], gi, snp, indel, seed), width)
+
+
+def write_pangenome(path: str, n_genomes: int, genome_len: int, snp: float = 1e-3, indel: float = 1e-4,
+                    seed: int = DEFAULT_SEED, first_index: int = 0, width: int = 60, workers: int = 8,
+                    progress=None) -> int:
+    """pangenome(...) (one record per genome) streamed to `path` by a pool of
+    `workers` spawned processes, genome by genome in order, so inputs of
+    several GB (C4: 5.08 GB) are never held whole.  Byte-identical to
+    pangenome(...).  Returns the bytes written."""
+    import multiprocessing
+    jobs = [(gi, genome_len, snp, indel, seed, width) for gi in range(first_index, first_index + n_genomes)]
+    n = 0
+    with open(path, "wb") as f:
+        if workers <= 1:
+            it = map(_genome_fasta, jobs)
+            pool = None
+        else:
+            # spawn: the caller may already hold a GPU context, which a forked child must not inherit
+            pool = multiprocessing.get_context("spawn").Pool(workers)
+            it = pool.imap(_genome_fasta, jobs, chunksize=2)
+        try:
+            for i, b in enumerate(it):
+                f.write(b)
+                n += len(b)
+                if progress and (i + 1) % 100 == 0:
+                    progress(i + 1, n)
+        finally:
+            if pool is not None:
+                pool.close()
+                pool.join()
+    return n
+
+
 # Named workloads of BASELINE.json "configs" (SURVEY.md §8(d) table).
 CONFIGS = {
     # C2: synthetic stand-in for E. coli K-12 MG1655 (4,641,652 bp) with 7 inserted
@@ -163,3 +208,18 @@ def ecoli_like(length: int = 4_641_652, seed: int = DEFAULT_SEED, repeats: int =
         prev = c
     parts.append(g[prev:])
     return to_fasta_lines(b"NC_000913.3 synthetic E. coli K-12 MG1655 stand-in", np.concatenate(parts))
+
+
+if __name__ == "__main__":
+    # python -m pangenome_amd.synth c3|c4|popN OUT [workers]: write a workload's FASTA
+    import sys
+    import time
+    name, out = sys.argv[1], sys.argv[2]
+    workers = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    n = {"c3": 100, "c4": 1000}.get(name) or int(name[3:]) * 100
+    t0 = time.time()
+    size = write_pangenome(out, n, 5_000_000, workers=workers,
+                           progress=lambda i, b: print("%s: %d genomes, %.2f GB, %.0f s" % (name, i, b / 1e9,
+                                                                                            time.time() - t0),
+                                                       flush=True))
+    print("%s: wrote %d bytes to %s in %.0f s" % (name, size, out, time.time() - t0), flush=True)

@@ -176,3 +176,44 @@ def test_c3_cli_region_table_vs_oracle_digest(tmp_path, name):
         with open(log, "a") as f:
             f.write(json.dumps({"test": name, "stages_s": stages, "cli_wall_s": round(wall, 3),
                                 "n_edges": dg["n_edges"], "n_rows": dg["n_rows"]}) + "\n")
+
+
+def test_c4_past_4gib_vs_oracle_digest(tmp_path):
+    """C4 (1000 x 5 Mbp, 5.08 GB of FASTA: byte offsets, class-stream offsets
+    and record regions past 2^32) on one MI355X through the CLI's dBG pass
+    (kmer.seq2rdbg: the file memory-mapped, staged through the pinned ring,
+    pg_build_host), then the rdBG; n_dbg / n_rdbg and the SHA-256 of the sorted
+    dBG and rdBG against the oracle's digest (tests/golden/scale/c4.json, 31
+    min of one core in the build container).  The FASTA is written by
+    `python -m pangenome_amd.synth c4` (spawned workers, ~20 s), or taken from
+    $PG_C4_FASTA."""
+    import subprocess
+    import sys
+    import time
+    from pangenome_amd import kmer
+    dg = load_digest("c4")
+    assert dg is not None, "tests/golden/scale/c4.json missing (make_scale_digests.py c4)"
+    path = os.environ.get("PG_C4_FASTA")
+    if not path or not os.path.isfile(path):
+        path = str(tmp_path / "c4.fa")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        subprocess.run([sys.executable, "-m", "pangenome_amd.synth", "c4", path, "16"], cwd=root, check=True,
+                       timeout=600)
+    assert os.path.getsize(path) == dg["fasta_bytes"] > 2 ** 32
+    t0 = time.time()
+    g = kmer.seq2rdbg(path, 27, 5, 2 ** 63, brkpt="", chunk=2 ** 33, rc=True)
+    build_s = time.time() - t0
+    assert g.stats.n_bases == dg["n_bases"]
+    assert (g.stats.n_dbg, g.stats.n_rdbg) == (dg["n_dbg"], dg["n_rdbg"])
+    keys, masks = g.dbg_items()
+    assert dbg_digest(keys, masks) == dg["dbg_sha256"]
+    del keys, masks
+    kmer.dbg2rdbg(g)
+    assert rdbg_digest(g.rdbg_keys()) == dg["rdbg_sha256"]
+    log = os.environ.get("PG_TIMING_LOG")
+    if log:
+        import json
+        with open(log, "a") as f:
+            f.write(json.dumps({"test": "c4", "seq2rdbg_s": round(build_s, 3), "n_dbg": dg["n_dbg"],
+                                "n_rdbg": dg["n_rdbg"], "n_records_a": g.stats.n_records_a}) + "\n")
+    g.ctx.close()
