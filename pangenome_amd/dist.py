@@ -463,9 +463,11 @@ class DistRun:
         self.device, self.dev_index = device, dev_index
         self.rank, self.world = comm.rank, comm.world
         self.out = out or sys.stdout
-        self.buf = np.memmap(qry, mode="r", dtype=np.uint8) if os.path.getsize(qry) else np.zeros(0, np.uint8)
+        from .kmer import populate, seq2bytes
+        self.buf = seq2bytes(qry, populate=False)        # (the shard's bytes are populated once it is known)
         self.bounds = shard_bounds(self.buf, self.world)
         lo, hi = self.bounds[self.rank], self.bounds[self.rank + 1]
+        populate(self.buf, lo, hi)
         self.data = np.ascontiguousarray(self.buf[lo:hi])
         meta = self.sh.load(self.data)
         metas = comm.allgather_obj({k_: np.asarray(v, np.int64) for k_, v in meta.items()})
