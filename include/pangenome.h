@@ -236,6 +236,11 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * of an upload are smaller (2, 4, 8 ... MiB). */
 #define PG_TUNE_STAGE_PIECE 6
 #define PG_TUNE_STAGE_SLOTS 7
+/* PG_TUNE_HOST_REGISTER: 1 (default) = a pageable input's page-aligned
+ * chunks are registered (hipHostRegister, read-only) for the duration of the
+ * upload and DMA'd directly, falling back to the staging ring for the rest
+ * when a chunk cannot be; 0 = staging ring only. */
+#define PG_TUNE_HOST_REGISTER 8
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Timings and counters of the last build (see pg_stats). */

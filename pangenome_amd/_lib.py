@@ -22,6 +22,7 @@ PG_TUNE_H2D_CHUNK = 4
 PG_TUNE_HOST_THREADS = 5
 PG_TUNE_STAGE_PIECE = 6
 PG_TUNE_STAGE_SLOTS = 7
+PG_TUNE_HOST_REGISTER = 8
 
 
 class PgStats(C.Structure):

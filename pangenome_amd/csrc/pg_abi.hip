@@ -291,6 +291,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || (value && value < 4096)) throw pg::Error(PG_EINVAL, "pg_tune: staging piece must be 0 or >= 4096");
         x->c.stage_piece = value ? (uint64_t)value : (32ull << 20);
         break;
+      case PG_TUNE_HOST_REGISTER:
+        if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: host register must be 0 or 1");
+        x->c.host_register = (int)value;
+        break;
       case PG_TUNE_STAGE_SLOTS:
         if (value < 0 || value == 1 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: staging slots must be 0 or 2..8");
         x->c.stage_slots = value ? (uint64_t)value : 4;

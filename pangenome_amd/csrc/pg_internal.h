@@ -111,6 +111,7 @@ struct Ctx {
   int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
   uint64_t stage_piece = 32ull << 20;  // pg_tune: bytes per staging-ring slot (one DMA)
   uint64_t stage_slots = 4;       // pg_tune: staging-ring slots (2..8)
+  int host_register = 1;          // pg_tune: register pageable chunks and DMA them (0: staging ring only)
   HostPool* pool = nullptr;       // staging ring threads (created on the first pageable upload)
   PinBuf stage_pin;               // staging ring slots
   int bb_shift = 0;               // pg_tune: table bits below the sized ones (tests of the overflow paths)

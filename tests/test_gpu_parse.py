@@ -227,16 +227,17 @@ def test_build_host_streamed(case):
         ctx.close()
 
 
-@pytest.mark.parametrize("threads", [1, 3, 0])
-def test_build_host_mmap_and_pinned(tmp_path, threads):
+@pytest.mark.parametrize("threads,register", [(1, 0), (3, 0), (0, 0), (0, 1)])
+def test_build_host_mmap_and_pinned(tmp_path, threads, register):
     """The input kinds pg_build_host meets: a read-only np.memmap of the file
     (kmer.seq2bytes, what the CLI passes: through the pinned staging ring,
     40+ chunks so the ring's slots and the 16 chunk events are reused many
     times), a pinned torch buffer (DMA'd directly) and a pinned buffer at an
-    offset; all against the oracle, with 1, 3 and the default staging threads."""
+    offset; all against the oracle, with 1, 3 and the default staging threads,
+    and with the mmap's chunks registered and DMA'd directly (the default)."""
     import torch
     from pangenome_amd import kmer, synth
-    from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK, PG_TUNE_HOST_THREADS
+    from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK, PG_TUNE_HOST_REGISTER, PG_TUNE_HOST_THREADS
     buf = synth.pangenome(10, 120_000, snp=2e-3, indel=2e-4, seed=21)
     q = tmp_path / "in.fa"
     q.write_bytes(buf)
@@ -249,6 +250,7 @@ def test_build_host_mmap_and_pinned(tmp_path, threads):
     ctx = Context(27)
     ctx.tune(PG_TUNE_H2D_CHUNK, 16 * 1024 * 2)
     ctx.tune(PG_TUNE_HOST_THREADS, threads)
+    ctx.tune(PG_TUNE_HOST_REGISTER, register)
     for src in ("mmap", "pinned", "mmap", "pinned_offset"):
         if src == "mmap":
             st = ctx.build_host(mm, True)

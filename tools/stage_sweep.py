@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def main():
     from scale_util import make_input
     from pangenome_amd import kmer
-    from pangenome_amd._lib import Context, PG_TUNE_HOST_THREADS, PG_TUNE_STAGE_PIECE, PG_TUNE_STAGE_SLOTS
+    from pangenome_amd._lib import Context, PG_TUNE_HOST_REGISTER, PG_TUNE_HOST_THREADS, PG_TUNE_STAGE_PIECE, PG_TUNE_STAGE_SLOTS
     fa = make_input("c3a")
     d = tempfile.mkdtemp()
     q = os.path.join(d, "c3.fa")
@@ -26,13 +26,17 @@ def main():
     mm = kmer.seq2bytes(q)
     ctx = Context(27)
     res = []
-    combos = list(itertools.product((8, 16, 32, 64), (4, 6, 8), (4, 8, 12)))
+    combos = [c + (0,) for c in itertools.product((8, 16, 32, 64), (4, 6, 8), (4, 8, 12))]
     if len(sys.argv) > 1:
         combos = [tuple(int(x) for x in a.split(",")) for a in sys.argv[1:]]
-    for piece, slots, thr in combos:
+    for piece, slots, thr, reg in combos:
         ctx.tune(PG_TUNE_STAGE_PIECE, piece << 20)
         ctx.tune(PG_TUNE_STAGE_SLOTS, min(slots, 8))
         ctx.tune(PG_TUNE_HOST_THREADS, thr)
+        ctx.tune(PG_TUNE_HOST_REGISTER, reg)
+        t = time.perf_counter()
+        ctx.build_host(mm, True)
+        first = time.perf_counter() - t
         for _ in range(2):
             ctx.build_host(mm, True)
         ts = []
@@ -45,7 +49,7 @@ def main():
             t = time.perf_counter()
             ctx.set_fasta(mm)
             us.append(time.perf_counter() - t)
-        r = {"piece_mib": piece, "slots": slots, "threads": thr, "window_ms_mean": round(1e3 * sum(ts) / len(ts), 3),
+        r = {"piece_mib": piece, "slots": slots, "threads": thr, "register": reg, "first_ms": round(1e3 * first, 3), "window_ms_mean": round(1e3 * sum(ts) / len(ts), 3),
              "window_ms_min": round(1e3 * min(ts), 3), "upload_ms_min": round(1e3 * min(us), 3)}
         res.append(r)
         print(json.dumps(r), flush=True)
