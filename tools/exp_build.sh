@@ -6,7 +6,7 @@ set -eu
 cd "$(dirname "$0")/../pangenome_amd/csrc"
 for n in "$@"; do
   d=build_e$n; mkdir -p $d
-  for f in pg_parse pg_dbg pg_walk pg_persist pg_abi; do
+  for f in pg_stage pg_parse pg_dbg pg_walk pg_persist pg_abi; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -DPG_EXP_BITS=$n -c -o $d/$f.o $f.hip &
   done
   wait
