@@ -241,7 +241,16 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * upload and DMA'd directly, falling back to the staging ring for the rest
  * when a chunk cannot be; 0 = staging ring only. */
 #define PG_TUNE_HOST_REGISTER 8
+/* PG_TUNE_DEVICE_CAP: the most device bytes the library's buffers may hold
+ * in this process, over all contexts (0 = no cap): an allocation past it
+ * fails with PG_ENOMEM.  Setting it also restarts pg_device_bytes' peak.
+ * For tests of a path's memory budget at a scaled-down size. */
+#define PG_TUNE_DEVICE_CAP 9
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
+
+/* Device bytes the library's buffers hold in this process now (peak == 0)
+ * or at most since the last PG_TUNE_DEVICE_CAP (peak != 0). */
+uint64_t pg_device_bytes(int peak);
 
 /* Timings and counters of the last build (see pg_stats). */
 int pg_get_stats(const pg_ctx* ctx, pg_stats* stats);

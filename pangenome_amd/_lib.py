@@ -23,6 +23,7 @@ PG_TUNE_HOST_THREADS = 5
 PG_TUNE_STAGE_PIECE = 6
 PG_TUNE_STAGE_SLOTS = 7
 PG_TUNE_HOST_REGISTER = 8
+PG_TUNE_DEVICE_CAP = 9
 
 
 class PgStats(C.Structure):
@@ -76,6 +77,7 @@ SIGNATURES = {
     "pg_dbg_dump": (C.c_int, [_P, _U64P, _P, _P, _P, _U64P]),
     "pg_dbg_load": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_oakht_capacity": (C.c_uint64, [C.c_uint64]),
+    "pg_device_bytes": (C.c_uint64, [C.c_int]),
     "pg_format_xyz": (C.c_uint64, [_P, _P, C.c_uint64, _P, C.c_uint64]),
     "pg_format_rows": (C.c_uint64, [_P, C.c_uint64, _P, _P, _P, C.c_uint64]),
 }

@@ -295,6 +295,11 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: host register must be 0 or 1");
         x->c.host_register = (int)value;
         break;
+      case PG_TUNE_DEVICE_CAP:
+        if (value < 0) throw pg::Error(PG_EINVAL, "pg_tune: device cap must be >= 0");
+        pg::DevBytes::cap().store((uint64_t)value);
+        pg::DevBytes::peak().store(pg::DevBytes::cur().load());
+        break;
       case PG_TUNE_STAGE_SLOTS:
         if (value < 0 || value == 1 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: staging slots must be 0 or 2..8");
         x->c.stage_slots = value ? (uint64_t)value : 4;
@@ -303,6 +308,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         throw pg::Error(PG_EINVAL, "pg_tune: unknown parameter " + std::to_string(what));
     }
   });
+}
+
+uint64_t pg_device_bytes(int peak) {
+  return peak ? pg::DevBytes::peak().load() : pg::DevBytes::cur().load();
 }
 
 int pg_get_stats(const pg_ctx* x, pg_stats* stats) {

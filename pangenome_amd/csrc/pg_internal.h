@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdint>
 #include <cstdlib>
@@ -29,22 +30,47 @@ struct Error : std::runtime_error {
       throw ::pg::Error(-5, std::string(#x) + ": " + hipGetErrorString(e_));            \
   } while (0)
 
+// Device bytes held by every DevBuf of the process, their peak, and an
+// optional cap (pg_tune PG_TUNE_DEVICE_CAP: tests of the memory budget of a
+// path at a scaled-down size; 0 = none).
+struct DevBytes {
+  static std::atomic<uint64_t>& cur() { static std::atomic<uint64_t> v{0}; return v; }
+  static std::atomic<uint64_t>& peak() { static std::atomic<uint64_t> v{0}; return v; }
+  static std::atomic<uint64_t>& cap() { static std::atomic<uint64_t> v{0}; return v; }
+  static void add(uint64_t b) {
+    const uint64_t now = cur().fetch_add(b) + b;
+    uint64_t pk = peak().load();
+    while (now > pk && !peak().compare_exchange_weak(pk, now)) {}
+  }
+};
+
 // A growable device buffer (never shrinks; reused across calls so the steady
 // state does no hipMalloc).
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }                // (function-local scratch buffers free themselves)
   void reserve(size_t bytes) {
     if (bytes <= cap) return;
-    if (p) PG_HIP(hipFree(p));
-    p = nullptr;
+    release();
     size_t nb = bytes + bytes / 8 + 256;
+    const uint64_t lim = DevBytes::cap().load();
+    if (lim && DevBytes::cur().load() + nb > lim)
+      throw Error(-12, "device memory cap: " + std::to_string(DevBytes::cur().load() + nb) + " > " +
+                           std::to_string(lim) + " bytes");
     PG_HIP(hipMalloc(&p, nb));
     cap = nb;
+    DevBytes::add(nb);
   }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipFree(p);
+      DevBytes::cur().fetch_sub(cap);
+    }
     p = nullptr;
     cap = 0;
   }

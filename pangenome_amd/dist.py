@@ -70,6 +70,9 @@ SENTINEL = 2 ** 64 - 1
 # its exchange in chunks of this size (exchange_stream; C5: 3.75 Gbp per GPU
 # in 4 chunks).  C3 / C4 shards (0.5-0.63 Gbp) exchange whole.
 STREAM_BASES = 1 << 30
+# The `<in>_db.npz` dump is built on rank 0 from every rank's (key, mask,
+# count) entries: at most this many of them (_grab_counts).
+DUMP_MAX_ENTRIES = 1 << 31
 
 
 def _is_cuda(device) -> bool:
@@ -173,33 +176,74 @@ def stream_chunks(flags, seq_len, limit: int) -> list:
     return res
 
 
+def _sub_of(recv, nsub: int):
+    """Sub-log of each received 16-byte record: a hash of its key word (a
+    different one from the owner hash, so an owner's entries spread evenly)."""
+    import torch
+    golden = -7046029254386353131                     # 0x9E3779B97F4A7C15 as int64 (wrapping multiply)
+    return ((recv[:, 0] * golden) >> 20) & (nsub - 1)
+
+
+def _free_device_bytes(device) -> int:
+    import torch
+    if _is_cuda(device):
+        return int(torch.cuda.mem_get_info(device)[0])
+    return 1 << 36
+
+
 def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_records: int, rc0: bool, extra: int = 0,
-                    staged=None, group=None, on_chunk=None, compact_at: int = 1 << 26):
+                    staged=None, group=None, on_chunk=None, compact_at=None, subparts=None):
     """The streaming exchange of SURVEY §8(e) for shards whose whole local
     table does not fit beside the owner partition (C5: 3.75 Gbp per GPU).
 
     Per chunk of records (stream_chunks): the local OR-table of the chunk
     (`shard.build`, K1 already done for the whole shard), its entries to their
-    owners with one all-to-all (`_route`), appended to the owner's record log
-    on the device.  When the log has doubled since its last compaction (and
-    holds at least `compact_at` records) the owner OR-merges it and
-    re-exports the merged table as the new log (pg_dbg_merge, then
-    pg_dbg_partition into one run), so the log stays within ~2x the owner's
-    distinct entries.  After the last chunk the log is merged once and the
-    rdBG rule runs on the owner partition, exactly as exchange_and_reduce.
-    Every rank runs the same number of rounds (the maximum chunk count; a
-    rank out of records builds an empty chunk).  `staged` (rank 0's -r
-    checkpoint slots) goes into the first chunk only; `extra` (the n<k empty
-    records) too.  `on_chunk()` runs after each chunk's build (the dump
-    gathers its occurrence counts there).  Returns (n_dbg_total,
-    n_rdbg_total, n_rdbg_local, bytes_sent, rounds)."""
+    owners with one all-to-all (`_route`).  The owner keeps what it receives
+    in `subparts` sub-logs by a hash of the key (default: the round count,
+    rounded up to a power of two), so that no step ever handles the whole
+    log at once: a compaction OR-merges ONE sub-log (pg_dbg_merge, 1/P of the
+    owner's entries, within the stage A-C buffers the chunk builds already
+    hold) and re-exports it in place (pg_dbg_partition into one run); it runs
+    on a sub-log that has doubled since its last compaction once the whole log
+    holds `compact_at` records (default: a quarter of the device memory free
+    when the exchange starts, at 16 B per record).  After the last chunk each
+    sub-log is merged once, the rdBG rule applied to it and its rdBG keys
+    kept; the owner's counts are the sums.  Every rank runs the same number of
+    rounds (the maximum chunk count; a rank out of records builds an empty
+    chunk).  `staged` (rank 0's -r checkpoint slots) goes into the first chunk
+    only; `extra` (the n<k empty records) too.  `on_chunk()` runs after each
+    chunk's build (the dump gathers its occurrence counts there).  Returns
+    (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent, rounds, the owner's
+    rdBG keys)."""
     import torch
     import torch.distributed as dist
     _, comm = _comm_device(device, group)
     nch = torch.tensor([len(chunks)], dtype=torch.int64, device=comm)
     dist.all_reduce(nch, op=dist.ReduceOp.MAX, group=group)
     rounds = max(1, int(nch.item()))
-    log, logn, base, sentinel, sent = [], 0, 0, False, 0
+    P = 1
+    while P < min(64, subparts or rounds):
+        P *= 2
+    if compact_at is None:
+        compact_at = max(1 << 20, _free_device_bytes(device) // 4 // 16)
+    logs = [[] for _ in range(P)]
+    logn, base = [0] * P, [0] * P
+    sentinel, sent = False, 0
+
+    def compact(p):
+        cat = torch.cat(logs[p]) if len(logs[p]) > 1 else logs[p][0]
+        logs[p] = []                                   # (the pieces go as soon as they are merged)
+        if _is_cuda(device):
+            torch.cuda.synchronize(device)
+        shard.merge(cat.data_ptr(), int(cat.shape[0]), False)
+        del cat
+        m = int(shard.partition(1)[0])
+        out = torch.empty((max(m, 1), 2), dtype=torch.int64, device=device)
+        if m:
+            shard.partition(1, out.data_ptr(), m)
+        logs[p] = [out[:m]] if m else []
+        logn[p] = base[p] = m
+
     for i in range(rounds):
         if staged is not None and i < 2:
             if i == 0:
@@ -212,27 +256,48 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
             on_chunk()
         recv, s, _ = _route(shard, world, device, group)
         sent += s
-        if recv.shape[0]:
-            log.append(recv)
-            logn += int(recv.shape[0])
-        if logn >= compact_at and logn >= 2 * base and len(log) > 1:
-            cat = torch.cat(log)
-            if _is_cuda(device):
-                torch.cuda.synchronize(device)
-            shard.merge(cat.data_ptr(), logn, False)
-            m = int(shard.partition(1)[0])
-            out = torch.empty((max(m, 1), 2), dtype=torch.int64, device=device)
-            if m:
-                shard.partition(1, out.data_ptr(), m)
-            del cat
-            log, logn, base = ([out[:m]] if m else []), m, m
-    if len(log) > 1:
-        allr = torch.cat(log)
-    elif log:
-        allr = log[0]
-    else:
-        allr = torch.empty((0, 2), dtype=torch.int64, device=device)
-    return _owner_reduce(shard, allr, rank, device, sentinel, group) + (sent, rounds)
+        n = int(recv.shape[0])
+        if n:
+            if P == 1:
+                pieces, cnt = [recv], [n]
+            else:
+                sub = _sub_of(recv, P)
+                cnt = torch.bincount(sub, minlength=P).tolist()
+                pieces = torch.split(recv[torch.argsort(sub, stable=True)], cnt)
+                del sub
+            for p in range(P):
+                if cnt[p]:
+                    logs[p].append(pieces[p])
+                    logn[p] += int(cnt[p])
+            del recv, pieces
+        total = sum(logn)
+        if total >= compact_at:
+            for p in sorted(range(P), key=lambda q: -logn[q]):
+                if logn[p] >= 2 * base[p] and len(logs[p]) > 1:
+                    compact(p)
+    # the n<k sentinel key belongs to one owner: rank 0 (sub-log 0)
+    flag = torch.tensor([1 if sentinel else 0], dtype=torch.int64, device=comm)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    sent_global = bool(flag.item())
+    n_dbg_loc = n_rdbg_loc = 0
+    keys = []
+    for p in range(P):
+        cat = (torch.cat(logs[p]) if len(logs[p]) > 1 else logs[p][0]) if logs[p] else None
+        logs[p] = []
+        if _is_cuda(device):
+            torch.cuda.synchronize(device)
+        n = 0 if cat is None else int(cat.shape[0])
+        shard.merge(cat.data_ptr() if n else 0, n, sentinel=sent_global and rank == 0 and p == 0)
+        del cat
+        st = shard.build_rdbg()
+        n_dbg_loc += int(st.n_dbg)
+        n_rdbg_loc += int(st.n_rdbg)
+        keys.append(np.ascontiguousarray(shard.owner_rdbg(), dtype=np.uint64))
+    sums = torch.tensor([n_dbg_loc, n_rdbg_loc], dtype=torch.int64, device=comm)
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+    n_dbg, n_rdbg = sums.tolist()
+    own = np.sort(np.concatenate(keys)) if keys else np.zeros(0, np.uint64)
+    return int(n_dbg), int(n_rdbg), n_rdbg_loc, sent, rounds, own
 
 
 # ------------------------------------------------------------------ sharding
@@ -453,10 +518,10 @@ class DistRun:
 
     def __init__(self, qry: str, k: int, shard, comm: Comm, device=None, out=None, dev_index: int = 0,
                  edge_chunk: int = host.CHUNK, dbg_chunk: int = host.CHUNK, stream_bases: int = STREAM_BASES,
-                 compact_at: int = 1 << 26):
+                 compact_at=None):
         self.qry, self.k, self.sh, self.comm = qry, min(max(1, int(k)), 27), shard, comm
         self.stream_bases = int(stream_bases)              # a shard above this streams its exchange
-        self.compact_at = int(compact_at)
+        self.compact_at = None if compact_at is None else int(compact_at)
         self.streamed = None
         self.edge_chunk = int(edge_chunk)                  # seq2graph's checkpoint size (:2073; tests vary it)
         self.dbg_chunk = int(dbg_chunk)                    # seq2rdbg's
@@ -529,10 +594,26 @@ class DistRun:
         return max(int(self.S.local(sl, r).sum()) for r in range(self.world)) if self.world else 0
 
     def _grab_counts(self, parts: list):
-        """This build's occurrence counts, gathered to rank 0 (appended to parts)."""
+        """This build's occurrence counts, gathered to rank 0 (appended to
+        parts) as 11 bytes per entry (key, 12-bit mask as uint16, saturated
+        count as uint8).  rank 0 builds the `<in>_db.npz` table from all of
+        them on its one GPU and in its host memory (the reference's own dump
+        holds 11 B per oakht slot, :251-259), so the gathered entries are
+        capped at DUMP_MAX_ENTRIES: past it the dump fails with a clear error
+        instead of exhausting rank 0 (C5's ~2.2e10 keys would need ~320 GB of
+        slot arrays)."""
+        import torch
         keys, masks, counts = self.sh.counts()
-        got = self.comm.gather_bytes(_pack(keys.astype(np.uint64), masks.astype(np.uint16).astype(np.int64),
-                                           counts.astype(np.int64)))
+        _, dev = _comm_device(self.device, self.comm.group)
+        n = torch.tensor([keys.shape[0]], dtype=torch.int64, device=dev)
+        self.comm.dist.all_reduce(n, op=self.comm.dist.ReduceOp.SUM, group=self.comm.group)
+        self._dump_entries = getattr(self, "_dump_entries", 0) + int(n.item())
+        if self._dump_entries > DUMP_MAX_ENTRIES:
+            raise RuntimeError("<in>_db.npz: %d oakht entries gathered so far exceed the single-rank dump's budget "
+                               "of %d (DUMP_MAX_ENTRIES): the dump of an input this size does not fit one rank"
+                               % (self._dump_entries, DUMP_MAX_ENTRIES))
+        got = self.comm.gather_bytes(_pack(keys.astype(np.uint64), masks.astype(np.uint16),
+                                           np.minimum(counts, 255).astype(np.uint8)))
         if self.rank == 0:
             parts.extend(got)
 
@@ -575,11 +656,10 @@ class DistRun:
         if self.rank == 0:
             ks, ms, cs = [], [], []
             for p in parts:
-                k_, m_, c_ = _unpack(p, (np.uint64, np.int64, np.int64))
+                k_, m_, c_ = _unpack(p, (np.uint64, np.uint16, np.uint8))
                 ks.append(k_); ms.append(m_); cs.append(c_)
-            cap, size, K, V, C = self.sh.dump_global(np.concatenate(ks), np.concatenate(ms).astype(np.uint16),
-                                                     np.minimum(np.concatenate(cs), 255).astype(np.uint8),
-                                                     self.k, self.dev_index)
+            cap, size, K, V, C = self.sh.dump_global(np.concatenate(ks), np.concatenate(ms),
+                                                     np.concatenate(cs), self.k, self.dev_index)
             host.write_db_npz(fn, cap, size, K, V, C, offset=offset)
         self.comm.barrier()
 
@@ -591,10 +671,11 @@ class DistRun:
             return
         if self.streamed is not None:
             n_dbg, n_rdbg = self.streamed[:2]
+            own = self.streamed[5]                          # (the sub-logs' rdBG keys)
         else:
             n_dbg, n_rdbg, _, _ = exchange_and_reduce(self.sh, self.world, self.rank, self.device, self.sentinel,
                                                       self.comm.group)
-        own = np.ascontiguousarray(self.sh.owner_rdbg(), dtype=np.uint64)
+            own = np.ascontiguousarray(self.sh.owner_rdbg(), dtype=np.uint64)
         allk = np.sort(np.concatenate([p.view(np.uint64) for p in self.comm.allgather_bytes(own.view(np.uint8))]))
         if allk.shape[0] != n_rdbg:
             raise RuntimeError("rdBG all-gather: %d keys, owners reported %d" % (allk.shape[0], n_rdbg))
@@ -681,7 +762,7 @@ def reduce_edges(parts):
 
 
 def entry_point(argv, out=None, shard_factory=None, device=None, dev_index: int = 0, edge_chunk: int = host.CHUNK,
-                dbg_chunk: int = host.CHUNK, stream_bases: int = STREAM_BASES, compact_at: int = 1 << 26):
+                dbg_chunk: int = host.CHUNK, stream_bases: int = STREAM_BASES, compact_at=None):
     """kmer.entry_point (:1971-2146) on every rank of an initialised process
     group; rank 0 prints.  `shard_factory(k)` makes the rank's backend
     (default: GpuShard on dev_index)."""

@@ -252,3 +252,61 @@ def test_dist_cli_writes_reference_checkpoints(tmp_path):
     z, ref = np.load(str(q) + "_rdb_brkpt.npz"), np.load(fR.brkpt)
     for a in ("parameters", "keys", "values"):
         assert z[a].tolist() == ref[a].tolist(), a
+
+
+def _budget_rank(rank, world, port, q, fasta, mode, cap):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from pangenome_amd._lib import PG_TUNE_DEVICE_CAP, PangenomeError, load
+    from pangenome_amd.dist import GpuShard, exchange_and_reduce, exchange_stream, stream_chunks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    sh = GpuShard(27, 0)
+    meta = sh.load(np.frombuffer(fasta, np.uint8))
+    R = meta["seq_len"].shape[0]
+    sh.ctx.tune(PG_TUNE_DEVICE_CAP, cap)                   # (restarts the peak)
+    try:
+        if mode == "whole":
+            sentinel = sh.build(np.ones(R, np.uint8), 0, True)
+            res = exchange_and_reduce(sh, world, rank, dev, sentinel)
+            keys = sh.owner_rdbg()
+        else:
+            chunks = stream_chunks(np.ones(R, np.uint8), meta["seq_len"], int(meta["seq_len"][0]))
+            res = exchange_stream(sh, world, rank, dev, chunks, R, True, compact_at=1)
+            keys = res[5]
+        q.put((rank, ("ok", res[0], res[1], np.sort(keys), int(load().pg_device_bytes(1)))))
+    except PangenomeError as e:
+        q.put((rank, ("error", str(e))))
+    finally:
+        sh.ctx.tune(PG_TUNE_DEVICE_CAP, 0)
+        dist.destroy_process_group()
+
+
+def test_streamed_exchange_device_budget(oracle_mod):
+    """ADVICE r2 (the C5 form's memory): the streamed exchange keeps the
+    owner's record log in sub-logs and merges one at a time, so the
+    library's device buffers stay near one chunk's build instead of the whole
+    shard's.  At a scaled-down size (16 x 200 kbp at 1 % SNP, one genome per
+    chunk): both forms give the oracle's dBG / rdBG; the streamed one peaks
+    lower; under a device cap between the two peaks (PG_TUNE_DEVICE_CAP) the
+    streamed run still completes and the whole-shard build fails with
+    PG_ENOMEM."""
+    from pangenome_amd import synth
+    fasta = synth.pangenome(16, 200_000, snp=0.01, indel=1e-3, seed=31)
+    ref = oracle_mod.OracleRun(fasta, 27, 2)
+    n_dbg, rdbg = ref.dbg()[0].shape[0], ref.rdbg()
+    whole = spawn_ranks(1, _budget_rank, (fasta, "whole", 0))[0]
+    strm = spawn_ranks(1, _budget_rank, (fasta, "stream", 0))[0]
+    for r in (whole, strm):
+        assert r[0] == "ok", r
+        assert (r[1], r[2]) == (n_dbg, rdbg.shape[0])
+        assert np.array_equal(r[3], rdbg)
+    assert strm[4] < whole[4], (strm[4], whole[4])
+    cap = (strm[4] + whole[4]) // 2
+    capped = spawn_ranks(1, _budget_rank, (fasta, "stream", cap))[0]
+    assert capped[0] == "ok" and np.array_equal(capped[3], rdbg), capped[:2]
+    failed = spawn_ranks(1, _budget_rank, (fasta, "whole", cap))[0]
+    assert failed[0] == "error" and "device memory cap" in failed[1], failed
