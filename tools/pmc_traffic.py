@@ -9,8 +9,9 @@ tallied at 64 B, MI355X_MICROARCH.md §HBM; profiles/fetch_calib.json), so it
 is doubled for every kernel except k_emit_work, whose reads are per-lane
 16-B loads of scattered segments (a random 16-B load is one 64-B request,
 counted exactly).  WRITE_SIZE reads streaming stores exactly.  Per kernel the
-mean over its dispatches after the first third (warm-up builds) times its
-dispatches per build (4 chunks for the coverage / emission passes)."""
+mean over its dispatches of the last three builds (the HBM-resident ones:
+the cold first build runs the chunked host window) times its dispatches per
+build (3 chunks for the coverage / emission passes)."""
 import collections
 import csv
 import glob
@@ -21,12 +22,12 @@ import sys
 tag = sys.argv[1] if len(sys.argv) > 1 else "tr"
 config = sys.argv[2] if len(sys.argv) > 2 else "c3"
 SPANS = {
-    "k1_parse": r"k_span_sum|ROCPRIM|k_emit\b|k_emit\(|k_records|k_pack_records",
+    "k1_parse": r"k_span_sum|lookback_scan|scan_impl|k_emit\b|k_emit\(|k_records|k_pack_records",
     "k3a_cover_emit": r"k_cover|k_emit_work|k_short_emit",
     "k3b_split": r"k_split",
     "k3c_range": r"k_build_range",
 }
-PER_BUILD = {"k_cover": 4, "k_emit_work": 4}
+PER_BUILD = {"k_cover": 3, "k_emit_work": 3}
 
 
 def load(i):
@@ -40,6 +41,13 @@ def load(i):
     return vals
 
 
+def last_builds(v, per_build, builds=3):
+    """The kernel's dispatches of the last `builds` builds: the bench's
+    HBM-resident builds (its cold first build goes through the chunked host
+    window, whose K1 / stage A dispatches are smaller)."""
+    return v[-builds * per_build:] or v
+
+
 fetch, write = load(1), load(2)
 per_kernel = {}
 for k in set(fetch) | set(write):
@@ -47,7 +55,7 @@ for k in set(fetch) | set(write):
     mult = next((m for n, m in PER_BUILD.items() if n in short), 1)
 
     def mean(v):
-        v = v[len(v) // 3:] or v
+        v = last_builds(v, mult)
         return sum(v) / len(v) if v else 0.0
     f = mean(fetch.get(k, [])) * (1 if "k_emit_work" in short else 2)
     w = mean(write.get(k, []))
@@ -62,5 +70,5 @@ out = {"source": "tools/pmc_kernels.sh (rocprofv3 --pmc FETCH_SIZE, then WRITE_S
        "hbm_bytes_per_build": spans,
        "per_kernel": {k: {kk: (int(vv) if kk != "dispatches_per_build" else vv) for kk, vv in v.items()}
                       for k, v in sorted(per_kernel.items())}}
-json.dump(out, open("profiles/traffic_%s.json" % config, "w"), indent=1)
+json.dump(out, open("gpurun_out/traffic_%s.json" % config, "w"), indent=1)      # (copied into profiles/ by hand)
 print(json.dumps(spans, indent=1))
