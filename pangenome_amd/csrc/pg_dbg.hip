@@ -359,13 +359,15 @@ __device__ __forceinline__ void lds_bytes16(const uint8_t* s, uint32_t idx, uint
     asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
     raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
   }
-  const uint32_t sb = idx & 3u;
+  // (uniform by contract: a scalar branch and an SGPR shift, not four
+  // exec-masked cases; stage A -1.5 %)
+  const uint32_t sb = __builtin_amdgcn_readfirstlane(idx & 3u);
   auto take = [&](auto W) {
     constexpr int w = decltype(W)::value;
 #pragma unroll
     for (int i = 0; i < ND; ++i) out[i] = __builtin_amdgcn_alignbyte(raw[w + i + 1], raw[w + i], sb);
   };
-  switch ((idx >> 2) & 3u) {
+  switch (__builtin_amdgcn_readfirstlane((idx >> 2) & 3u)) {
     case 0: take(std::integral_constant<int, 0>{}); break;
     case 1: take(std::integral_constant<int, 1>{}); break;
     case 2: take(std::integral_constant<int, 2>{}); break;
@@ -434,7 +436,8 @@ __device__ __forceinline__ uint32_t segment_cover(const uint8_t* s_cls, const ui
     if (j >= D.n) break;                                      // block-uniform
     const bool ok = (rel >= D.lo[j]) & (rel <= D.hi[j]);
     uint32_t Rw[NB];
-    lds_bytes16(s_ref, o + (uint32_t)(ok ? D.off[j] : 0), Rw);
+    // (a lane outside the range reads in-bounds bytes at the same alignment)
+    lds_bytes16(s_ref, o + (uint32_t)(ok ? D.off[j] : (D.off[j] & 15)), Rw);
     uint32_t nz = 0;
 #pragma unroll
     for (int i = 0; i < NB; ++i) nz |= (G[i] != Rw[i] ? 1u : 0u) << i;
@@ -1531,6 +1534,11 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
   double capx = 1.15;
   uint64_t ovf_mult = 1;
   double rseg_frac = c.r_ratio > 0 ? std::min(2.0, 1.5 * c.r_ratio + 0.002) : 2.0;
+  // a split level that overflowed: its partitions' exact counts (the cursors
+  // count every record, kept or not) size it on the next attempt, so skewed
+  // keys cost one re-run per level instead of a geometric capacity search
+  std::vector<uint64_t> lv_exact;
+  int lv_exact_bb = -1;
   c.t6.init();
   for (int attempt = 0; attempt < 8; ++attempt) {
     const int fp = std::max(cb, bb - RANGE_BITS);
@@ -1554,7 +1562,9 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
     for (int L = cb; L < fp || lv.empty();) {
       const int S = std::min(7, fp - L);
       const uint64_t pin = 1ull << L, nb = 1ull << S;
-      const uint64_t capo = (uint64_t)((double)maxin / (double)nb * capx) + 64;
+      uint64_t capo = (uint64_t)((double)maxin / (double)nb * capx) + 64;
+      if (lv_exact_bb == bb && lv.size() < lv_exact.size())
+        capo = std::max(capo, lv_exact[lv.size()] + lv_exact[lv.size()] / 16 + 64);
       lv.push_back(Lv{L, S, pin, capo, pin * nsub, std::max<uint64_t>(1, (maxreg + SCH - 1) / SCH), ctr_words});
       ctr_words += CSTRIDE * pin * nb;
       maxin = maxreg = capo;
@@ -1638,7 +1648,29 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
       if (a.bits & F_A_OVER) return false;
     }
     const unsigned bits = hf[4];
-    if (bits & F_SPLIT_OVER) { capx *= 1.5; continue; }
+    static const bool dbg_build = std::getenv("PG_DEBUG_BUILD") != nullptr;
+    if (dbg_build)
+      std::fprintf(stderr, "finish_build attempt %d: total %llu maxreg %llu maxbin %llu bb %d levels %zu rec_max %llu "
+                   "capx %.2f ovf %llu rcap %llu bits %u\n", attempt, (unsigned long long)a.total,
+                   (unsigned long long)a.maxreg, (unsigned long long)a.maxbin, bb, lv.size(),
+                   (unsigned long long)rec_max, capx, (unsigned long long)ovf, (unsigned long long)rcap, bits);
+    if (bits & F_SPLIT_OVER) {
+      std::vector<unsigned long long> ctr(std::max<uint64_t>(ctr_words, 1));
+      PG_HIP(hipMemcpy(ctr.data(), c.ctrS.p, 8 * ctr_words, hipMemcpyDeviceToHost));
+      std::vector<uint64_t> ex(lv.size(), 0);
+      bool over = false;                          // some level's exact count exceeds its capacity
+      for (size_t i = 0; i < lv.size(); ++i) {
+        const uint64_t np = lv[i].pin << lv[i].S;
+        for (uint64_t q = 0; q < np; ++q) ex[i] = std::max<uint64_t>(ex[i], ctr[lv[i].ctr_off + CSTRIDE * q]);
+        over |= ex[i] > lv[i].cap;
+      }
+      if (lv_exact_bb == bb)
+        for (size_t i = 0; i < ex.size() && i < lv_exact.size(); ++i) ex[i] = std::max(ex[i], lv_exact[i]);
+      lv_exact = ex;
+      lv_exact_bb = bb;
+      if (!over) capx *= 1.5;                     // (not expected: the flag without a visible overflow)
+      continue;
+    }
     if (bits & F_LDS_SPILL) {
       if (bb < kb) { ++bb; continue; }
       throw Error(-12, "build: LDS overflow set full at the largest table");

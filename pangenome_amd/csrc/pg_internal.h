@@ -61,7 +61,14 @@ struct DevBuf {
     if (lim && DevBytes::cur().load() + nb > lim)
       throw Error(-12, "device memory cap: " + std::to_string(DevBytes::cur().load() + nb) + " > " +
                            std::to_string(lim) + " bytes");
-    PG_HIP(hipMalloc(&p, nb));
+    const hipError_t e = hipMalloc(&p, nb);
+    if (e != hipSuccess) {
+      p = nullptr;
+      (void)hipGetLastError();
+      throw Error(e == hipErrorOutOfMemory ? -12 : -5,
+                  std::string("hipMalloc of ") + std::to_string(nb) + " bytes (" +
+                      std::to_string(DevBytes::cur().load()) + " held by the library): " + hipGetErrorString(e));
+    }
     cap = nb;
     DevBytes::add(nb);
   }

@@ -88,36 +88,86 @@ def _comm_device(device, group):
     return stage, (torch.device("cpu") if stage else device)
 
 
-def _route(table, world: int, device, group=None, sentinel_local: bool = False):
+def _route(table, world: int, device, group=None, sentinel_local: bool = False, subparts: int = 1):
     """This rank's table -> owner runs of 16-byte records (pg_dbg_partition)
     -> one all-to-all.  The run lengths go out with this rank's n<k sentinel
     flag in one small all-to-all (its receive sizes are the only host read).
-    Returns (the records this rank owns as an (n, 2) int64 tensor on
-    `device`, bytes sent to other ranks, whether any rank saw the sentinel)."""
+    With `subparts` = P > 1 the table is cut into world x P parts (part q:
+    owner q // P, the owner's sub-log q % P; world x P <= 64), so an owner's
+    run from each rank arrives already split into its P sub-logs.  Returns
+    (the records this rank owns as an (n, 2) int64 tensor on `device`, the
+    received counts per (source rank, sub-log) as a (world, P) array, bytes
+    sent to other ranks, whether any rank saw the sentinel)."""
     import torch
     import torch.distributed as dist
+    P = subparts
     stage, comm = _comm_device(device, group)
-    counts = table.partition(world)
+    counts = table.partition(world * P).astype(np.int64).reshape(world, P)
     total = int(counts.sum())
     send = torch.empty((max(total, 1), 2), dtype=torch.int64, device=device)
     if total:
-        table.partition(world, send.data_ptr(), total)
-    head = np.zeros((world, 2), np.int64)
-    head[:, 0] = counts.astype(np.int64)
-    head[:, 1] = 1 if sentinel_local else 0
+        table.partition(world * P, send.data_ptr(), total)
+    head = np.zeros((world, P + 1), np.int64)
+    head[:, :P] = counts
+    head[:, P] = 1 if sentinel_local else 0
     send_head = torch.from_numpy(head).to(comm)
     recv_head = torch.empty_like(send_head)
     dist.all_to_all_single(recv_head, send_head, group=group)
     rh = recv_head.cpu().numpy()
-    rsplit = rh[:, 0].tolist()
+    rsplit = rh[:, :P].sum(axis=1).tolist()
     nrecv = int(sum(rsplit))
     recv = torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm)
-    dist.all_to_all_single(recv[:nrecv], (send.cpu() if stage else send)[:total], output_split_sizes=rsplit,
-                           input_split_sizes=counts.astype(np.int64).tolist(), group=group)
+    ssplit = counts.sum(axis=1).tolist()
     if stage:
+        dist.all_to_all_single(recv[:nrecv], send.cpu()[:total], output_split_sizes=rsplit,
+                               input_split_sizes=ssplit, group=group)
         recv = recv.to(device)
+    else:
+        _all_to_all_rows(recv, send, rsplit, ssplit, comm, group)
     rank = dist.get_rank(group)
-    return recv[:nrecv], 16 * (total - int(counts[rank])), bool(rh[:, 1].any())
+    return recv[:nrecv], rh[:, :P], 16 * (total - int(counts[rank].sum())), bool(rh[:, P].any())
+
+
+# Records per peer and collective on device backends: RCCL 2.26 (ROCm 7)
+# all_to_all returns wrong data for a peer message past 1 GiB (half of a
+# 1.6 GB message lost at world 1, tools/rccl_a2a_check.py); a C5 round moves
+# ~2 GB per peer at N = 8.
+A2A_ROWS = 1 << 25
+
+
+def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None):
+    """all_to_all of (n, 2) int64 rows in pieces of at most A2A_ROWS rows per
+    peer (every rank runs the same number of pieces: the largest message of
+    any rank, by one MAX all-reduce, decides).  Views of contiguous runs, no
+    copies."""
+    import torch
+    import torch.distributed as dist
+    world = len(ssplit)
+    big = torch.tensor([max(max(ssplit), max(rsplit)) if world else 0], dtype=torch.int64, device=comm)
+    dist.all_reduce(big, op=dist.ReduceOp.MAX, group=group)
+    npieces = max(1, -(-int(big.item()) // A2A_ROWS))
+    if npieces == 1:
+        dist.all_to_all_single(recv[:sum(rsplit)], send[:sum(ssplit)], output_split_sizes=rsplit,
+                               input_split_sizes=ssplit, group=group)
+        return
+    so = np.concatenate([[0], np.cumsum(ssplit)]).astype(np.int64)
+    ro = np.concatenate([[0], np.cumsum(rsplit)]).astype(np.int64)
+    lists = dist.get_backend(group) != "gloo"             # (gloo has no list all_to_all: pieces copied)
+    for j in range(npieces):
+        lo = j * A2A_ROWS
+        ins = [send[so[o] + min(lo, ssplit[o]):so[o] + min(lo + A2A_ROWS, ssplit[o])] for o in range(world)]
+        outs = [recv[ro[o] + min(lo, rsplit[o]):ro[o] + min(lo + A2A_ROWS, rsplit[o])] for o in range(world)]
+        if lists:
+            dist.all_to_all(outs, ins, group=group)
+        else:
+            tmp = torch.empty((max(1, sum(x.shape[0] for x in outs)), 2), dtype=recv.dtype, device=recv.device)
+            n = sum(x.shape[0] for x in outs)
+            dist.all_to_all_single(tmp[:n], torch.cat(ins), output_split_sizes=[x.shape[0] for x in outs],
+                                   input_split_sizes=[x.shape[0] for x in ins], group=group)
+            at = 0
+            for x in outs:
+                x.copy_(tmp[at:at + x.shape[0]])
+                at += x.shape[0]
 
 
 def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None, sentinel_global=None):
@@ -149,7 +199,7 @@ def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bo
     """Owner all-to-all + OR-merge + rdBG rule on the owner partition: two
     host reads (the receive sizes, the global counts).  Returns (n_dbg_total,
     n_rdbg_total, n_rdbg_local, bytes_sent)."""
-    recv, sent, sentinel = _route(table, world, device, group, sentinel_local)
+    recv, _, sent, sentinel = _route(table, world, device, group, sentinel_local)
     return _owner_reduce(table, recv, rank, device, sentinel_local, group, sentinel_global=sentinel) + (sent,)
 
 
@@ -176,14 +226,6 @@ def stream_chunks(flags, seq_len, limit: int) -> list:
     return res
 
 
-def _sub_of(recv, nsub: int):
-    """Sub-log of each received 16-byte record: a hash of its key word (a
-    different one from the owner hash, so an owner's entries spread evenly)."""
-    import torch
-    golden = -7046029254386353131                     # 0x9E3779B97F4A7C15 as int64 (wrapping multiply)
-    return ((recv[:, 0] * golden) >> 20) & (nsub - 1)
-
-
 def _free_device_bytes(device) -> int:
     import torch
     if _is_cuda(device):
@@ -200,7 +242,9 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
     (`shard.build`, K1 already done for the whole shard), its entries to their
     owners with one all-to-all (`_route`).  The owner keeps what it receives
     in `subparts` sub-logs by a hash of the key (default: the round count,
-    rounded up to a power of two), so that no step ever handles the whole
+    rounded up to a power of two, at most 64 / world: _route cuts the
+    sender's table into world x P parts, so the sub-logs arrive split and
+    no device-wide sort of a round's records is needed), so that no step ever handles the whole
     log at once: a compaction OR-merges ONE sub-log (pg_dbg_merge, 1/P of the
     owner's entries, within the stage A-C buffers the chunk builds already
     hold) and re-exports it in place (pg_dbg_partition into one run); it runs
@@ -222,7 +266,7 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
     dist.all_reduce(nch, op=dist.ReduceOp.MAX, group=group)
     rounds = max(1, int(nch.item()))
     P = 1
-    while P < min(64, subparts or rounds):
+    while P < min(64 // max(1, world), subparts or rounds):
         P *= 2
     if compact_at is None:
         compact_at = max(1 << 20, _free_device_bytes(device) // 4 // 16)
@@ -254,22 +298,18 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         sentinel |= bool(shard.build(f, extra if i == 0 else 0, rc0))
         if on_chunk is not None:
             on_chunk()
-        recv, s, _ = _route(shard, world, device, group)
+        recv, sub, s, _ = _route(shard, world, device, group, subparts=P)
         sent += s
-        n = int(recv.shape[0])
-        if n:
-            if P == 1:
-                pieces, cnt = [recv], [n]
-            else:
-                sub = _sub_of(recv, P)
-                cnt = torch.bincount(sub, minlength=P).tolist()
-                pieces = torch.split(recv[torch.argsort(sub, stable=True)], cnt)
-                del sub
+        # each source's run arrives as its P sub-log runs: views, no gather
+        off = 0
+        for src in range(sub.shape[0]):
             for p in range(P):
-                if cnt[p]:
-                    logs[p].append(pieces[p])
-                    logn[p] += int(cnt[p])
-            del recv, pieces
+                m = int(sub[src, p])
+                if m:
+                    logs[p].append(recv[off:off + m])
+                    logn[p] += m
+                off += m
+        del recv
         total = sum(logn)
         if total >= compact_at:
             for p in sorted(range(P), key=lambda q: -logn[q]):

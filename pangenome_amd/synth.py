@@ -184,16 +184,35 @@ def c5_record(genome: int, record: int, record_len: int = 125_000_000, snp: floa
     return to_fasta_lines(b"g%d_c%d" % (genome, record), v)
 
 
+def _c5_job(args) -> bytes:
+    g, r, record_len = args
+    return c5_record(g, r, record_len)
+
+
 def write_c5(path: str, n_genomes: int = 10, records: int = 24, record_len: int = 125_000_000,
-             genomes=None) -> int:
-    """Stream C5 (or the genomes listed) to `path`; returns the bytes written."""
+             genomes=None, pairs=None, workers: int = 1) -> int:
+    """Stream C5 (or the genomes listed, or the (genome, record) pairs listed,
+    in that order) to `path` through `workers` spawned processes (~5 GB of
+    memory each at 125 Mbp); returns the bytes written."""
+    if pairs is None:
+        pairs = [(g, r) for g in (range(n_genomes) if genomes is None else genomes) for r in range(records)]
+    jobs = [(g, r, record_len) for g, r in pairs]
     n = 0
     with open(path, "wb") as f:
-        for g in (range(n_genomes) if genomes is None else genomes):
-            for r in range(records):
-                b = c5_record(g, r, record_len)
+        if workers <= 1:
+            it, pool = map(_c5_job, jobs), None
+        else:
+            import multiprocessing
+            pool = multiprocessing.get_context("spawn").Pool(workers)
+            it = pool.imap(_c5_job, jobs)
+        try:
+            for b in it:
                 f.write(b)
                 n += len(b)
+        finally:
+            if pool is not None:
+                pool.close()
+                pool.join()
     return n
 
 

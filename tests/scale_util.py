@@ -38,6 +38,11 @@ INPUTS = {
                  desc="bench --gpus 4 population: genomes 0..399"),
     "pop8": dict(kind="pan", n=800, length=5_000_000, snp=1e-3, indel=1e-4, first=0, k=27, c=2,
                  desc="bench --gpus 8 population: genomes 0..799"),
+    # C5's form at a size the oracle finishes (125 Mbp records
+    # of 3 Gbp genomes, 1 % SNP, 0.1 % indel): records 0-1 of genomes 0-1 in
+    # the file's genome-major order (0.5 Gbp; two segments, each twice)
+    "c5s": dict(kind="c5", genomes=[0, 1], records=[0, 1], k=27, c=2,
+                desc="C5 form: synth.c5_record(g, r) for g in 0-1, r in 0-1 (4 x 125 Mbp, 1 % SNP, 0.1 % indel)"),
 }
 
 
@@ -46,6 +51,8 @@ def make_input(name: str) -> bytes:
     s = INPUTS[name]
     if s["kind"] == "ecoli":
         return synth.ecoli_like()
+    if s["kind"] == "c5":
+        return b"".join(synth.c5_record(g, r) for g in s["genomes"] for r in s["records"])
     return synth.pangenome(s["n"], s["length"], snp=s["snp"], indel=s["indel"], first_index=s["first"])
 
 

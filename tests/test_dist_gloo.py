@@ -21,13 +21,16 @@ def _records(fasta: bytes):
     return [p if i == 0 else b">" + p for i, p in enumerate(parts)]
 
 
-def _worker(rank, world, port, fasta, k, q):
+def _worker(rank, world, port, fasta, k, q, a2a_rows=None):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch.distributed as dist
     from oracle import oracle
+    from pangenome_amd import dist as pdist
     from pangenome_amd.dist import exchange_and_reduce
+    if a2a_rows:
+        pdist.A2A_ROWS = a2a_rows                 # the piecewise all-to-all (RCCL's 1 GiB limit)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     recs = _records(fasta)
@@ -48,8 +51,8 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_exchange_matches_single_process(oracle_mod, world):
+@pytest.mark.parametrize("world,a2a_rows", [(2, None), (3, None), (3, 1000)])
+def test_sharded_exchange_matches_single_process(oracle_mod, world, a2a_rows):
     from pangenome_amd import synth
     k = 27
     fasta = synth.pangenome(6, 30_000, snp=0.01, indel=1e-3, seed=41) + b">tiny\nACG\n"
@@ -59,7 +62,7 @@ def test_sharded_exchange_matches_single_process(oracle_mod, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fasta, k, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fasta, k, q, a2a_rows)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=120) for _ in range(world))

@@ -1,0 +1,129 @@
+"""C5's form on one GPU: SURVEY 8(d)'s C5 workload (10 x 3 Gbp genomes written
+as 125 Mbp records, 1 % SNP, 0.1 % indel; pangenome_amd/synth.c5_record) and
+8(e)'s streamed owner exchange (dist.exchange_stream), which a C5 shard of
+3.75 Gbp per GPU needs because its whole local table does not fit beside the
+owner partition.
+
+* ``c5s`` (records 0-1 of genomes 0-1 in the file's genome-major order,
+  0.5 Gbp, 725 M dBG keys — far less redundant than C3: two distinct 125 Mbp
+  segments, each twice at 1 % SNP): the whole build and the streamed exchange
+  at world 1 (one record per chunk, a compaction after every chunk) against
+  the oracle's digest (tests/golden/scale/c5s.json: n_dbg, n_rdbg, SHA-256 of
+  the sorted dBG and rdBG).  Over gloo (host-staged collectives) and over the
+  nccl backend, i.e. RCCL's all_to_all_single on device buffers with one rank.
+* the C5 shard one rank holds at N = 8 (3.75 Gbp: genome 0's 24 records and
+  genome 1's first 6, 3.8 GB of FASTA), run only with PG_RUN_C5_FULL=1
+  (~5 min; profiles/r03_c5_shard.log): **parity unpinned** — the oracle would
+  need about an hour and ~60 GB of host memory for it — so it is checked
+  through size-independent properties: the streamed exchange gives the same
+  n_dbg, n_rdbg and rdBG SHA-256 at 2^30 bases per chunk (4 chunks, the
+  production setting) and at 2^29 (8 chunks, different compactions); the dBG
+  is closed under reverse complement (no N and odd k: n_dbg is even); and the
+  same holds at world 1 over RCCL.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+from dist_util import ROOT, spawn_ranks
+from scale_util import load_digest
+
+pytestmark = pytest.mark.gpu
+TESTS = os.path.dirname(os.path.abspath(__file__))
+
+
+def _c5_rank(rank, world, port, q, path, backend, chunk_bases, compact_at, whole, subparts):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, TESTS)
+    import torch
+    import torch.distributed as dist
+    from pangenome_amd import kmer
+    from pangenome_amd.dist import GpuShard, exchange_stream, stream_chunks
+    from scale_util import dbg_digest, rdbg_digest
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = {"backend": dist.get_backend()}
+    sh = GpuShard(27, 0)
+    t0 = time.time()
+    meta = sh.load(kmer.seq2bytes(path))
+    R = int(meta["seq_len"].shape[0])
+    out["records"], out["bases"] = R, int(meta["seq_len"].sum())
+    out["parse_s"] = time.time() - t0
+    print("c5 rank: %s parsed %d records, %d bases in %.1f s" % (backend, R, out["bases"], out["parse_s"]), flush=True)
+    if whole:
+        t0 = time.time()
+        st = sh.ctx.build_dbg(np.ones(R, np.uint8), 0, True)
+        st = sh.ctx.build_rdbg()
+        out["whole_s"] = time.time() - t0
+        keys, masks = sh.ctx.dbg()
+        out["whole"] = [int(st.n_dbg), int(st.n_rdbg), dbg_digest(keys, masks), rdbg_digest(sh.ctx.rdbg())]
+        del keys, masks
+    t0 = time.time()
+    chunks = stream_chunks(np.ones(R, np.uint8), meta["seq_len"], chunk_bases)
+    res = exchange_stream(sh, world, rank, dev, chunks, R, True, compact_at=compact_at, subparts=subparts)
+    out["stream_s"] = time.time() - t0
+    out["stream"] = [int(res[0]), int(res[1]), int(res[4]), rdbg_digest(np.sort(res[5]))]
+    print("c5 rank: %s streamed in %.1f s: %s" % (backend, out["stream_s"], out["stream"][:3]), flush=True)
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def c5s_file(tmp_path_factory):
+    from pangenome_amd import synth
+    dg = load_digest("c5s")
+    assert dg is not None, "tests/golden/scale/c5s.json missing (make_scale_digests.py c5s)"
+    p = str(tmp_path_factory.mktemp("c5") / "c5s.fa")
+    n = synth.write_c5(p, pairs=[(g, r) for g in (0, 1) for r in (0, 1)], workers=4)
+    assert n == dg["fasta_bytes"]
+    return p, dg
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("backend", ["gloo", "nccl"])
+def test_c5_form_streamed_vs_oracle_digest(c5s_file, backend):
+    path, dg = c5s_file
+    out = spawn_ranks(1, _c5_rank, (path, backend, 125_000_000, 1, backend == "gloo", None), timeout=600)[0]
+    assert out["backend"] == backend
+    assert (out["records"], out["bases"]) == (4, dg["n_bases"])
+    if "whole" in out:
+        assert out["whole"] == [dg["n_dbg"], dg["n_rdbg"], dg["dbg_sha256"], dg["rdbg_sha256"]]
+    n_dbg, n_rdbg, rounds, rsha = out["stream"]
+    assert rounds == 4
+    assert (n_dbg, n_rdbg, rsha) == (dg["n_dbg"], dg["n_rdbg"], dg["rdbg_sha256"])
+
+
+@pytest.mark.timeout(1100)
+@pytest.mark.skipif(os.environ.get("PG_RUN_C5_FULL") != "1", reason="the 3.75 Gbp C5 shard: PG_RUN_C5_FULL=1")
+def test_c5_shard_full_size_properties(tmp_path):
+    from pangenome_amd import synth
+    p = str(tmp_path / "c5_shard0.fa")
+    t0 = time.time()
+    nbytes = synth.write_c5(p, pairs=[(0, r) for r in range(24)] + [(1, r) for r in range(6)], workers=10)
+    gen_s = time.time() - t0
+    print("c5 shard: %d bytes generated in %.0f s" % (nbytes, gen_s), flush=True)
+    runs = {}
+    for tag, backend, chunk in (("gloo_2^30", "gloo", 1 << 30), ("gloo_2^29", "gloo", 1 << 29),
+                                ("nccl_2^30", "nccl", 1 << 30)):
+        runs[tag] = spawn_ranks(1, _c5_rank, (p, backend, chunk, None, False, None), timeout=1100)[0]
+    a, b, c = runs["gloo_2^30"], runs["gloo_2^29"], runs["nccl_2^30"]
+    for tag, r in runs.items():
+        print("c5 shard %s: %s" % (tag, json.dumps(r, sort_keys=True)))
+    assert a["records"] == 30 and a["bases"] > 3_700_000_000
+    assert a["stream"][2] == 4 and b["stream"][2] == 8
+    # chunking-independent (the OR-merge commutes): same counts and rdBG keys
+    assert a["stream"][:2] == b["stream"][:2] == c["stream"][:2]
+    assert a["stream"][3] == b["stream"][3] == c["stream"][3]
+    # both strands of every window, no N, odd k: the key set is closed under
+    # reverse complement with no palindromes
+    assert a["stream"][0] % 2 == 0 and a["stream"][1] > 0
