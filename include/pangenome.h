@@ -214,9 +214,13 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 
 /* Tuning (tests and experiments; the defaults are the product setting).
  * PG_TUNE_K3_CHUNKS: chunks of the K3 tile list whose work pass overlaps the
- * next chunk's coverage pass, 1..6, or 0 = by tile count (4 when the tile
- * list has >= 16384 tiles, else 1). */
+ * next chunk's coverage pass, 1..6, or 0 = by tile count (3 when the list
+ * has >= 3072 coverage groups, else 1). */
 #define PG_TUNE_K3_CHUNKS 1
+/* PG_TUNE_K3_COVER: form of the K3 coverage pass, 0 (default) = members
+ * compared quad by quad from registers, 1 = members staged in LDS (round 2);
+ * the results are the same, only the records left to the work pass differ. */
+#define PG_TUNE_K3_COVER 10
 /* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
  * count asks (0..8): exercises the overflow set, its spill and the re-run
  * with more buckets (results are unchanged). */

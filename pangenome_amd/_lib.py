@@ -24,6 +24,7 @@ PG_TUNE_STAGE_PIECE = 6
 PG_TUNE_STAGE_SLOTS = 7
 PG_TUNE_HOST_REGISTER = 8
 PG_TUNE_DEVICE_CAP = 9
+PG_TUNE_K3_COVER = 10
 
 
 class PgStats(C.Structure):

@@ -649,6 +649,281 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
     }
 }
 
+// ---- K3 coverage pass, quad form (the default).  Same groups, drift search
+// and coverage rule as k_cover, with the members never staged in LDS: thread
+// t compares ONE 16-byte quad of each member (dwords D0+4t .. D0+4t+3 of the
+// class stream, D0 = the dword holding the tile's first context byte
+// rs+qt-1) against every drift of both references, a 4-bit mismatch nibble
+// per (reference, drift), and segment t then reads the nibbles of quads t,
+// t+1, t+2 (the 12 dwords that hold its IW+k+1 context bytes) from LDS.
+// Each context byte is compared once instead of ~2.75 times, the member
+// bytes go straight from HBM into registers (one coalesced 16-byte load per
+// thread and member, issued beside the reference staging), and the block
+// holds 16 KB of LDS instead of 27.8 KB.  The anchors of the drift search (3
+// x 32 bytes per member) are staged on their own.
+constexpr int RPAD = 32;                      // s_ref front pad: quads reaching below the span stay in bounds
+constexpr int RSZ = RPAD + RSPAN + 32;        // + tail slack: a quad holding a staged byte never reads past it
+constexpr int ANCB = 48;                      // staged bytes per anchor (from its 16-byte aligned start)
+constexpr int NQD = CBLOCK + 2;               // quads per member: segment t reads quads t .. t+2
+typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+// the 16 bytes of class stream at byte address a (4-byte aligned), 0 outside [0, ncls)
+__device__ __forceinline__ uint4 quad_at(const uint8_t* cls, long long a, uint64_t ncls, bool live) {
+  uint4 v = make_uint4(0u, 0u, 0u, 0u);
+  if (live && a >= 0 && (uint64_t)a + 16 <= ncls) {
+    const u32x4a4 x = *reinterpret_cast<const u32x4a4*>(cls + a);
+    v = make_uint4(x.x, x.y, x.z, x.w);
+  }
+  return v;
+}
+// mismatch nibble of a member quad against the reference quad at s_ref index
+// e (e & 15 uniform over the wave); an index whose two 16-byte reads would
+// leave s_ref reads at e & 15 instead (no covered segment uses such a quad)
+__device__ __forceinline__ uint32_t quad_nib(const uint8_t* s_ref, int e, const uint4& M) {
+  if (e < 0 || e > RSZ - 32) e &= 15;
+  uint32_t R[4];
+  lds_bytes16(s_ref, (uint32_t)e, R);
+  return (uint32_t)(M.x != R[0]) | (uint32_t)(M.y != R[1]) << 1 | (uint32_t)(M.z != R[2]) << 2 |
+         (uint32_t)(M.w != R[3]) << 3;
+}
+// covered windows of a segment from the 12-bit dword mismatch map of its
+// quads (bit i: dword i from the dword holding byte q0-1, which sits sh
+// bytes into it): segment_cover's rule on that grid
+__device__ __forceinline__ uint32_t map_cover(uint32_t nz, int sh, int k) {
+  constexpr uint32_t ALL = (1u << IW) - 1u;
+  nz &= (2u << ((IW + k + sh) >> 2)) - 1u;                 // dwords holding bytes q0-1 .. q0+IW+k-1
+  if (!nz) return ALL;
+  const int first = 4 * __builtin_ctz(nz) - sh, last = 4 * (31 - __builtin_clz(nz)) + 3 - sh;
+  const int ulo = max(0, first - k - 1), uhi = min(IW - 1, last);
+  return ALL & ~(((2u << uhi) - 1u) & ~((1u << ulo) - 1u));
+}
+__device__ __forceinline__ void drift_task_anc(const uint8_t* s_anc, const uint8_t* s_ref, int ia, int ibhi, int lo,
+                                               int hi, int w, unsigned* best) {
+  drift_task(s_anc, s_ref, ia, ibhi, lo, hi, w, best);
+}
+// cover_search on the staged anchors: member m's anchor ai is s_anc[m][ai],
+// its first byte at index (rs + a) & 15
+__device__ __forceinline__ void cover_search_q(uint8_t (*s_anc)[NANCH][ANCB], uint8_t (*s_ref)[RSZ],
+                                               const MemGeo* geo, const RefGeo& R0, const RefGeo& R1,
+                                               unsigned (*best)[2][NANCH], long long qt, uint32_t dm0, uint32_t dm1) {
+  constexpr int NT = QM * 2 * NANCH, PER = CBLOCK / 32;
+  constexpr int NW = (2 * DRIFT + 3) / 4 + 2;
+  auto geom = [&](const RefGeo& R, const MemGeo& G, int ai, int& ia, int& ibhi, int& lo, int& hi) {
+    const long long a = qt + 8 + (long long)ai * ASTEP;
+    ia = (int)((G.rs + a) & 15);
+    ibhi = (int)(R.rbase + a + DRIFT);
+    lo = max(ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
+    hi = a + ALEN > G.rn ? -1 : min(ibhi, (int)(R.rbase + R.phi) - ALEN);
+  };
+#pragma unroll 1
+  for (int t0 = 0; t0 < NT; t0 += PER) {
+    const int t = t0 + ((int)threadIdx.x >> 5), l = (int)threadIdx.x & 31;
+    const int m = t / (2 * NANCH), ri = (t / NANCH) & 1, ai = t % NANCH;
+    if (t < NT && (((ri ? dm1 : dm0) >> m) & 1u)) {
+      const MemGeo& G = geo[m];
+      int ia, ibhi, lo, hi;
+      geom(ri ? R1 : R0, G, ai, ia, ibhi, lo, hi);
+      lo = max(lo, ibhi - (G.h[ri] + HWIN2));
+      hi = min(hi, ibhi - (G.h[ri] - HWIN2));
+      const int w = (lo >> 2) + l;
+      if (lo <= hi && 4 * w <= hi) drift_task_anc(s_anc[m][ai], s_ref[ri], ia, ibhi, lo, hi, w, &best[m][ri][ai]);
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int p = 0; p < 2 * QM; ++p) {                          // block-uniform
+    const int m = p >> 1, ri = p & 1;
+    if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
+    const MemGeo& G = geo[m];
+#pragma unroll 1
+    for (int ai = 0; ai < NANCH; ++ai) {
+      int ia, ibhi, lo, hi;
+      geom(ri ? R1 : R0, G, ai, ia, ibhi, lo, hi);
+      for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += CBLOCK)
+        drift_task_anc(s_anc[m][ai], s_ref[ri], ia, ibhi, lo, hi, w, &best[m][ri][ai]);
+    }
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(CBLOCK)
+k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __restrict__ descs,
+          WorkItem* __restrict__ queue, unsigned long long* __restrict__ qcount, unsigned long long qcap, int k,
+          int ref, long long rfs, long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints,
+          int nrec, uint64_t ngroups, uint32_t b0, uint32_t b1, uint32_t bt) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_ref[2][RSZ];
+  __shared__ __attribute__((aligned(16))) uint8_t s_anc[QM][NANCH][ANCB];
+  __shared__ __attribute__((aligned(16))) uint4 s_xq[QM][2];       // member quads CBLOCK, CBLOCK+1
+  __shared__ uint32_t s_nib[QM][NQD];                              // bit 4*(3*ri+j)+i: dword i, reference ri, drift j
+  __shared__ unsigned s_best[QM][2][NANCH];
+  __shared__ uint32_t s_scan[CBLOCK / 64];
+  __shared__ unsigned long long s_qbase;
+  __shared__ MemGeo s_geo[QM];
+  __shared__ Drifts s_dr[QM][2];
+  uint64_t g, ge;
+  xcd_chunk(ngroups, b0, b1, bt, blockIdx.x & 7, g, ge);
+  g += blockIdx.x >> 3;
+  if (g >= ge) return;                             // (block-uniform, before any barrier)
+  const int t = (int)threadIdx.x;
+  const long long qt = (long long)descs[QM * g].stripe * TILE;
+  // the members (uniform loads): records, which members dedup
+  long long mrs[QM], mrn[QM];
+  uint32_t dm0 = 0, dm1 = 0, live = 0;
+#pragma unroll
+  for (int m = 0; m < QM; ++m) {
+    const TileDesc td = descs[QM * g + m];
+    mrs[m] = td.rs;
+    mrn[m] = td.rn;
+    const bool d0 = td.r >= 0 && ref >= 0 && ref != td.r;
+    live |= (uint32_t)(td.r >= 0) << m;
+    dm0 |= (uint32_t)d0 << m;
+    dm1 |= (uint32_t)(d0 && ref2 >= 0 && ref2 != td.r) << m;
+  }
+  // member quads straight into registers: dwords D0+4t .. (D0 = floor((rs+qt-1)/4))
+  uint4 Mq[QM];
+#pragma unroll
+  for (int m = 0; m < QM; ++m) {
+    const long long d0 = (mrs[m] + qt - 1) >> 2;
+    Mq[m] = quad_at(cls, 4 * d0 + 16ll * t, ncls, (dm0 >> m) & 1u);
+  }
+  if (t < 2 * QM) {                                // quads CBLOCK, CBLOCK+1 of member t/2
+    const int m = t >> 1;
+    long long rs = mrs[0];
+#pragma unroll
+    for (int x = 1; x < QM; ++x) rs = m == x ? mrs[x] : rs;
+    s_xq[m][t & 1] = quad_at(cls, 4 * ((rs + qt - 1) >> 2) + 16ll * (CBLOCK + (t & 1)), ncls, (dm0 >> m) & 1u);
+  } else if (t >= 64 && t < 64 + QM * NANCH * 3) { // anchors: 3 chunks of 16 bytes each
+    const int x = t - 64, m = x / (NANCH * 3), ai = (x / 3) % NANCH, c = x % 3;
+    long long rs = mrs[0];
+#pragma unroll
+    for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
+    const long long a = ((rs + qt + 8 + (long long)ai * ASTEP) & ~15ll) + 16 * c;
+    *reinterpret_cast<uint4*>(&s_anc[m][ai][16 * c]) = quad_at(cls, a, ncls, (dm0 >> m) & 1u);
+  } else if (t >= 128 && t < 128 + QM) {           // hints (per XCD, reference and record)
+    const int m = t - 128;
+    const TileDesc td = descs[QM * g + m];
+    int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
+    const int h0 = ((dm0 >> m) & 1u) ? hx[td.r] : -1;
+    const int h1 = ((dm1 >> m) & 1u) ? hx[nrec + td.r] : -1;
+    MemGeo G;
+    G.r = td.r;
+    G.rs = td.rs;
+    G.rn = td.rn;
+    G.a0 = G.hi = 0;
+    G.h[0] = h0 < 0 ? DRIFT : h0;
+    G.h[1] = h1 < 0 ? DRIFT : h1;
+    s_geo[m] = G;
+  }
+  if (t >= 192 && t < 192 + QM * 2 * NANCH) (&s_best[0][0][0])[t - 192] = ~0u;
+  // the references' spans of this stripe: [qt-1-DRIFT, qt+TILE+k+1+DRIFT) clipped
+  RefGeo rg[2];
+  long long ra0[2], rend[2];
+#pragma unroll
+  for (int ri = 0; ri < 2; ++ri) {
+    const long long s = ri ? r2s : rfs, n = ri ? r2n : rfn;
+    rg[ri].plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
+    rg[ri].phi = qt + TILE + k + 1 + DRIFT < n ? qt + TILE + k + 1 + DRIFT : n;
+    rg[ri].rfn = n;
+    ra0[ri] = (s + rg[ri].plo) & ~15ll;
+    rend[ri] = s + rg[ri].phi;
+    rg[ri].rbase = s - ra0[ri] + RPAD;
+  }
+  {
+    static_assert(RSPAN <= 2 * CBLOCK * 16, "two chunks per thread");
+    uint4 v[2][2];
+    bool lv[2][2];
+    const long long o0 = (long long)t * 16, o1 = o0 + CBLOCK * 16;
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const long long from = ra0[ri], to = (ri ? dm1 != 0 : dm0 != 0) ? rend[ri] : from;
+      lv[ri][0] = from + o0 < to;
+      lv[ri][1] = from + o1 < to;
+      v[ri][0] = lv[ri][0] ? *reinterpret_cast<const uint4*>(cls + from + o0) : make_uint4(0u, 0u, 0u, 0u);
+      v[ri][1] = lv[ri][1] ? *reinterpret_cast<const uint4*>(cls + from + o1) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      if (lv[ri][0]) *reinterpret_cast<uint4*>(s_ref[ri] + RPAD + o0) = v[ri][0];
+      if (lv[ri][1]) *reinterpret_cast<uint4*>(s_ref[ri] + RPAD + o1) = v[ri][1];
+    }
+  }
+  __syncthreads();
+  if (dm0) cover_search_q(s_anc, s_ref, s_geo, rg[0], rg[1], s_best, qt, dm0, dm1);
+  // hints and drift sets: one lane per (member, reference); a drift set's
+  // offsets index s_ref from thread 0's quad (add 16 t)
+  if (t < 2 * QM) {
+    const int m = t >> 1, ri = t & 1;
+    if ((((ri ? dm1 : dm0) >> m) & 1u)) {
+      const MemGeo& G = s_geo[m];
+      publish_hint(s_best[m][ri], hints + (size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + G.r);
+      const RefGeo R = ri ? rg[1] : rg[0];
+      const long long qs = qt - 1 - ((G.rs + qt - 1) & 3);   // record position of thread 0's quad
+      s_dr[m][ri] = drifts_of(s_best[m][ri], qt, -qs, R.rbase, R.rfn, R.plo, R.phi, k);
+    }
+  }
+  __syncthreads();
+  // mismatch nibbles of every quad against every drift of both references
+#pragma unroll
+  for (int m = 0; m < QM; ++m) {
+    uint32_t w = 0, wx = 0;
+    if ((dm0 >> m) & 1u) {
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri) {
+        if (ri && !((dm1 >> m) & 1u)) break;
+        const int nd = __builtin_amdgcn_readfirstlane(s_dr[m][ri].n);
+#pragma unroll
+        for (int j = 0; j < NANCH; ++j) {
+          if (j >= nd) break;
+          const int off = __builtin_amdgcn_readfirstlane(s_dr[m][ri].off[j]);
+          w |= quad_nib(s_ref[ri], off + 16 * t, Mq[m]) << (4 * (3 * ri + j));
+          if (t < 2) wx |= quad_nib(s_ref[ri], off + 16 * (CBLOCK + t), s_xq[m][t]) << (4 * (3 * ri + j));
+        }
+      }
+    }
+    s_nib[m][t] = w;
+    if (t < 2) s_nib[m][CBLOCK + t] = wx;
+  }
+  __syncthreads();
+  const long long q0 = qt + (long long)t * IW;
+  const int rel = t * IW;
+  uint32_t cov[QM], nwk = 0, wmask = 0;
+#pragma unroll
+  for (int m = 0; m < QM; ++m) {
+    const long long last = mrn[m] - k;
+    uint32_t covered = 0;
+    if (((dm0 >> m) & 1u) && q0 > 0 && q0 + IW <= last) {
+      const int sh = (int)((mrs[m] + qt - 1) & 3);
+      const uint32_t w0 = s_nib[m][t], w1 = s_nib[m][t + 1], w2 = s_nib[m][t + 2];
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri) {
+        if (ri && !((dm1 >> m) & 1u)) break;
+        const int nd = __builtin_amdgcn_readfirstlane(s_dr[m][ri].n);
+#pragma unroll
+        for (int j = 0; j < NANCH; ++j) {
+          if (j >= nd) break;
+          const int lo = __builtin_amdgcn_readfirstlane(s_dr[m][ri].lo[j]);
+          const int hi = __builtin_amdgcn_readfirstlane(s_dr[m][ri].hi[j]);
+          const int s = 4 * (3 * ri + j);
+          const uint32_t nz = ((w0 >> s) & 15u) | ((w1 >> s) & 15u) << 4 | ((w2 >> s) & 15u) << 8;
+          covered |= ((rel >= lo) & (rel <= hi)) ? map_cover(nz, sh, k) : 0u;
+        }
+      }
+    }
+    cov[m] = covered;
+    const bool work = ((live >> m) & 1u) && q0 <= last && covered != (1u << IW) - 1u;
+    wmask |= (uint32_t)work << m;
+    nwk += work ? 1u : 0u;
+  }
+  uint32_t nwork;
+  uint32_t pos = block_excl_scan<CBLOCK>(nwk, s_scan, nwork);
+  const unsigned sub = blockIdx.x % NQ;
+  if (t == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < QM; ++m)
+    if ((wmask >> m) & 1u) queue[sub * qcap + s_qbase + pos++] = WorkItem{mrs[m], mrn[m] - k, q0, cov[m], 0u};
+}
+
 // ---------------------------------------------------------------- stage A
 // Records go to NBIN coarse bins (h >> shift: the top bits of the bucket
 // index), each with one region per XCD (region = bin * 8 + XCD), so that a
@@ -1765,10 +2040,14 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   for (int i = 0; i < nch; ++i) {
     auto* qi = q + qoff[i];
     auto* qni = qn + (cbytes / 8) * i;
-    if (gc[i])
+    if (gc[i] && c.k3_cover == 1)
       hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
                          c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
                          (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch);
+    else if (gc[i])
+      hipLaunchKernelGGL(k_cover_q, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, (uint64_t)c.cls.cap, td, qi, qni,
+                         (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
+                         c.k3_hint.as<int>(), (int)c.n_records, ntiles, (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch);
     PG_HIP(hipGetLastError());
     hipStream_t ws = s1;
     if (nch > 1 && i + 1 == nch) {

@@ -153,14 +153,16 @@ def test_overflow_and_rerun_paths_vs_oracle(oracle_mod, k):
         ctx.close()
 
 
+@pytest.mark.parametrize("form", [0, 1])
 @pytest.mark.parametrize("c", [0, 2])
-def test_k3_reference_dedup_vs_oracle(oracle_mod, c):
-    """k_insert skips a follower window whose k+2 context bytes equal the lead
-    record's at some drift: copies of the lead with insertions (drift inside
-    and beyond the +-512 search), deletions, SNPs, an N run, lowercase bytes,
-    shorter copies (reference windows near its ends) and a reverse complement."""
+def test_k3_reference_dedup_vs_oracle(oracle_mod, c, form):
+    """The coverage pass skips a follower window whose k+2 context bytes equal
+    the lead record's at some drift: copies of the lead with insertions (drift
+    inside and beyond the +-512 search), deletions, SNPs, an N run, lowercase
+    bytes, shorter copies (reference windows near its ends) and a reverse
+    complement; both forms of the pass (quad compare, LDS-staged members)."""
     from pangenome_amd import synth
-    from pangenome_amd._lib import Context
+    from pangenome_amd._lib import Context, PG_TUNE_K3_COVER
     rng = np.random.default_rng(7 + c)
     acgt = np.frombuffer(b"ACGT", np.uint8)
     lead = acgt[rng.integers(0, 4, 30_000)]
@@ -184,6 +186,7 @@ def test_k3_reference_dedup_vs_oracle(oracle_mod, c):
     fasta = b"".join(b">g%d\n" % i + g.tobytes() + b"\n" for i, g in enumerate(copies))
     ref = oracle_mod.OracleRun(fasta, 27, c)
     ctx = Context(27)
+    ctx.tune(PG_TUNE_K3_COVER, form)
     ctx.set_fasta(fasta)
     ctx.parse()
     ctx.build_dbg(None, 0, c == 2)
@@ -194,6 +197,32 @@ def test_k3_reference_dedup_vs_oracle(oracle_mod, c):
     ctx.build_rdbg()
     assert np.array_equal(ctx.rdbg(), ref.rdbg())
     ctx.close()
+
+
+@pytest.mark.parametrize("k", [5, 15, 21, 27])
+def test_k3_cover_forms_vs_oracle(oracle_mod, k):
+    """Both coverage-pass forms give the oracle's dBG and rdBG at several k
+    (the quad form's window mask depends on k and on each record's start
+    modulo 4: odd line widths and headers shift it), and the quad form leaves
+    no more than 2 % more stage A records than the LDS-staged one."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context, PG_TUNE_K3_COVER
+    fasta = synth.pangenome(9, 120_000, snp=2e-3, indel=3e-4, seed=400 + k, width=61)
+    ref = oracle_mod.OracleRun(fasta, k, 2)
+    rk, rm = ref.dbg()
+    recs = []
+    for form in (0, 1):
+        ctx = Context(k)
+        ctx.tune(PG_TUNE_K3_COVER, form)
+        ctx.set_fasta(fasta)
+        ctx.parse()
+        st = ctx.build(None, 0, True)
+        keys, masks = ctx.dbg()
+        assert np.array_equal(keys, rk) and np.array_equal(masks, rm), form
+        assert np.array_equal(ctx.rdbg(), ref.rdbg()), form
+        recs.append(st.n_records_a)
+        ctx.close()
+    assert recs[0] <= recs[1] * 1.02 + 64, recs
 
 
 def test_edge_checkpoint_reversal_vs_oracle(km, oracle_mod, tmp_path):
