@@ -221,6 +221,13 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * compared quad by quad from registers, 1 = members staged in LDS (round 2);
  * the results are the same, only the records left to the work pass differ. */
 #define PG_TUNE_K3_COVER 10
+/* PG_TUNE_K3_WBLK: blocks per CU of the K3 work passes when the tile list
+ * runs in chunks: low 4 bits for every chunk but the last, high 4 bits for
+ * the last (0 = 2 and the same as the others). */
+#define PG_TUNE_K3_WBLK 11
+/* PG_TUNE_K3_EMIT: form of the K3 work pass, 0 (default) = each queued
+ * segment's records computed and emitted in two halves, 1 = at once. */
+#define PG_TUNE_K3_EMIT 12
 /* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
  * count asks (0..8): exercises the overflow set, its spill and the re-run
  * with more buckets (results are unchanged). */

@@ -25,6 +25,8 @@ PG_TUNE_STAGE_SLOTS = 7
 PG_TUNE_HOST_REGISTER = 8
 PG_TUNE_DEVICE_CAP = 9
 PG_TUNE_K3_COVER = 10
+PG_TUNE_K3_WBLK = 11
+PG_TUNE_K3_EMIT = 12
 
 
 class PgStats(C.Structure):

@@ -275,6 +275,14 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: K3 cover form must be 0 or 1");
         x->c.k3_cover = (int)value;
         break;
+      case PG_TUNE_K3_WBLK:
+        if (value < 0 || value > 255) throw pg::Error(PG_EINVAL, "pg_tune: K3 work blocks must be in [0, 255]");
+        x->c.k3_wblk = (int)value;
+        break;
+      case PG_TUNE_K3_EMIT:
+        if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: K3 emit form must be 0 or 1");
+        x->c.k3_emit = (int)value;
+        break;
       case PG_TUNE_BUCKET_SHIFT:
         if (value < 0 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: bucket shift must be in [0, 8]");
         x->c.bb_shift = (int)value;

@@ -149,24 +149,24 @@ constexpr int ASTEP = (TILE - ALEN - 16) / (NANCH - 1);      // anchor spacing
 // which a reference record inserts, or past the record's last window).
 // Interior segments run from registers; a segment holding window 0 or the
 // last window takes the generic path with the boundary rules.
-template <bool RC>
+template <bool RC, int X0 = 0, int NX = IW>
 __device__ __forceinline__ void segment_records(const uint8_t* s_cls, long long base, long long q0, long long last,
                                                 int k, uint64_t shift, const TableView& T, uint32_t covered,
-                                                uint64_t (&hh)[IW], uint32_t (&mm)[IW]) {
-  uint64_t K = 0, Kr = 0;
-  init_keys(s_cls, (uint32_t)(base + q0), k, K, Kr);
+                                                uint64_t& K, uint64_t& Kr, uint64_t (&hh)[NX], uint32_t (&mm)[NX]) {
+  static_assert(X0 % 4 == 0 && NX % 4 == 0 && X0 + NX <= IW, "whole dwords of the segment");
+  if (X0 == 0) init_keys(s_cls, (uint32_t)(base + q0), k, K, Kr);
   if (q0 > 0 && q0 + IW <= last) {
     // interior segment (no window 0, no last window, all IW live): the context
     // bytes come from LDS once, into registers; P(i) = S(q-1), D(i) = S(q+k-1)
-    // for window q = q0 + i, and D(i+1) = S(q+k)
-    const uint32_t o = (uint32_t)(base + q0);
-    uint32_t P[IW / 4], D[IW / 4 + 1];
+    // for window q = q0 + X0 + i, and D(i+1) = S(q+k)
+    const uint32_t o = (uint32_t)(base + q0) + X0;
+    uint32_t P[NX / 4], D[NX / 4 + 1];
     lds_bytes(s_cls, o - 1, P);
     lds_bytes(s_cls, o + (uint32_t)k - 1, D);
 #pragma unroll
-    for (int x = 0; x < IW; ++x) {
+    for (int x = 0; x < NX; ++x) {
       const uint32_t p = byte_at(P, x), s = byte_at(D, x + 1);
-      if (x) {                                   // Nu // 5 + alpha * 5^(k-1) (:1072)
+      if (X0 + x) {                              // Nu // 5 + alpha * 5^(k-1) (:1072)
         const uint32_t din = byte_at(D, x);
         K = (K - digit_fw(p)) * INV5 + (uint64_t)digit_fw(din) * shift;
         Kr = (Kr - (uint64_t)digit_rc(p) * shift) * 5 + digit_rc(din);
@@ -184,19 +184,19 @@ __device__ __forceinline__ void segment_records(const uint8_t* s_cls, long long 
         c = le ? K : Kr;
         m = le ? mf : (mf << B_SHIFT);
       }
-      mm[x] = ((covered >> x) & 1u) ? 0u : m;
+      mm[x] = ((covered >> (X0 + x)) & 1u) ? 0u : m;
       hh[x] = T.perm(c);
     }
     return;
   }
   auto S = [&](long long q) -> uint32_t { return s_cls[base + q]; };
 #pragma unroll
-  for (int x = 0; x < IW; ++x) {
-    const long long q = q0 + x;
+  for (int x = 0; x < NX; ++x) {
+    const long long q = q0 + X0 + x;
     hh[x] = 0;
     mm[x] = 0;
     if (q <= last) {
-      if (x) {                                   // Nu // 5 + alpha * 5^(k-1) (:1072)
+      if (X0 + x) {                              // Nu // 5 + alpha * 5^(k-1) (:1072)
         const uint32_t dout = S(q - 1), din = S(q + k - 1);
         K = (K - digit_fw(dout)) * INV5 + (uint64_t)digit_fw(din) * shift;
         Kr = (Kr - (uint64_t)digit_rc(dout) * shift) * 5 + digit_rc(din);
@@ -218,7 +218,7 @@ __device__ __forceinline__ void segment_records(const uint8_t* s_cls, long long 
       } else {
         if (K <= Kr) { c = K; m = mf; } else { c = Kr; m = mf << B_SHIFT; }
       }
-      mm[x] = ((covered >> x) & 1u) ? 0u : m;
+      mm[x] = ((covered >> (X0 + x)) & 1u) ? 0u : m;
       hh[x] = T.perm(c);
     }
   }
@@ -246,7 +246,7 @@ constexpr int QSTRIDE = 8;                    // counter spacing (unsigned long 
 // (|delta| << 16 | drift) of every matching candidate (atomicMin: the
 // smallest drift wins).  The hints and drift sets are published by the caller.
 constexpr int HWIN2 = (PG_EXP_BITS & 32768) ? 40 : 56;
-constexpr int QM = 4;                         // member tiles per coverage block (one stripe)
+constexpr int QM = 4;                         // member tiles per coverage block (one stripe; 8 measured slower)
 struct MemGeo {                               // a member tile: record, staging window, hints
   long long rs, rn, a0, hi;
   int r, h[2];                                // h: the XCD's last drift per reference (DRIFT: none)
@@ -799,8 +799,8 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
     for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
     const long long a = ((rs + qt + 8 + (long long)ai * ASTEP) & ~15ll) + 16 * c;
     *reinterpret_cast<uint4*>(&s_anc[m][ai][16 * c]) = quad_at(cls, a, ncls, (dm0 >> m) & 1u);
-  } else if (t >= 128 && t < 128 + QM) {           // hints (per XCD, reference and record)
-    const int m = t - 128;
+  } else if (t >= 160 && t < 160 + QM) {           // hints (per XCD, reference and record)
+    const int m = t - 160;
     const TileDesc td = descs[QM * g + m];
     int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
     const int h0 = ((dm0 >> m) & 1u) ? hx[td.r] : -1;
@@ -814,6 +814,8 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
     G.h[1] = h1 < 0 ? DRIFT : h1;
     s_geo[m] = G;
   }
+  static_assert(2 * QM <= 64 && 64 + QM * NANCH * 3 <= 160 && 160 + QM <= 192 && 192 + QM * 2 * NANCH <= CBLOCK,
+                "thread ranges of the staging roles");
   if (t >= 192 && t < 192 + QM * 2 * NANCH) (&s_best[0][0][0])[t - 192] = ~0u;
   // the references' spans of this stripe: [qt-1-DRIFT, qt+TILE+k+1+DRIFT) clipped
   RefGeo rg[2];
@@ -848,7 +850,11 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
     }
   }
   __syncthreads();
-  if (dm0) cover_search_q(s_anc, s_ref, s_geo, rg[0], rg[1], s_best, qt, dm0, dm1);
+  if (dm0 && !(PG_EXP_BITS & (1 << 20))) cover_search_q(s_anc, s_ref, s_geo, rg[0], rg[1], s_best, qt, dm0, dm1);
+  if ((PG_EXP_BITS & (1 << 20)) && t < 2 * QM) {   // (experiment: the hint as the only drift)
+    const int m = t >> 1, ri = t & 1;
+    for (int ai = 0; ai < NANCH; ++ai) s_best[m][ri][ai] = (unsigned)s_geo[m].h[ri];
+  }
   // hints and drift sets: one lane per (member, reference); a drift set's
   // offsets index s_ref from thread 0's quad (add 16 t)
   if (t < 2 * QM) {
@@ -942,33 +948,85 @@ struct BinOut {
   unsigned* flags;                            // [0] sentinel, [1] stage A bits
 };
 
-// every thread of the block calls this (two barriers); s_cnt must be zero on entry (and is left zero)
+// Block emission.  The records of a round (NR per thread, some empty) are
+// ranked per (sub-round of ESUB records per thread, bin) by LDS atomics; one
+// returning atomic per bin reserves the round's run in the bin's region for
+// this XCD; then, sub-round by sub-round, the records are placed in an LDS
+// stage in bin order and written out by consecutive threads, so a store
+// instruction covers a few contiguous runs instead of one record in each of
+// up to 64 bins (the scattered form spent the work pass issuing stores: SQ
+// WAIT_INST_ANY 10.7 K quad-cycles per wave, ~100 us per C3 chunk).
+// Every thread of the block calls this (2 + 2 * NR / ESUB barriers, the last
+// one after the stage's reads); L.cnt must be zero on entry and is left zero.
+constexpr int ESUB = 4;                       // records per thread and sub-round
+constexpr int EST = IBLOCK * ESUB;            // staged records per sub-round: 12 KB
+template <int NS>
+struct EmitLds {
+  uint32_t cnt[NS][NBIN];                     // per sub-round and bin: records
+  uint32_t off[NS][NBIN + 1];                 // their exclusive scan over bins (stage offsets), total last
+  unsigned long long base[NS][NBIN];          // region position of the bin's first record of the sub-round
+};
 template <int NR>
 __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[NR], const uint32_t (&m)[NR],
-                                           uint32_t* s_cnt, unsigned long long* s_base) {
+                                           EmitLds<NR / ESUB>& L, unsigned long long* st_key, uint32_t* st_mw) {
+  constexpr int NS = NR / ESUB;
+  static_assert(NR % ESUB == 0 && NBIN == 64, "whole sub-rounds; one wave scans the bins");
+  const int t = (int)threadIdx.x;
   uint32_t rk[NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) rk[j] = m[j] ? atomicAdd(&s_cnt[(uint32_t)(h[j] >> O.shift)], 1u) : 0u;
+  for (int j = 0; j < NR; ++j) rk[j] = m[j] ? atomicAdd(&L.cnt[j / ESUB][(uint32_t)(h[j] >> O.shift)], 1u) : 0u;
   __syncthreads();
   const uint32_t x = blockIdx.x & 7;
-  if (threadIdx.x < NBIN) {
-    const uint32_t n = s_cnt[threadIdx.x];
-    s_base[threadIdx.x] = n ? atomicAdd(O.cursor + CSTRIDE * (threadIdx.x * 8 + x), (unsigned long long)n) : 0ull;
-    s_cnt[threadIdx.x] = 0u;
+  if (t < NBIN) {
+    uint32_t n[NS], tot = 0;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      n[q] = L.cnt[q][t];
+      L.cnt[q][t] = 0u;
+      tot += n[q];
+    }
+    unsigned long long b = tot ? atomicAdd(O.cursor + CSTRIDE * (t * 8 + x), (unsigned long long)tot) : 0ull;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) {
+      L.base[q][t] = b;
+      b += n[q];
+      uint32_t v = n[q];
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(v, o, 64);
+        if (t >= o) v += y;
+      }
+      L.off[q][t] = v - n[q];
+      if (t == NBIN - 1) L.off[q][NBIN] = v;
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    if (!m[j]) continue;
-    const uint32_t p = (uint32_t)(h[j] >> O.shift);
-    const unsigned long long pos = s_base[p] + rk[j];
-    if (pos < O.cap) {
-      const uint64_t at = (uint64_t)(p * 8 + x) * O.cap + pos;
-      O.key[at] = h[j];
-      O.mw[at] = m[j];
-    } else {
-      atomicOr(O.flags + 1, F_A_OVER);
+  for (int q = 0; q < NS; ++q) {
+#pragma unroll
+    for (int j = q * ESUB; j < (q + 1) * ESUB; ++j)
+      if (m[j]) {
+        const uint32_t at = L.off[q][(uint32_t)(h[j] >> O.shift)] + rk[j];
+        st_key[at] = h[j];
+        st_mw[at] = m[j];
+      }
+    __syncthreads();
+    const uint32_t tot = L.off[q][NBIN];
+    for (uint32_t e = (uint32_t)t; e < tot; e += IBLOCK) {
+      const unsigned long long hv = st_key[e];
+      const uint32_t p = (uint32_t)(hv >> O.shift);
+      const unsigned long long pos = L.base[q][p] + (e - L.off[q][p]);
+      if (PG_EXP_BITS & (1 << 17)) {
+        if (hv == 42ull) O.flags[3] = (unsigned)pos;   // (experiment: no record stores)
+      } else if (pos < O.cap) {
+        const uint64_t at = (uint64_t)(p * 8 + x) * O.cap + pos;
+        O.key[at] = hv;
+        O.mw[at] = st_mw[e];
+      } else {
+        atomicOr(O.flags + 1, F_A_OVER);
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -976,25 +1034,32 @@ __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[
 // of a round of IBLOCK segments leave through block_emit.  The NQ sub-queues
 // are read as one concatenated list (their counts scanned in LDS); the
 // segment's 64 context bytes (from position q0-2, 16-byte aligned) are
-// staged in the thread's own LDS slot.
-template <bool RC>
+// staged in the thread's own LDS slot.  NP = 2: the segment's windows are
+// computed and emitted in two halves (half the records in registers, so
+// ~2x the waves per CU; the emission stage is then an LDS array of its own,
+// the rows being still in use); NP = 1: all 16 at once, the stage reusing
+// the rows.
+template <bool RC, int NP>
 __global__ void __launch_bounds__(IBLOCK)
 k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
             const unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift,
             TableView T, BinOut O) {
   static_assert(NQ == 64, "one wave scans the sub-queue counts");
+  static_assert(NP == 1 || NP == 2, "one or two parts");
+  if (PG_EXP_BITS & (1 << 19)) return;             // (experiment: no work pass)
+  constexpr int NX = IW / NP;
   // 64 staged bytes + 4 per thread: rows of 17 dwords, an odd stride, so the
   // rows' dword reads are bank-conflict free (80-byte rows were 4-way
   // conflicted: 1847 conflict cycles per wave, PMC); the realigning dword
   // reads past a row land in the next one, or read 0 past the allocation.
-  // 18.7 KiB in all, so that a work block fits beside 5 coverage blocks
-  // (5 x 27.8 KiB) of the next chunk on a CU's 160 KiB.
   constexpr int SROW = 68;
   static_assert(SROW % 8 == 4 && SROW >= 64, "odd dword stride, 64 staged bytes");
   __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][SROW];
+  __shared__ __attribute__((aligned(16))) uint8_t stage2[NP == 2 ? 12 * EST : 16];
   __shared__ unsigned long long s_pre[NQ + 1];
-  __shared__ uint32_t s_cnt[NBIN];
-  __shared__ unsigned long long s_base[NBIN];
+  __shared__ EmitLds<NX / ESUB> s_emit;
+  static_assert(sizeof(scratch) >= 12 * EST, "the emission stage reuses the segment rows");
+  uint8_t* const st = NP == 2 ? &stage2[0] : &scratch[0][0];
   if (threadIdx.x < 64) {
     const unsigned long long c = qcount[QSTRIDE * threadIdx.x];
     unsigned long long x = c;
@@ -1005,7 +1070,8 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
     }
     s_pre[threadIdx.x + 1] = x;                    // inclusive -> s_pre[j+1]
     if (threadIdx.x == 0) s_pre[0] = 0ull;
-    s_cnt[threadIdx.x] = 0u;
+#pragma unroll
+    for (int q = 0; q < NX / ESUB; ++q) s_emit.cnt[q][threadIdx.x] = 0u;
   }
   __syncthreads();
   uint8_t* slot = scratch[threadIdx.x];
@@ -1013,27 +1079,45 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
   for (unsigned long long i0 = (unsigned long long)blockIdx.x * IBLOCK; i0 < n;
        i0 += (unsigned long long)gridDim.x * IBLOCK) {          // block-uniform trip count
     const unsigned long long i = i0 + threadIdx.x;
-    uint64_t hh[IW];
-    uint32_t mm[IW];
+    uint64_t hh[NX], K = 0, Kr = 0;
+    uint32_t mm[NX];
+    WorkItem w{0, -1, 0, 0u, 0u};
+    long long aligned = 0;
     if (i < n) {
       int lo = 0;                                  // largest j with s_pre[j] <= i
 #pragma unroll
       for (int step = NQ / 2; step > 0; step >>= 1)
         if (s_pre[lo + step] <= i) lo += step;
-      const WorkItem w = queue[(unsigned long long)lo * qcap + (i - s_pre[lo])];
-      const long long from = w.rs + w.q0 - 2, aligned = from > 0 ? from & ~15ll : 0;
+      w = queue[(unsigned long long)lo * qcap + (i - s_pre[lo])];
+      const long long from = w.rs + w.q0 - 2;
+      aligned = from > 0 ? from & ~15ll : 0;
       uint32_t* s32 = reinterpret_cast<uint32_t*>(slot);          // (4-byte aligned rows)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint4 v = *reinterpret_cast<const uint4*>(cls + aligned + 16 * j);
         s32[4 * j] = v.x; s32[4 * j + 1] = v.y; s32[4 * j + 2] = v.z; s32[4 * j + 3] = v.w;
       }
-      segment_records<RC>(slot, w.rs - aligned, w.q0, w.last, k, shift, T, w.covered, hh, mm);
-    } else {
-#pragma unroll
-      for (int x = 0; x < IW; ++x) { hh[x] = 0; mm[x] = 0; }
     }
-    block_emit<IW>(O, hh, mm, s_cnt, s_base);
+    auto part = [&](auto P) {
+      constexpr int X0 = decltype(P)::value * NX;
+      if (i < n) {
+        segment_records<RC, X0, NX>(slot, w.rs - aligned, w.q0, w.last, k, shift, T, w.covered, K, Kr, hh, mm);
+      } else {
+#pragma unroll
+        for (int x = 0; x < NX; ++x) { hh[x] = 0; mm[x] = 0; }
+      }
+      if (PG_EXP_BITS & (1 << 18)) {                  // (experiment: no emission)
+        uint64_t acc = 0;
+#pragma unroll
+        for (int x = 0; x < NX; ++x) acc ^= hh[x] + mm[x];
+        if (acc == 42ull) O.flags[3] = 1u;
+      } else {
+        block_emit<NX>(O, hh, mm, s_emit, reinterpret_cast<unsigned long long*>(st),
+                       reinterpret_cast<uint32_t*>(st + 8 * EST));
+      }
+    };
+    part(std::integral_constant<int, 0>{});
+    if constexpr (NP == 2) part(std::integral_constant<int, 1>{});
   }
 }
 
@@ -1052,9 +1136,10 @@ __global__ void __launch_bounds__(IBLOCK)
 k_short_emit(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start,
              const long long* __restrict__ rec_len, const uint8_t* __restrict__ rec_flag, uint64_t R, int k,
              uint64_t shift, int rc, TableView T, BinOut O) {
-  __shared__ uint32_t s_cnt[NBIN];
-  __shared__ unsigned long long s_base[NBIN];
-  if (threadIdx.x < NBIN) s_cnt[threadIdx.x] = 0u;
+  __shared__ EmitLds<1> s_emit;
+  __shared__ unsigned long long st_key[EST];
+  __shared__ uint32_t st_mw[EST];
+  if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
   __syncthreads();
   for (uint64_t r0 = blockIdx.x * (uint64_t)IBLOCK; r0 < R; r0 += (uint64_t)gridDim.x * IBLOCK) {
     const uint64_t r = r0 + threadIdx.x;
@@ -1079,7 +1164,7 @@ k_short_emit(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_
         if (rc) short_strand(cls, rec_start[r], n, 1, k, shift, emit);
       }
     }
-    block_emit<4>(O, hh, mm, s_cnt, s_base);
+    block_emit<4>(O, hh, mm, s_emit, st_key, st_mw);
   }
 }
 
@@ -1091,9 +1176,10 @@ __global__ void k_set_flag(unsigned* flags) { atomicOr(flags, 1u); }
 // add_kmer would OR it (the sentinel sets the flag).
 __global__ void __launch_bounds__(IBLOCK)
 k_preload_emit(const PreEnt* __restrict__ e, uint64_t n, TableView T, BinOut O) {
-  __shared__ uint32_t s_cnt[NBIN];
-  __shared__ unsigned long long s_base[NBIN];
-  if (threadIdx.x < NBIN) s_cnt[threadIdx.x] = 0u;
+  __shared__ EmitLds<1> s_emit;
+  __shared__ unsigned long long st_key[EST];
+  __shared__ uint32_t st_mw[EST];
+  if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
   __syncthreads();
   for (uint64_t b = blockIdx.x * (uint64_t)(4 * IBLOCK); b < n; b += (uint64_t)gridDim.x * 4 * IBLOCK) {
     uint64_t hh[4];
@@ -1109,7 +1195,7 @@ k_preload_emit(const PreEnt* __restrict__ e, uint64_t n, TableView T, BinOut O) 
         else canon_record(T, x, e[i].mask & MASK12, hh[t], mm[t]);
       }
     }
-    block_emit<4>(O, hh, mm, s_cnt, s_base);
+    block_emit<4>(O, hh, mm, s_emit, st_key, st_mw);
   }
 }
 
@@ -1117,9 +1203,10 @@ k_preload_emit(const PreEnt* __restrict__ e, uint64_t n, TableView T, BinOut O) 
 // + 1 and the 26-bit mask word of both orientations.
 __global__ void __launch_bounds__(IBLOCK)
 k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
-  __shared__ uint32_t s_cnt[NBIN];
-  __shared__ unsigned long long s_base[NBIN];
-  if (threadIdx.x < NBIN) s_cnt[threadIdx.x] = 0u;
+  __shared__ EmitLds<1> s_emit;
+  __shared__ unsigned long long st_key[EST];
+  __shared__ uint32_t st_mw[EST];
+  if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
   __syncthreads();
   for (uint64_t b = blockIdx.x * (uint64_t)(4 * IBLOCK); b < n; b += (uint64_t)gridDim.x * 4 * IBLOCK) {
     uint64_t hh[4];
@@ -1134,7 +1221,7 @@ k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
         if (s.key1) { hh[t] = T.perm(s.key1 - 1ull); mm[t] = s.mask & (uint32_t)MW_MASK; }
       }
     }
-    block_emit<4>(O, hh, mm, s_cnt, s_base);
+    block_emit<4>(O, hh, mm, s_emit, st_key, st_mw);
   }
 }
 
@@ -1973,7 +2060,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
 
 // chunks of the tile list whose work pass overlaps the next coverage pass
 constexpr int K3_CHUNKS = (PG_EXP_BITS & 4096) ? 2 : (PG_EXP_BITS & 512) ? 4 : (PG_EXP_BITS & 1024) ? 5 : (PG_EXP_BITS & 2048) ? 6 : 3;
-constexpr int K3_WBLK = (PG_EXP_BITS & 8192) ? 3 : (PG_EXP_BITS & 16384) ? 1 : 2;                    // work blocks per CU (chunked form)
+constexpr int K3_WBLK = 4;                    // work blocks per CU (chunked form; pg_tune PG_TUNE_K3_WBLK)
 constexpr uint64_t K3_CHUNK_MIN = 1024;       // coverage groups per chunk below which one chunk runs
 
 static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, const BinOut& O) {
@@ -2027,7 +2114,8 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   c.t1.init();
   c.t1.start(s0);
   fl.launch(s0);
-  const unsigned wgrid = (unsigned)c.n_cu * K3_WBLK;
+  const unsigned wgrid = (unsigned)c.n_cu * (c.k3_wblk & 15 ? c.k3_wblk & 15 : K3_WBLK);
+  const unsigned wgrid_last = c.k3_wblk >> 4 ? (unsigned)c.n_cu * (c.k3_wblk >> 4) : wgrid;
   auto* q = c.k3_queue.as<WorkItem>();
   auto* qn = reinterpret_cast<unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes);
   const long long rfs = c.k3_ref >= 0 ? c.h_rec_start[c.k3_ref] : 0, rfn = c.k3_ref >= 0 ? c.h_rec_len[c.k3_ref] : 0;
@@ -2061,13 +2149,11 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
       PG_HIP(hipStreamWaitEvent(s1, c.ev[1 + i], 0));        // s1: work 0 .. i-1, then this
     }
     const uint64_t mi = std::min<uint64_t>(NQ * qcapc[i], c.windows_fw / IW + c.n_records + 1);
-    const unsigned gw = nch > 1 ? wgrid : grid_for(mi, IBLOCK, 16384);
-    if (rc0)
-      hipLaunchKernelGGL(k_emit_work<true>, dim3(gw), b, 0, ws, cls, qi, qni, (unsigned long long)qcapc[i], c.k, shift,
-                         c.tv, O);
-    else
-      hipLaunchKernelGGL(k_emit_work<false>, dim3(gw), b, 0, ws, cls, qi, qni, (unsigned long long)qcapc[i], c.k,
-                         shift, c.tv, O);
+    const unsigned gw = nch > 1 ? (i + 1 == nch ? wgrid_last : wgrid) : grid_for(mi, IBLOCK, 16384);
+    const bool halves = c.k3_emit != 1;
+    auto* kw = rc0 ? (halves ? k_emit_work<true, 2> : k_emit_work<true, 1>)
+                   : (halves ? k_emit_work<false, 2> : k_emit_work<false, 1>);
+    hipLaunchKernelGGL(kw, dim3(gw), b, 0, ws, cls, qi, qni, (unsigned long long)qcapc[i], c.k, shift, c.tv, O);
     PG_HIP(hipGetLastError());
   }
   const bool tail = part == SA_WHOLE || part == SA_TAIL;
