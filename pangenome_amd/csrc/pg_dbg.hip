@@ -90,13 +90,12 @@ __device__ int ovf_or(const TableView& T, uint64_t c, uint32_t mw, unsigned* fl)
 template <int ND>
 __device__ __forceinline__ void lds_bytes(const uint8_t* s, uint32_t idx, uint32_t (&out)[ND]) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(s + (idx & ~3u));
-  const uint32_t sh = (idx & 3u) * 8u;
+  const uint32_t sb = idx & 3u;
   uint32_t raw[ND + 1];
 #pragma unroll
   for (int i = 0; i <= ND; ++i) raw[i] = w[i];
 #pragma unroll
-  for (int i = 0; i < ND; ++i)
-    out[i] = sh ? (raw[i] >> sh) | (raw[i + 1] << (32u - sh)) : raw[i];
+  for (int i = 0; i < ND; ++i) out[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sb);   // one v_alignbyte each
 }
 template <int ND>
 __device__ __forceinline__ uint32_t byte_at(const uint32_t (&w)[ND], int j) {
@@ -663,7 +662,6 @@ k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, Wor
 // x 32 bytes per member) are staged on their own.
 constexpr int RPAD = 32;                      // s_ref front pad: quads reaching below the span stay in bounds
 constexpr int RSZ = RPAD + RSPAN + 32;        // + tail slack: a quad holding a staged byte never reads past it
-constexpr int ANCB = 48;                      // staged bytes per anchor (from its 16-byte aligned start)
 constexpr int NQD = CBLOCK + 2;               // quads per member: segment t reads quads t .. t+2
 typedef unsigned int u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
@@ -697,22 +695,44 @@ __device__ __forceinline__ uint32_t map_cover(uint32_t nz, int sh, int k) {
   const int ulo = max(0, first - k - 1), uhi = min(IW - 1, last);
   return ALL & ~(((2u << uhi) - 1u) & ~((1u << ulo) - 1u));
 }
-__device__ __forceinline__ void drift_task_anc(const uint8_t* s_anc, const uint8_t* s_ref, int ia, int ibhi, int lo,
-                                               int hi, int w, unsigned* best) {
-  drift_task(s_anc, s_ref, ia, ibhi, lo, hi, w, best);
+// drift_task for an anchor staged dword-aligned (A: its 32 bytes)
+__device__ __forceinline__ void drift_task_anc(const uint32_t* A, const uint8_t* s_ref, int ibhi, int lo, int hi, int w,
+                                               unsigned* best) {
+  const uint32_t* rw = reinterpret_cast<const uint32_t*>(s_ref);
+  const uint32_t x0 = A[0], x1 = A[1];
+  const uint32_t W0 = rw[w], W1 = rw[w + 1], W2 = rw[w + 2];
+  uint32_t hit = 0;
+#pragma unroll
+  for (int sb = 0; sb < 4; ++sb) {
+    const int ib = 4 * w + sb;
+    const bool h = (ib >= lo) & (ib <= hi) & (__builtin_amdgcn_alignbyte(W1, W0, sb) == x0) &
+                   (__builtin_amdgcn_alignbyte(W2, W1, sb) == x1);
+    hit |= (uint32_t)h << sb;
+  }
+  while (hit) {
+    const int ib = 4 * w + __builtin_ctz(hit);
+    hit &= hit - 1u;
+    uint32_t Bw[ALEN / 4];
+    lds_bytes(s_ref, (uint32_t)ib, Bw);
+    bool eq = true;
+#pragma unroll
+    for (int i = 2; i < ALEN / 4; ++i) eq &= Bw[i] == A[i];
+    const int d = ibhi - ib;
+    const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+    if (eq) atomicMin(best, (ad << 16) | (unsigned)d);
+  }
 }
-// cover_search on the staged anchors: member m's anchor ai is s_anc[m][ai],
-// its first byte at index (rs + a) & 15
+// cover_search on the staged anchors: member m's anchor ai is s_anc[m][ai]
+// (its 32 bytes, realigned to dwords when staged)
 // (Checking each triple's hint drift exactly first and searching only the
 // misses measured neutral: stage A 0.599 ms either way.)
-__device__ __forceinline__ void cover_search_q(uint8_t (*s_anc)[NANCH][ANCB], uint8_t (*s_ref)[RSZ],
+__device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4], uint8_t (*s_ref)[RSZ],
                                                const MemGeo* geo, const RefGeo& R0, const RefGeo& R1,
                                                unsigned (*best)[2][NANCH], long long qt, uint32_t dm0, uint32_t dm1) {
   constexpr int NT = QM * 2 * NANCH, PER = CBLOCK / 32;
   constexpr int NW = (2 * DRIFT + 3) / 4 + 2;
-  auto geom = [&](const RefGeo& R, const MemGeo& G, int ai, int& ia, int& ibhi, int& lo, int& hi) {
+  auto geom = [&](const RefGeo& R, const MemGeo& G, int ai, int& ibhi, int& lo, int& hi) {
     const long long a = qt + 8 + (long long)ai * ASTEP;
-    ia = (int)((G.rs + a) & 15);
     ibhi = (int)(R.rbase + a + DRIFT);
     lo = max(ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
     hi = a + ALEN > G.rn ? -1 : min(ibhi, (int)(R.rbase + R.phi) - ALEN);
@@ -723,12 +743,12 @@ __device__ __forceinline__ void cover_search_q(uint8_t (*s_anc)[NANCH][ANCB], ui
     const int m = t / (2 * NANCH), ri = (t / NANCH) & 1, ai = t % NANCH;
     if (t < NT && (((ri ? dm1 : dm0) >> m) & 1u)) {
       const MemGeo& G = geo[m];
-      int ia, ibhi, lo, hi;
-      geom(ri ? R1 : R0, G, ai, ia, ibhi, lo, hi);
+      int ibhi, lo, hi;
+      geom(ri ? R1 : R0, G, ai, ibhi, lo, hi);
       lo = max(lo, ibhi - (G.h[ri] + HWIN2));
       hi = min(hi, ibhi - (G.h[ri] - HWIN2));
       const int w = (lo >> 2) + l;
-      if (lo <= hi && 4 * w <= hi) drift_task_anc(s_anc[m][ai], s_ref[ri], ia, ibhi, lo, hi, w, &best[m][ri][ai]);
+      if (lo <= hi && 4 * w <= hi) drift_task_anc(s_anc[m][ai], s_ref[ri], ibhi, lo, hi, w, &best[m][ri][ai]);
     }
   }
   __syncthreads();
@@ -739,10 +759,10 @@ __device__ __forceinline__ void cover_search_q(uint8_t (*s_anc)[NANCH][ANCB], ui
     const MemGeo& G = geo[m];
 #pragma unroll 1
     for (int ai = 0; ai < NANCH; ++ai) {
-      int ia, ibhi, lo, hi;
-      geom(ri ? R1 : R0, G, ai, ia, ibhi, lo, hi);
+      int ibhi, lo, hi;
+      geom(ri ? R1 : R0, G, ai, ibhi, lo, hi);
       for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += CBLOCK)
-        drift_task_anc(s_anc[m][ai], s_ref[ri], ia, ibhi, lo, hi, w, &best[m][ri][ai]);
+        drift_task_anc(s_anc[m][ai], s_ref[ri], ibhi, lo, hi, w, &best[m][ri][ai]);
     }
   }
   __syncthreads();
@@ -756,7 +776,7 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
           int ref, long long rfs, long long rfn, int ref2, long long r2s, long long r2n, int* __restrict__ hints,
           int nrec, uint64_t ngroups, uint32_t b0, uint32_t b1, uint32_t bt) {
   __shared__ __attribute__((aligned(16))) uint8_t s_ref[2][RSZ];
-  __shared__ __attribute__((aligned(16))) uint8_t s_anc[QM][NANCH][ANCB];
+  __shared__ __attribute__((aligned(16))) uint32_t s_anc[QM][NANCH][ALEN / 4];
   __shared__ __attribute__((aligned(16))) uint4 s_xq[QM][2];       // member quads CBLOCK, CBLOCK+1
   __shared__ uint32_t s_nib[QM][NQD];                              // bit 4*(3*ri+j)+i: dword i, reference ri, drift j
   __shared__ unsigned s_best[QM][2][NANCH];
@@ -796,13 +816,22 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
 #pragma unroll
     for (int x = 1; x < QM; ++x) rs = m == x ? mrs[x] : rs;
     s_xq[m][t & 1] = quad_at(cls, 4 * ((rs + qt - 1) >> 2) + 16ll * (CBLOCK + (t & 1)), ncls, (dm0 >> m) & 1u);
-  } else if (t >= 64 && t < 64 + QM * NANCH * 3) { // anchors: 3 chunks of 16 bytes each
-    const int x = t - 64, m = x / (NANCH * 3), ai = (x / 3) % NANCH, c = x % 3;
+  } else if (t >= 64 && t < 64 + QM * NANCH) {     // anchors: 32 bytes each, realigned to dwords
+    const int x = t - 64, m = x / NANCH, ai = x % NANCH;
     long long rs = mrs[0];
 #pragma unroll
     for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
-    const long long a = ((rs + qt + 8 + (long long)ai * ASTEP) & ~15ll) + 16 * c;
-    *reinterpret_cast<uint4*>(&s_anc[m][ai][16 * c]) = quad_at(cls, a, ncls, (dm0 >> m) & 1u);
+    const long long a = rs + qt + 8 + (long long)ai * ASTEP, a4 = a & ~3ll;
+    const bool lv = (dm0 >> m) & 1u;
+    const uint4 q0 = quad_at(cls, a4, ncls, lv), q1 = quad_at(cls, a4 + 16, ncls, lv),
+                q2 = quad_at(cls, a4 + 32, ncls, lv);
+    const uint32_t r[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x};
+    const uint32_t sb = (uint32_t)(a & 3);
+    uint32_t o[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sb);
+    *reinterpret_cast<uint4*>(&s_anc[m][ai][0]) = make_uint4(o[0], o[1], o[2], o[3]);
+    *reinterpret_cast<uint4*>(&s_anc[m][ai][4]) = make_uint4(o[4], o[5], o[6], o[7]);
   } else if (t >= 160 && t < 160 + QM) {           // hints (per XCD, reference and record)
     const int m = t - 160;
     const TileDesc td = descs[QM * g + m];
@@ -818,7 +847,7 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
     G.h[1] = h1 < 0 ? DRIFT : h1;
     s_geo[m] = G;
   }
-  static_assert(2 * QM <= 64 && 64 + QM * NANCH * 3 <= 160 && 160 + QM <= 192 && 192 + QM * 2 * NANCH <= CBLOCK,
+  static_assert(2 * QM <= 64 && 64 + QM * NANCH <= 160 && 160 + QM <= 192 && 192 + QM * 2 * NANCH <= CBLOCK,
                 "thread ranges of the staging roles");
   if (t >= 192 && t < 192 + QM * 2 * NANCH) (&s_best[0][0][0])[t - 192] = ~0u;
   // the references' spans of this stripe: [qt-1-DRIFT, qt+TILE+k+1+DRIFT) clipped
