@@ -228,6 +228,9 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 /* PG_TUNE_K3_EMIT: form of the K3 work pass, 0 (default) = each queued
  * segment's records computed and emitted in two halves, 1 = at once. */
 #define PG_TUNE_K3_EMIT 12
+/* PG_TUNE_K3_TAIL: size of the last K3 chunk in 16ths of the others (1..64,
+ * 0 = 10: the work pass left behind the last coverage pass is smaller). */
+#define PG_TUNE_K3_TAIL 13
 /* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
  * count asks (0..8): exercises the overflow set, its spill and the re-run
  * with more buckets (results are unchanged). */

@@ -27,6 +27,7 @@ PG_TUNE_DEVICE_CAP = 9
 PG_TUNE_K3_COVER = 10
 PG_TUNE_K3_WBLK = 11
 PG_TUNE_K3_EMIT = 12
+PG_TUNE_K3_TAIL = 13
 
 
 class PgStats(C.Structure):

@@ -283,6 +283,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: K3 emit form must be 0 or 1");
         x->c.k3_emit = (int)value;
         break;
+      case PG_TUNE_K3_TAIL:
+        if (value < 0 || value > 64) throw pg::Error(PG_EINVAL, "pg_tune: K3 tail must be in [0, 64]");
+        x->c.k3_tail = (int)value;
+        break;
       case PG_TUNE_BUCKET_SHIFT:
         if (value < 0 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: bucket shift must be in [0, 8]");
         x->c.bb_shift = (int)value;

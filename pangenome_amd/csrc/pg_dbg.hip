@@ -2128,11 +2128,19 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   int nch = ntiles >= (uint64_t)K3_CHUNKS * K3_CHUNK_MIN ? K3_CHUNKS : 1;
   if (c.k3_chunks > 0) nch = std::min(6, c.k3_chunks);
   if (!ntiles) nch = 0;
+  // chunk i covers the fraction [cb[i], cb[i+1]) / cbt of every XCD's share:
+  // 16 parts each, the last chunk 10 (c.k3_tail: a smaller last chunk
+  // leaves a smaller work pass behind the last coverage pass: C3 stage A
+  // 0.566 / 0.568 / 0.581 ms at 10 / 12 / 8 against 0.586 at 16)
+  const uint32_t tailw = c.k3_tail ? (uint32_t)c.k3_tail : 10u;
+  uint32_t cb[8] = {};
+  for (int i = 1; i <= nch; ++i) cb[i] = cb[i - 1] + (i == nch ? tailw : 16u);
+  const uint32_t cbt = nch ? cb[nch] : 1u;
   uint64_t gc[8] = {}, qoff[8] = {}, qcapc[8] = {}, items = 0;
   for (int i = 0; i < nch; ++i) {
     for (int x = 0; x < 8; ++x) {
       uint64_t t, te;
-      xcd_chunk(ntiles, (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch, (uint64_t)x, t, te);
+      xcd_chunk(ntiles, cb[i], cb[i + 1], cbt, (uint64_t)x, t, te);
       gc[i] = std::max<uint64_t>(gc[i], 8 * (te - t));
     }
     qcapc[i] = (gc[i] + NQ - 1) / NQ * (QM * CBLOCK);   // per sub-queue: a block queues <= QM * CBLOCK
@@ -2165,11 +2173,11 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     if (gc[i] && c.k3_cover == 1)
       hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
                          c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
-                         (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch);
+                         cb[i], cb[i + 1], cbt);
     else if (gc[i])
       hipLaunchKernelGGL(k_cover_q, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, (uint64_t)c.cls.cap, td, qi, qni,
                          (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
-                         c.k3_hint.as<int>(), (int)c.n_records, ntiles, (uint32_t)i, (uint32_t)i + 1, (uint32_t)nch);
+                         c.k3_hint.as<int>(), (int)c.n_records, ntiles, cb[i], cb[i + 1], cbt);
     PG_HIP(hipGetLastError());
     hipStream_t ws = s1;
     if (nch > 1 && i + 1 == nch) {

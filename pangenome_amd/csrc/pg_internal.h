@@ -142,6 +142,7 @@ struct Ctx {
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
   int k3_wblk = 0;                // pg_tune: work blocks per CU, low 4 bits; last chunk's, high 4 bits (0 = 2)
   int k3_emit = 0;                // pg_tune: work pass (0 = two halves per segment, 1 = one)
+  int k3_tail = 0;                // pg_tune: last K3 chunk in 16ths of the others (0 = 16)
   int k3_cover = 0;               // pg_tune: coverage pass (0 = quad form, 1 = LDS-staged members)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
   int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
