@@ -726,29 +726,27 @@ __device__ __forceinline__ void drift_task_anc(const uint32_t* A, const uint8_t*
 // (its 32 bytes, realigned to dwords when staged)
 // (Checking each triple's hint drift exactly first and searching only the
 // misses measured neutral: stage A 0.599 ms either way.)
+// Search geometry of one (member, reference, anchor) triple, computed once
+// per block in the staging phase: ibhi = the reference index of drift 0's
+// candidate + DRIFT; [lo, hi] the full search range, [lo1, hi1] its part
+// within the hint window (empty if the triple does not dedup).
+struct TriGeo {
+  int ibhi, lo, hi, lo1, hi1;
+};
 __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4], uint8_t (*s_ref)[RSZ],
-                                               const MemGeo* geo, const RefGeo& R0, const RefGeo& R1,
-                                               unsigned (*best)[2][NANCH], long long qt, uint32_t dm0, uint32_t dm1) {
+                                               const TriGeo* tri, unsigned (*best)[2][NANCH], uint32_t dm0,
+                                               uint32_t dm1) {
   constexpr int NT = QM * 2 * NANCH, PER = CBLOCK / 32;
   constexpr int NW = (2 * DRIFT + 3) / 4 + 2;
-  auto geom = [&](const RefGeo& R, const MemGeo& G, int ai, int& ibhi, int& lo, int& hi) {
-    const long long a = qt + 8 + (long long)ai * ASTEP;
-    ibhi = (int)(R.rbase + a + DRIFT);
-    lo = max(ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
-    hi = a + ALEN > G.rn ? -1 : min(ibhi, (int)(R.rbase + R.phi) - ALEN);
-  };
 #pragma unroll 1
   for (int t0 = 0; t0 < NT; t0 += PER) {
     const int t = t0 + ((int)threadIdx.x >> 5), l = (int)threadIdx.x & 31;
-    const int m = t / (2 * NANCH), ri = (t / NANCH) & 1, ai = t % NANCH;
-    if (t < NT && (((ri ? dm1 : dm0) >> m) & 1u)) {
-      const MemGeo& G = geo[m];
-      int ibhi, lo, hi;
-      geom(ri ? R1 : R0, G, ai, ibhi, lo, hi);
-      lo = max(lo, ibhi - (G.h[ri] + HWIN2));
-      hi = min(hi, ibhi - (G.h[ri] - HWIN2));
-      const int w = (lo >> 2) + l;
-      if (lo <= hi && 4 * w <= hi) drift_task_anc(s_anc[m][ai], s_ref[ri], ibhi, lo, hi, w, &best[m][ri][ai]);
+    if (t < NT) {
+      const int m = t / (2 * NANCH), ri = (t / NANCH) & 1, ai = t % NANCH;
+      const TriGeo g = tri[t];
+      const int w = (g.lo1 >> 2) + l;
+      if (g.lo1 <= g.hi1 && 4 * w <= g.hi1)
+        drift_task_anc(s_anc[m][ai], s_ref[ri], g.ibhi, g.lo1, g.hi1, w, &best[m][ri][ai]);
     }
   }
   __syncthreads();
@@ -756,13 +754,11 @@ __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4
   for (int p = 0; p < 2 * QM; ++p) {                          // block-uniform
     const int m = p >> 1, ri = p & 1;
     if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
-    const MemGeo& G = geo[m];
 #pragma unroll 1
     for (int ai = 0; ai < NANCH; ++ai) {
-      int ibhi, lo, hi;
-      geom(ri ? R1 : R0, G, ai, ibhi, lo, hi);
-      for (int w = (lo >> 2) + (int)threadIdx.x; 4 * w <= hi && w < (lo >> 2) + NW; w += CBLOCK)
-        drift_task_anc(s_anc[m][ai], s_ref[ri], ibhi, lo, hi, w, &best[m][ri][ai]);
+      const TriGeo g = tri[(m * 2 + ri) * NANCH + ai];
+      for (int w = (g.lo >> 2) + (int)threadIdx.x; 4 * w <= g.hi && w < (g.lo >> 2) + NW; w += CBLOCK)
+        drift_task_anc(s_anc[m][ai], s_ref[ri], g.ibhi, g.lo, g.hi, w, &best[m][ri][ai]);
     }
   }
   __syncthreads();
@@ -784,12 +780,26 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
   __shared__ unsigned long long s_qbase;
   __shared__ MemGeo s_geo[QM];
   __shared__ Drifts s_dr[QM][2];
+  __shared__ TriGeo s_tri[QM * 2 * NANCH];
   uint64_t g, ge;
   xcd_chunk(ngroups, b0, b1, bt, blockIdx.x & 7, g, ge);
   g += blockIdx.x >> 3;
   if (g >= ge) return;                             // (block-uniform, before any barrier)
   const int t = (int)threadIdx.x;
   const long long qt = (long long)descs[QM * g].stripe * TILE;
+  // the references' spans of this stripe: [qt-1-DRIFT, qt+TILE+k+1+DRIFT) clipped
+  RefGeo rg[2];
+  long long ra0[2], rend[2];
+#pragma unroll
+  for (int ri = 0; ri < 2; ++ri) {
+    const long long s = ri ? r2s : rfs, n = ri ? r2n : rfn;
+    rg[ri].plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
+    rg[ri].phi = qt + TILE + k + 1 + DRIFT < n ? qt + TILE + k + 1 + DRIFT : n;
+    rg[ri].rfn = n;
+    ra0[ri] = (s + rg[ri].plo) & ~15ll;
+    rend[ri] = s + rg[ri].phi;
+    rg[ri].rbase = s - ra0[ri] + RPAD;
+  }
   // the members (uniform loads): records, which members dedup
   long long mrs[QM], mrn[QM];
   uint32_t dm0 = 0, dm1 = 0, live = 0;
@@ -832,36 +842,37 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
     for (int i = 0; i < 8; ++i) o[i] = __builtin_amdgcn_alignbyte(r[i + 1], r[i], sb);
     *reinterpret_cast<uint4*>(&s_anc[m][ai][0]) = make_uint4(o[0], o[1], o[2], o[3]);
     *reinterpret_cast<uint4*>(&s_anc[m][ai][4]) = make_uint4(o[4], o[5], o[6], o[7]);
-  } else if (t >= 160 && t < 160 + QM) {           // hints (per XCD, reference and record)
+  } else if (t >= 160 && t < 160 + QM) {           // the members' records
     const int m = t - 160;
     const TileDesc td = descs[QM * g + m];
-    int* hx = hints + (size_t)(blockIdx.x & 7) * 2 * nrec;
-    const int h0 = ((dm0 >> m) & 1u) ? hx[td.r] : -1;
-    const int h1 = ((dm1 >> m) & 1u) ? hx[nrec + td.r] : -1;
     MemGeo G;
     G.r = td.r;
     G.rs = td.rs;
     G.rn = td.rn;
     G.a0 = G.hi = 0;
-    G.h[0] = h0 < 0 ? DRIFT : h0;
-    G.h[1] = h1 < 0 ? DRIFT : h1;
+    G.h[0] = G.h[1] = 0;
     s_geo[m] = G;
   }
   static_assert(2 * QM <= 64 && 64 + QM * NANCH <= 160 && 160 + QM <= 192 && 192 + QM * 2 * NANCH <= CBLOCK,
                 "thread ranges of the staging roles");
-  if (t >= 192 && t < 192 + QM * 2 * NANCH) (&s_best[0][0][0])[t - 192] = ~0u;
-  // the references' spans of this stripe: [qt-1-DRIFT, qt+TILE+k+1+DRIFT) clipped
-  RefGeo rg[2];
-  long long ra0[2], rend[2];
-#pragma unroll
-  for (int ri = 0; ri < 2; ++ri) {
-    const long long s = ri ? r2s : rfs, n = ri ? r2n : rfn;
-    rg[ri].plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
-    rg[ri].phi = qt + TILE + k + 1 + DRIFT < n ? qt + TILE + k + 1 + DRIFT : n;
-    rg[ri].rfn = n;
-    ra0[ri] = (s + rg[ri].plo) & ~15ll;
-    rend[ri] = s + rg[ri].phi;
-    rg[ri].rbase = s - ra0[ri] + RPAD;
+  if (t >= 192 && t < 192 + QM * 2 * NANCH) {     // triples: search geometry around the hint (per XCD,
+                                                   // reference and record)
+    const int x = t - 192, m = x / (2 * NANCH), ri = (x / NANCH) & 1, ai = x % NANCH;
+    (&s_best[0][0][0])[x] = ~0u;
+    TriGeo G{0, 0, -1, 0, -1};
+    if ((((ri ? dm1 : dm0) >> m) & 1u)) {
+      const TileDesc td = descs[QM * g + m];
+      const int hh = hints[(size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + td.r];
+      const int h = hh < 0 ? DRIFT : hh;
+      const RefGeo& R = ri ? rg[1] : rg[0];
+      const long long a = qt + 8 + (long long)ai * ASTEP;
+      G.ibhi = (int)(R.rbase + a + DRIFT);
+      G.lo = max(G.ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
+      G.hi = a + ALEN > td.rn ? -1 : min(G.ibhi, (int)(R.rbase + R.phi) - ALEN);
+      G.lo1 = max(G.lo, G.ibhi - (h + HWIN2));
+      G.hi1 = min(G.hi, G.ibhi - (h - HWIN2));
+    }
+    s_tri[x] = G;
   }
   {
     static_assert(RSPAN <= 2 * CBLOCK * 16, "two chunks per thread");
@@ -883,12 +894,7 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
     }
   }
   __syncthreads();
-  if (dm0 && !(PG_EXP_BITS & (1 << 20)))
-    cover_search_q(s_anc, s_ref, s_geo, rg[0], rg[1], s_best, qt, dm0, dm1);
-  if ((PG_EXP_BITS & (1 << 20)) && t < 2 * QM) {   // (experiment: the hint as the only drift)
-    const int m = t >> 1, ri = t & 1;
-    for (int ai = 0; ai < NANCH; ++ai) s_best[m][ri][ai] = (unsigned)s_geo[m].h[ri];
-  }
+  if (dm0) cover_search_q(s_anc, s_ref, s_tri, s_best, dm0, dm1);
   // hints and drift sets: one lane per (member, reference); a drift set's
   // offsets index s_ref from thread 0's quad (add 16 t)
   if (t < 2 * QM) {
