@@ -750,10 +750,12 @@ __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4
     }
   }
   __syncthreads();
+  bool full = false;                                          // (block-uniform; rare: no barrier without it)
 #pragma unroll 1
-  for (int p = 0; p < 2 * QM; ++p) {                          // block-uniform
+  for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
     if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
+    full = true;
 #pragma unroll 1
     for (int ai = 0; ai < NANCH; ++ai) {
       const TriGeo g = tri[(m * 2 + ri) * NANCH + ai];
@@ -761,7 +763,7 @@ __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4
         drift_task_anc(s_anc[m][ai], s_ref[ri], g.ibhi, g.lo, g.hi, w, &best[m][ri][ai]);
     }
   }
-  __syncthreads();
+  if (full) __syncthreads();
 }
 
 // (8 waves per SIMD: 78 SGPRs with 24 spilled to VGPR lanes, against 106 and
@@ -922,12 +924,13 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
           if (j >= nd) break;
           const int off = __builtin_amdgcn_readfirstlane(s_dr[m][ri].off[j]);
           w |= quad_nib(s_ref[ri], off + 16 * t, Mq[m]) << (4 * (3 * ri + j));
-          if (t < 2) wx |= quad_nib(s_ref[ri], off + 16 * (CBLOCK + t), s_xq[m][t]) << (4 * (3 * ri + j));
+          if (t >= CBLOCK - 2)                     // (the last wave: wave 0 computes the drift sets)
+            wx |= quad_nib(s_ref[ri], off + 16 * (t + 2), s_xq[m][t - (CBLOCK - 2)]) << (4 * (3 * ri + j));
         }
       }
     }
     s_nib[m][t] = w;
-    if (t < 2) s_nib[m][CBLOCK + t] = wx;
+    if (t >= CBLOCK - 2) s_nib[m][t + 2] = wx;
   }
   __syncthreads();
   const long long q0 = qt + (long long)t * IW;
