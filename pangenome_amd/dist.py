@@ -226,6 +226,16 @@ def stream_chunks(flags, seq_len, limit: int) -> list:
     return res
 
 
+def sublog_count(world: int, rounds: int, subparts=None) -> int:
+    """The owner's sub-log count P of exchange_stream: `subparts` or the round
+    count, rounded up to a power of two, but never past the largest power of
+    two with world x P <= 64 (pg_dbg_partition's part limit; world 3: 16)."""
+    P, want, cap = 1, max(1, subparts or rounds), 64 // max(1, world)
+    while P < want and P * 2 <= cap:
+        P *= 2
+    return P
+
+
 def _free_device_bytes(device) -> int:
     import torch
     if _is_cuda(device):
@@ -265,9 +275,7 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
     nch = torch.tensor([len(chunks)], dtype=torch.int64, device=comm)
     dist.all_reduce(nch, op=dist.ReduceOp.MAX, group=group)
     rounds = max(1, int(nch.item()))
-    P = 1
-    while P < min(64 // max(1, world), subparts or rounds):
-        P *= 2
+    P = sublog_count(world, rounds, subparts)
     if compact_at is None:
         compact_at = max(1 << 20, _free_device_bytes(device) // 4 // 16)
     logs = [[] for _ in range(P)]
@@ -300,13 +308,15 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
             on_chunk()
         recv, sub, s, _ = _route(shard, world, device, group, subparts=P)
         sent += s
-        # each source's run arrives as its P sub-log runs: views, no gather
+        # each source's run arrives as its P sub-log runs; with P > 1 each run
+        # is copied out, so that compacting one sub-log frees its memory (a
+        # view would keep the whole round's receive buffer alive)
         off = 0
         for src in range(sub.shape[0]):
             for p in range(P):
                 m = int(sub[src, p])
                 if m:
-                    logs[p].append(recv[off:off + m])
+                    logs[p].append(recv[off:off + m].clone() if P > 1 else recv[off:off + m])
                     logn[p] += m
                 off += m
         del recv

@@ -75,3 +75,50 @@ def test_sharded_exchange_matches_single_process(oracle_mod, world, a2a_rows):
         assert n_rdbg == ref_rdbg
     # owners hold disjoint partitions
     assert sum(out[r][2] for r in range(world)) == ref_rdbg
+
+
+def _stream_worker(rank, world, port, q, fasta, k):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from dist_util import OracleShard
+    from pangenome_amd.dist import exchange_stream, stream_chunks
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    recs = _records(fasta)
+    per = -(-len(recs) // world)
+    mine = b"".join(r if r.endswith(b"\n") else r + b"\n" for r in recs[rank * per:(rank + 1) * per])
+    sh = OracleShard(k)
+    meta = sh.load(np.frombuffer(mine, np.uint8))
+    R = int(meta["seq_len"].shape[0])
+    chunks = stream_chunks(np.ones(R, np.uint8), meta["seq_len"], 1)     # one record per round
+    res = exchange_stream(sh, world, rank, "cpu", chunks, R, True, compact_at=1)
+    q.put((rank, res[:5]))
+    dist.destroy_process_group()
+
+
+def test_streamed_exchange_many_rounds_world3(oracle_mod):
+    """World 3 with 18 rounds: the sub-log count stays within world x P <= 64
+    (P = 16, not the 32 that rounding 18 up would give: pg_dbg_partition
+    takes at most 64 parts)."""
+    from dist_util import spawn_ranks
+    from pangenome_amd import synth
+    k = 27
+    fasta = synth.pangenome(54, 2_000, snp=0.01, indel=1e-3, seed=43)
+    ref = oracle_mod.OracleRun(fasta, k, 2)
+    out = spawn_ranks(3, _stream_worker, (fasta, k))
+    for r in range(3):
+        n_dbg, n_rdbg, _, _, rounds = out[r]
+        assert rounds == 18
+        assert (n_dbg, n_rdbg) == (ref.dbg()[0].shape[0], ref.rdbg().shape[0])
+    assert sum(out[r][2] for r in range(3)) == ref.rdbg().shape[0]
+
+
+@pytest.mark.parametrize("world,rounds,subparts,want", [(1, 3, None, 4), (3, 17, None, 16), (3, 18, None, 16),
+                                                        (5, 9, None, 8), (6, 9, None, 8), (8, 4, None, 4),
+                                                        (8, 40, None, 8), (3, 2, 64, 16), (2, 1, None, 1)])
+def test_sublog_count(world, rounds, subparts, want):
+    from pangenome_amd.dist import sublog_count
+    P = sublog_count(world, rounds, subparts)
+    assert P == want and world * P <= 64 and P & (P - 1) == 0

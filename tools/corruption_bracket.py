@@ -1,0 +1,124 @@
+"""Development: bracket round 3's two silent corruptions on one MI355X.
+
+1. RCCL all_to_all to self (world 1): at which message size does the receive
+   buffer differ from what was sent?  Tried for all_to_all_single and
+   all_to_all(list), in int64 and uint8 elements (a byte limit and an element
+   limit then fail at different sizes), against a plain device copy of the
+   same size.  For a failing case the first differing byte offset and the
+   number of differing bytes are printed.
+2. The sub-log split round 3 removed from dist.exchange_stream:
+   recv[torch.argsort(sub, stable=True)] with sub = a hash of the key word,
+   on (n, 2) int64 rows, checked against numpy on the host.
+
+    python tools/corruption_bracket.py [a2a|sort|all] > out.json
+One JSON line per case on stdout.
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+GiB = 1 << 30
+
+
+def emit(**kw):
+    print(json.dumps(kw), flush=True)
+
+
+def fill(nbytes, dev):
+    """A byte pattern where every 8-byte word is its own index (so a shifted or
+    missing piece never matches by accident)."""
+    w = (nbytes + 7) // 8
+    t = torch.arange(w, dtype=torch.int64, device=dev)
+    t.mul_(0x9E3779B97F4A7C15 - (1 << 64)).add_(12345)
+    return t.view(torch.uint8)[:nbytes]
+
+
+def diff(a, b):
+    ne = a != b
+    n = int(ne.sum())
+    if not n:
+        return 0, -1, -1
+    u = ne.to(torch.uint8)
+    first = int(torch.argmax(u))
+    last = u.numel() - 1 - int(torch.argmax(torch.flip(u, (0,))))
+    return n, first, last
+
+
+def a2a_cases(dev):
+    sizes = [GiB - 4096, GiB, GiB + 4096, GiB + GiB // 2, 2 * GiB - 4096, 2 * GiB, 2 * GiB + 4096, 3 * GiB]
+    for nbytes in sizes:
+        src = fill(nbytes, dev)
+        for dt, es in (("int64", 8), ("uint8", 1)):
+            n = nbytes // es
+            s = src[:n * es].view(torch.int64 if dt == "int64" else torch.uint8)
+            for op in ("all_to_all_single", "all_to_all_list", "copy"):
+                r = torch.full_like(s, 0x5A if dt == "uint8" else 0x5A5A5A5A5A5A5A5A)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                if op == "all_to_all_single":
+                    dist.all_to_all_single(r, s, output_split_sizes=[n], input_split_sizes=[n])
+                elif op == "all_to_all_list":
+                    dist.all_to_all([r], [s])
+                else:
+                    r.copy_(s)
+                torch.cuda.synchronize()
+                dt_s = time.perf_counter() - t0
+                bad, first, last = diff(r.view(torch.uint8), s.view(torch.uint8))
+                emit(case="a2a", op=op, dtype=dt, elements=n, bytes=n * es, ok=bad == 0, bad_bytes=bad,
+                     first_bad_byte=first, last_bad_byte=last, ms=round(1e3 * dt_s, 2))
+                del r
+        del src
+        torch.cuda.empty_cache()
+
+
+def sort_cases(dev):
+    golden = -7046029254386353131                     # 0x9E3779B97F4A7C15 as int64 (wrapping multiply)
+    for rows in (1 << 26, 1 << 27, 125_000_000, 140_000_000, 1 << 28):
+        host = np.random.default_rng(rows).integers(0, 1 << 62, size=(rows, 2), dtype=np.int64)
+        t = torch.from_numpy(host).to(dev)
+        for nsub in (4, 16):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sub = ((t[:, 0] * golden) >> 20) & (nsub - 1)
+            idx = torch.argsort(sub, stable=True)
+            out = t[idx]
+            torch.cuda.synchronize()
+            ms = 1e3 * (time.perf_counter() - t0)
+            with np.errstate(over="ignore"):
+                hsub = ((host[:, 0] * np.int64(golden)) >> 20) & (nsub - 1)
+            hidx = np.argsort(hsub, kind="stable")
+            idx_ok = bool(np.array_equal(idx.cpu().numpy(), hidx))
+            sub_ok = bool(np.array_equal(sub.cpu().numpy(), hsub))
+            o = out.cpu().numpy()
+            ref = host[hidx]
+            ne = np.flatnonzero((o != ref).any(axis=1))
+            emit(case="sort", rows=rows, bytes=16 * rows, nsub=nsub, sub_ok=sub_ok, argsort_ok=idx_ok,
+                 gather_ok=ne.shape[0] == 0, bad_rows=int(ne.shape[0]),
+                 first_bad_row=int(ne[0]) if ne.shape[0] else -1, ms=round(ms, 2))
+            del sub, idx, out, o, ref
+        del t, host
+        torch.cuda.empty_cache()
+
+
+def main():
+    what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29547"))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    emit(case="env", torch=torch.__version__, hip=torch.version.hip,
+         rccl=".".join(map(str, torch.cuda.nccl.version())), device=torch.cuda.get_device_name(0))
+    if what in ("a2a", "all"):
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+        a2a_cases(dev)
+        dist.destroy_process_group()
+    if what in ("sort", "all"):
+        sort_cases(dev)
+
+
+if __name__ == "__main__":
+    main()
