@@ -217,9 +217,11 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * next chunk's coverage pass, 1..6, or 0 = by tile count (3 when the list
  * has >= 3072 coverage groups, else 1). */
 #define PG_TUNE_K3_CHUNKS 1
-/* PG_TUNE_K3_COVER: form of the K3 coverage pass, 0 (default) = members
- * compared quad by quad from registers, 1 = members staged in LDS (round 2);
- * the results are the same, only the records left to the work pass differ. */
+/* PG_TUNE_K3_COVER: form of the K3 coverage pass, 0 (default) = K1's packed
+ * 2-bit base stream compared word by word, exact per base (round 4); 1 =
+ * class bytes staged in LDS (round 2); 2 = class bytes compared 16 at a time
+ * from registers, per dword (round 3).  The results are the same, only the
+ * records left to the work pass differ. */
 #define PG_TUNE_K3_COVER 10
 /* PG_TUNE_K3_WBLK: blocks per CU of the K3 work passes when the tile list
  * runs in chunks: low 4 bits for every chunk but the last, high 4 bits for

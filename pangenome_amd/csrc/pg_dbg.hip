@@ -973,6 +973,365 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
     if ((wmask >> m) & 1u) queue[sub * qcap + s_qbase + pos++] = WorkItem{mrs[m], mrn[m] - k, q0, cov[m], 0u};
 }
 
+// ---- K3 coverage pass, packed form (the default; north_star's "2-bit
+// encode ... packed base stream").  Same groups, drift search and coverage
+// rule as k_cover_q, on K1's packed stream (16 bases per 32-bit word, 2 bits
+// each) instead of the class bytes:
+//  * wave m of the block is member m; lane l owns the member's windows
+//    64 l .. 64 l + 63 (4 segments) and loads the 7 words that hold their
+//    context bases straight from HBM (0.44 B per base where the class stream
+//    costs 1 B), with the exception bytes of those words;
+//  * the two references' spans are staged in LDS as words (1.4 KB each);
+//  * per (reference, drift) the lane XORs its words with the reference words
+//    at that drift (three ds_read_b128 and one v_alignbit per word), turns
+//    the 2-bit differences into one mismatch bit per base, and smears it over
+//    each window's k+2 context bases (log2 steps of v_alignbit + OR): a window
+//    is covered iff its smear bit is clear.  That is the coverage rule at base
+//    granularity, exact where the quad form resolves it per dword (4 bases),
+//    so no more windows go to the work pass than there;
+//  * exceptions: a 2-bit code equals the class only for ACGT, so a lane whose
+//    context words hold any base that is not ACGT (K1's exception bytes) is
+//    not covered, and a reference whose staged span holds one is not used for
+//    the stripe (the work pass then emits those windows exactly, as it does
+//    every uncovered window);
+//  * the drift search compares each anchor's 32 bases as two words, 16
+//    candidate offsets per lane and reference word, 8 lanes per triple.
+constexpr int RPADW = 4;                          // s_ref words in front of the staged span
+constexpr int RSTAGEW = (RSPAN + 15) / 16 + 2;    // staged words per reference (<=)
+constexpr int RDW = (RPADW + RSTAGEW + 16 + 3) / 4 * 4;   // + tail: a lane's 12-word read stays inside
+constexpr int LW = 7;                             // packed words per lane: 64 windows + k+1 bases, any alignment
+static_assert(IW * 4 == 64 && CBLOCK == 64 * QM, "a lane owns 4 segments; a wave owns a member");
+
+struct Drifts2 {
+  int n;
+  int U[NANCH], lo[NANCH], hi[NANCH];             // U: s_ref base index of the member's word-grid base
+};
+// the drift set of one (member, reference): drifts_of's rule, with U = the
+// s_ref base index that member base 16 D (record position pos16) maps to
+__device__ __forceinline__ Drifts2 drifts_p(const unsigned* s_best, long long qt, long long pos16, long long rbase,
+                                            long long rfn, long long plo, long long phi, int k) {
+  Drifts2 D;
+  D.n = 0;
+#pragma unroll
+  for (int j = 0; j < NANCH; ++j) D.U[j] = D.lo[j] = D.hi[j] = 0;
+  const long long pl = plo + 1 > 1 ? plo + 1 : 1;
+  const long long ph = rfn - k - IW < phi - IW - k ? rfn - k - IW : phi - IW - k;
+#pragma unroll
+  for (int ai = 0; ai < NANCH; ++ai) {
+    const unsigned b = s_best[ai];
+    if (b == ~0u) continue;
+    const int d = (int)(b & 0xFFFFu) - DRIFT;
+    const int u = (int)(rbase + pos16 - d);
+    bool dup = false;
+#pragma unroll
+    for (int j = 0; j < ai; ++j) dup |= j < D.n && D.U[j] == u;
+    if (dup) continue;
+    const long long lo = pl + d - qt, hi = ph + d - qt;
+    const int l32 = (int)(lo < -(1ll << 30) ? -(1ll << 30) : lo), h32 = (int)(hi > (1ll << 30) ? (1ll << 30) : hi);
+#pragma unroll
+    for (int j = 0; j <= ai; ++j)
+      if (j == D.n) { D.lo[j] = l32; D.hi[j] = h32; D.U[j] = u; }
+    ++D.n;
+  }
+  return D;
+}
+
+__device__ __forceinline__ uint32_t p2_word(const uint32_t* p2, long long i, uint64_t n_p2) {
+  return (i >= 0 && (uint64_t)i < n_p2) ? p2[i] : 0u;
+}
+// candidates ib = 16 w .. 16 w + 15 (s_ref base indices) of the anchor (A0, A1)
+// within [lo, hi]: its 32 bases against the reference's 32 from ib
+__device__ __forceinline__ void drift_task_p(uint32_t A0, uint32_t A1, const uint32_t* R, int ibhi, int lo, int hi,
+                                             int w, unsigned* best) {
+  const uint32_t W0 = R[w], W1 = R[w + 1], W2 = R[w + 2];
+  uint32_t hit = 0;
+#pragma unroll
+  for (int sb = 0; sb < 16; ++sb) hit |= (uint32_t)(__builtin_amdgcn_alignbit(W1, W0, 2 * sb) == A0) << sb;
+  const int l = lo - 16 * w, h = hi - 16 * w;
+  const uint32_t top = h >= 15 ? 0xFFFFu : h < 0 ? 0u : (2u << h) - 1u;
+  const uint32_t bot = l <= 0 ? 0u : l > 15 ? 0xFFFFu : (1u << l) - 1u;
+  hit &= top & ~bot;
+  while (hit) {
+    const int sb = __builtin_ctz(hit);
+    hit &= hit - 1u;
+    if (__builtin_amdgcn_alignbit(W2, W1, 2 * sb) == A1) {
+      const int d = ibhi - (16 * w + sb);
+      const unsigned ad = (unsigned)(d > DRIFT ? d - DRIFT : DRIFT - d);
+      atomicMin(best, (ad << 16) | (unsigned)d);
+    }
+  }
+}
+__device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2], const uint32_t (*s_ref)[RDW],
+                                               const TriGeo* tri, unsigned (*best)[2][NANCH], uint32_t dm0,
+                                               uint32_t dm1) {
+  constexpr int NT = QM * 2 * NANCH;
+  static_assert(NT * 8 <= CBLOCK && 2 * HWIN2 + 1 + 15 <= 8 * 16, "one round of 8 lanes per triple");
+  const int t = (int)threadIdx.x;
+  {
+    const int tr = t >> 3, sub = t & 7;
+    if (tr < NT) {
+      const int m = tr / (2 * NANCH), ri = (tr / NANCH) & 1, ai = tr % NANCH;
+      const TriGeo g = tri[tr];
+      const int w = (g.lo1 >> 4) + sub;
+      if (g.lo1 <= g.hi1 && 16 * w <= g.hi1)
+        drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo1, g.hi1, w, &best[m][ri][ai]);
+    }
+  }
+  __syncthreads();
+  bool full = false;                                          // (block-uniform; rare)
+#pragma unroll 1
+  for (int p = 0; p < 2 * QM; ++p) {
+    const int m = p >> 1, ri = p & 1;
+    if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
+    full = true;
+#pragma unroll 1
+    for (int ai = 0; ai < NANCH; ++ai) {
+      const TriGeo g = tri[(m * 2 + ri) * NANCH + ai];
+      for (int w = (g.lo >> 4) + t; 16 * w <= g.hi; w += CBLOCK)
+        drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo, g.hi, w, &best[m][ri][ai]);
+    }
+  }
+  if (full) __syncthreads();
+}
+
+// 8 words of s_ref from word index idx (idx & 3 the same on every lane: a
+// scalar branch picks them out of three aligned 16-byte reads)
+__device__ __forceinline__ void lds_words8(const uint32_t* R, int idx, uint32_t (&out)[8]) {
+  const uint4* r16 = reinterpret_cast<const uint4*>(R);
+  uint32_t raw[12];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    uint4 v = r16[(idx >> 2) + q];
+    asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+    raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
+  }
+  auto take = [&](auto W) {
+    constexpr int w = decltype(W)::value;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) out[i] = raw[w + i];
+  };
+  switch (__builtin_amdgcn_readfirstlane(idx & 3)) {
+    case 0: take(std::integral_constant<int, 0>{}); break;
+    case 1: take(std::integral_constant<int, 1>{}); break;
+    case 2: take(std::integral_constant<int, 2>{}); break;
+    default: take(std::integral_constant<int, 3>{}); break;
+  }
+}
+// the even bits of x (one per 2-bit base) compressed into 16 bits
+__device__ __forceinline__ uint32_t even_bits(uint32_t x) {
+  x = (x | (x >> 1)) & 0x33333333u;
+  x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+  x = (x | (x >> 4)) & 0x00FF00FFu;
+  return (x | (x >> 8)) & 0x0000FFFFu;
+}
+
+__global__ void __launch_bounds__(CBLOCK, 8)
+k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint64_t n_p2,
+          const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue, unsigned long long* __restrict__ qcount,
+          unsigned long long qcap, int k, int ref, long long rfs, long long rfn, int ref2, long long r2s,
+          long long r2n, int* __restrict__ hints, int nrec, uint64_t ngroups, uint32_t b0, uint32_t b1, uint32_t bt) {
+  __shared__ __attribute__((aligned(16))) uint32_t s_ref[2][RDW];
+  __shared__ uint32_t s_anc[QM][NANCH][2];
+  __shared__ unsigned s_best[QM][2][NANCH];
+  __shared__ uint32_t s_scan[CBLOCK / 64];
+  __shared__ unsigned long long s_qbase;
+  __shared__ Drifts2 s_dr[QM][2];
+  __shared__ TriGeo s_tri[QM * 2 * NANCH];
+  __shared__ uint32_t s_rexc;
+  uint64_t g, ge;
+  xcd_chunk(ngroups, b0, b1, bt, blockIdx.x & 7, g, ge);
+  g += blockIdx.x >> 3;
+  if (g >= ge) return;                             // (block-uniform, before any barrier)
+  const int t = (int)threadIdx.x;
+  const long long qt = (long long)descs[QM * g].stripe * TILE;
+  // the references' spans of this stripe: [qt-1-DRIFT, qt+TILE+k+1+DRIFT) clipped, staged as the words
+  // from rd0 (s_ref word RPADW); rbase = the s_ref base index of record position 0
+  RefGeo rg[2];
+  long long rd0[2];
+  int rnw[2];
+#pragma unroll
+  for (int ri = 0; ri < 2; ++ri) {
+    const long long s = ri ? r2s : rfs, n = ri ? r2n : rfn;
+    rg[ri].plo = qt - 1 - DRIFT > 0 ? qt - 1 - DRIFT : 0;
+    rg[ri].phi = qt + TILE + k + 1 + DRIFT < n ? qt + TILE + k + 1 + DRIFT : n;
+    rg[ri].rfn = n;
+    rd0[ri] = (s + rg[ri].plo) >> 4;
+    rnw[ri] = (int)(((s + rg[ri].phi + 15) >> 4) - rd0[ri]);
+    rg[ri].rbase = 16 * RPADW + s - 16 * rd0[ri];
+  }
+  long long mrs[QM], mrn[QM];
+  uint32_t dm0 = 0, dm1 = 0, live = 0;
+#pragma unroll
+  for (int m = 0; m < QM; ++m) {
+    const TileDesc td = descs[QM * g + m];
+    mrs[m] = td.rs;
+    mrn[m] = td.rn;
+    const bool d0 = td.r >= 0 && ref >= 0 && ref != td.r;
+    live |= (uint32_t)(td.r >= 0) << m;
+    dm0 |= (uint32_t)d0 << m;
+    dm1 |= (uint32_t)(d0 && ref2 >= 0 && ref2 != td.r) << m;
+  }
+  if (t == 0) s_rexc = 0u;
+  if (t < QM * NANCH) {                            // anchors: 32 bases = 2 words each
+    const int m = t / NANCH, ai = t % NANCH;
+    long long rs = mrs[0];
+#pragma unroll
+    for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
+    const long long ga = rs + qt + 8 + (long long)ai * ASTEP, x = ga >> 4;
+    const uint32_t sb = 2u * (uint32_t)(ga & 15);
+    uint32_t P0 = 0, P1 = 0, P2 = 0;
+    if ((dm0 >> m) & 1u) { P0 = p2_word(p2, x, n_p2); P1 = p2_word(p2, x + 1, n_p2); P2 = p2_word(p2, x + 2, n_p2); }
+    s_anc[m][ai][0] = __builtin_amdgcn_alignbit(P1, P0, sb);
+    s_anc[m][ai][1] = __builtin_amdgcn_alignbit(P2, P1, sb);
+  } else if (t >= 192 && t < 192 + QM * 2 * NANCH) {   // triples: search geometry around the XCD's hint
+    const int x = t - 192, m = x / (2 * NANCH), ri = (x / NANCH) & 1, ai = x % NANCH;
+    (&s_best[0][0][0])[x] = ~0u;
+    TriGeo G{0, 0, -1, 0, -1};
+    if ((((ri ? dm1 : dm0) >> m) & 1u)) {
+      const TileDesc td = descs[QM * g + m];
+      const int hh = hints[(size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + td.r];
+      const int h = hh < 0 ? DRIFT : hh;
+      const RefGeo& R = ri ? rg[1] : rg[0];
+      const long long a = qt + 8 + (long long)ai * ASTEP;
+      G.ibhi = (int)(R.rbase + a + DRIFT);
+      G.lo = max(G.ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
+      G.hi = a + ALEN > td.rn ? -1 : min(G.ibhi, (int)(R.rbase + R.phi) - ALEN);
+      G.lo1 = max(G.lo, G.ibhi - (h + HWIN2));
+      G.hi1 = min(G.hi, G.ibhi - (h - HWIN2));
+    }
+    s_tri[x] = G;
+  }
+  __syncthreads();                                 // (s_rexc cleared)
+  {
+    static_assert(RSTAGEW <= 2 * CBLOCK, "two words per thread and reference");
+    uint32_t v[2][2], ex = 0;
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      const int nw = (ri ? dm1 != 0 : dm0 != 0) ? rnw[ri] : 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = t + h * CBLOCK;
+        v[ri][h] = i < nw ? p2_word(p2, rd0[ri] + i, n_p2) : 0u;
+        if (i < nw && e16[rd0[ri] + i]) ex |= 1u << ri;
+      }
+    }
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (t + h * CBLOCK < rnw[ri]) s_ref[ri][RPADW + t + h * CBLOCK] = v[ri][h];
+    if (ex) atomicOr(&s_rexc, ex);
+  }
+  __syncthreads();
+  {
+    // a reference whose staged span holds a base that is not ACGT covers nothing here
+    const uint32_t rexc = s_rexc;
+    if (rexc & 1u) dm0 = dm1 = 0u;
+    if (rexc & 2u) dm1 = 0u;
+  }
+  if (dm0) cover_search_p(s_anc, s_ref, s_tri, s_best, dm0, dm1);
+  if (t < 2 * QM) {                                // hints and drift sets: one lane per (member, reference)
+    const int m = t >> 1, ri = t & 1;
+    if ((((ri ? dm1 : dm0) >> m) & 1u)) {
+      long long rs = mrs[0];
+      int r = descs[QM * g].r;
+#pragma unroll
+      for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
+      r = descs[QM * g + m].r;
+      publish_hint(s_best[m][ri], hints + (size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + r);
+      const RefGeo R = ri ? rg[1] : rg[0];
+      const long long pos16 = 16 * ((rs + qt - 1) >> 4) - rs;   // record position of the member's word grid
+      s_dr[m][ri] = drifts_p(s_best[m][ri], qt, pos16, R.rbase, R.rfn, R.plo, R.phi, k);
+    }
+  }
+  __syncthreads();
+  // ---- coverage: wave m = member m, lane l = windows 64 l .. 64 l + 63
+  const int m = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63;
+  long long rs = mrs[0], rn = mrn[0];
+#pragma unroll
+  for (int y = 1; y < QM; ++y) if (m == y) { rs = mrs[y]; rn = mrn[y]; }
+  const long long last = rn - k;
+  uint32_t covS[4] = {0u, 0u, 0u, 0u};            // per segment: bit 2 i = window i covered
+  bool mex = false;
+  if ((dm0 >> m) & 1u) {
+    const long long p0 = rs + qt - 1, wb = (p0 >> 4) + 4 * l;
+    const int sh2 = 2 * (int)(p0 & 15);
+    uint32_t M[LW];
+#pragma unroll
+    for (int i = 0; i < LW; ++i) M[i] = p2_word(p2, wb + i, n_p2);
+    {
+      // exception bytes of words wb .. wb + 6 (three aligned dwords around them)
+      const long long a = wb & ~3ll;
+      uint32_t e = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        if (a + 4 * i >= 0 && (uint64_t)(a + 4 * i + 4) <= n_p2 + 16) e |= *reinterpret_cast<const uint32_t*>(e16 + a + 4 * i);
+      mex = e != 0u;
+    }
+    const int L = k + 2;                           // context bases of a window
+    const int P = L >= 16 ? 16 : L >= 8 ? 8 : L >= 4 ? 4 : 2;
+    const uint32_t rsh = 2u * (uint32_t)(L - P);
+#pragma unroll
+    for (int ri = 0; ri < 2; ++ri) {
+      if (ri && !((dm1 >> m) & 1u)) break;
+      const int nd = __builtin_amdgcn_readfirstlane(s_dr[m][ri].n);
+#pragma unroll
+      for (int j = 0; j < NANCH; ++j) {
+        if (j >= nd) break;
+        const int U = __builtin_amdgcn_readfirstlane(s_dr[m][ri].U[j]);
+        const int lo = __builtin_amdgcn_readfirstlane(s_dr[m][ri].lo[j]);
+        const int hi = __builtin_amdgcn_readfirstlane(s_dr[m][ri].hi[j]);
+        int iw = (U >> 4) + 4 * l;
+        if (iw < 0 || iw + 12 > RDW) iw &= 3;      // (an invalid lane: in-bounds words, same alignment)
+        uint32_t Rw[8];
+        lds_words8(s_ref[ri], iw, Rw);
+        const uint32_t bs = 2u * (uint32_t)(U & 15);
+        uint32_t Z[LW];
+#pragma unroll
+        for (int i = 0; i < LW; ++i) {
+          const uint32_t x = M[i] ^ __builtin_amdgcn_alignbit(Rw[i + 1], Rw[i], bs);
+          Z[i] = (x | (x >> 1)) & 0x55555555u;     // even bit of each base: mismatch
+        }
+        uint32_t T[LW - 1];                         // from the lane's first context base (sh bases in)
+#pragma unroll
+        for (int i = 0; i < LW - 1; ++i) T[i] = __builtin_amdgcn_alignbit(Z[i + 1], Z[i], (uint32_t)sh2);
+        // smear: T[b] = any mismatch in bases b .. b + P - 1, then S = T | T >> (L - P)
+#pragma unroll
+        for (int e = 1; e <= 4; ++e) {
+          if ((1 << e) > P) break;                 // (uniform)
+#pragma unroll
+          for (int i = 0; i < LW - 1; ++i)         // length 2^(e-1) -> 2^e bases: shift by 2^(e-1) bases
+            T[i] |= __builtin_amdgcn_alignbit(i + 1 < LW - 1 ? T[i + 1] : 0u, T[i], (uint32_t)(1 << e));
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int rel = 64 * l + 16 * s;
+          const uint32_t S = T[s] | __builtin_amdgcn_alignbit(T[s + 1], T[s], rsh);
+          covS[s] |= (rel >= lo && rel <= hi) ? ~S & 0x55555555u : 0u;
+        }
+      }
+    }
+  }
+  uint32_t nwk = 0, wmask = 0, cov[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const long long q0 = qt + 64 * l + 16 * s;
+    const bool interior = q0 > 0 && q0 + IW <= last;
+    cov[s] = interior && !mex ? even_bits(covS[s]) : 0u;
+    const bool work = ((live >> m) & 1u) && q0 <= last && cov[s] != (1u << IW) - 1u;
+    wmask |= (uint32_t)work << s;
+    nwk += work ? 1u : 0u;
+  }
+  uint32_t nwork;
+  uint32_t pos = block_excl_scan<CBLOCK>(nwk, s_scan, nwork);
+  const unsigned sub = blockIdx.x % NQ;
+  if (t == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+    if ((wmask >> s) & 1u) queue[sub * qcap + s_qbase + pos++] = WorkItem{rs, rn - k, qt + 64 * l + 16 * s, cov[s], 0u};
+}
+
 // ---------------------------------------------------------------- stage A
 // Records go to NBIN coarse bins (h >> shift: the top bits of the bucket
 // index), each with one region per XCD (region = bin * 8 + XCD), so that a
@@ -2183,10 +2542,15 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
       hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
                          c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
                          cb[i], cb[i + 1], cbt);
-    else if (gc[i])
+    else if (gc[i] && c.k3_cover == 2)
       hipLaunchKernelGGL(k_cover_q, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, (uint64_t)c.cls.cap, td, qi, qni,
                          (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
                          c.k3_hint.as<int>(), (int)c.n_records, ntiles, cb[i], cb[i + 1], cbt);
+    else if (gc[i])
+      hipLaunchKernelGGL(k_cover_p, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, c.p2.as<uint32_t>(),
+                         c.e16.as<uint8_t>(), (uint64_t)(c.p2.cap / 4), td, qi, qni, (unsigned long long)qcapc[i], c.k,
+                         c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
+                         cb[i], cb[i + 1], cbt);
     PG_HIP(hipGetLastError());
     hipStream_t ws = s1;
     if (nch > 1 && i + 1 == nch) {

@@ -143,7 +143,7 @@ struct Ctx {
   int k3_wblk = 0;                // pg_tune: work blocks per CU, low 4 bits; last chunk's, high 4 bits (0 = 2)
   int k3_emit = 0;                // pg_tune: work pass (0 = two halves per segment, 1 = one)
   int k3_tail = 0;                // pg_tune: last K3 chunk in 16ths of the others (0 = 16)
-  int k3_cover = 0;               // pg_tune: coverage pass (0 = quad form, 1 = LDS-staged members)
+  int k3_cover = 0;               // pg_tune: coverage pass (0 = packed form, 1 = LDS-staged members, 2 = quad form)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
   int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
   uint64_t stage_piece = 32ull << 20;  // pg_tune: bytes per staging-ring slot (one DMA)
@@ -166,6 +166,8 @@ struct Ctx {
   DevBuf rec_hdr, rec_ptr;        // int64 per record: header byte span packed, `ptr` emulation
   DevBuf rec_flag;                // uint8 per record: take part in the current pass
   DevBuf cls;                     // uint8 per base: class code (records concatenated)
+  DevBuf p2;                      // uint32 per 16 bases: 2-bit codes (class & 3), the packed base stream
+  DevBuf e16;                     // uint8 per 16 bases: nonzero if any is not ACGT
   DevBuf scratch;                 // rocPRIM temp storage
   DevBuf rec_pack;                // the scan total + int64 [5][rec_cap]: the record table for one copy
   uint64_t rec_cap = 0;           // record arrays sized for the last parse's record count

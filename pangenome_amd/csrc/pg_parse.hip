@@ -14,6 +14,15 @@
 //                slice, written with aligned 16-byte stores); each header's
 //                byte span and record start.  No block-wide barrier.
 //   k_records    record lengths and seqio's `ptr` value.
+//   k_pack_fix   the packed base stream's words at span boundaries (below).
+//
+// Besides the class bytes K1 writes the packed base stream K3's coverage
+// pass reads (north_star's "2-bit encode"): one 32-bit word per 16 bases,
+// base j's class & 3 in bits 2j..2j+1 (A0 C1 G2 T3), and one exception byte
+// per 16 bases, nonzero when any of them is not ACGT (N, '$', other: the
+// 2-bit code is then not the class).  k_emit packs every 16-byte chunk it
+// writes whole; a chunk that two spans share is packed by k_pack_fix from
+// the class bytes once both spans are emitted.
 //
 // Line semantics (kmer_numba.py:126-132): a line starts at 0 and after every
 // '\n'; it ends at its '\n', or, for a final unterminated line, at byte n-1
@@ -276,10 +285,29 @@ __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__
 
 __constant__ uint8_t c_byte_class[256];
 
+// The packed word and exception byte of 16 class bytes (4 dwords, 4 classes
+// each): codes class & 3 gathered two bits per base, exception = any class
+// with bit 2 set (N, '$', other).
+__device__ __forceinline__ uint32_t pack_word(const uint4& v, uint32_t& exc) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t out = 0, e = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    uint32_t t = w[d] & 0x03030303u;                 // 2 bits in each byte
+    t = (t | (t >> 6)) & 0x000F000Fu;                // bytes 0,1 -> bits 0..3; 2,3 -> bits 16..19
+    t = (t | (t >> 12)) & 0xFFu;                     // 8 bits: 4 bases
+    out |= t << (8 * d);
+    e |= w[d] & 0x04040404u;
+  }
+  exc = e;
+  return out;
+}
+
 __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
                                                  uint64_t nspan,
                                                  const Fn* __restrict__ incl, uint64_t rcap,
-                                                 uint8_t* __restrict__ out, long long* __restrict__ rec_start,
+                                                 uint8_t* __restrict__ out, uint32_t* __restrict__ p2,
+                                                 uint8_t* __restrict__ e16, long long* __restrict__ rec_start,
                                                  long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
   // pending bytes (< 32) + one step's (<= WSTEP) + the fast step's fifth dword
   constexpr int STAGE = WSTEP + 48;
@@ -395,7 +423,11 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
       for (unsigned long long g = cb + 16ull * lane; g < full; g += 16ull * 64) {
         const uint8_t* src = stage + (g - cb);
         if (g >= own) {
-          *reinterpret_cast<uint4*>(out + g) = *reinterpret_cast<const uint4*>(src);
+          const uint4 cv = *reinterpret_cast<const uint4*>(src);
+          *reinterpret_cast<uint4*>(out + g) = cv;
+          uint32_t exc;
+          p2[g >> 4] = pack_word(cv, exc);              // (a shared chunk: k_pack_fix)
+          e16[g >> 4] = exc ? 1 : 0;
         } else {
           for (int jj = 0; jj < 16; ++jj)
             if (g + jj >= own) out[g + jj] = src[jj];
@@ -421,6 +453,26 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
     const unsigned long long q = cb + lane;
     if (q >= own && q < off) out[q] = stage[lane];
   }
+}
+
+// The packed word of every 16-byte chunk that spans s-1 and s share (the one
+// holding output offset own_s = incl[s-1].c0, when own_s is not a chunk
+// start, and the stream's last, partial chunk), recomputed from the class
+// bytes: k_emit writes only chunks one span owns whole.  Boundaries s0 .. s1
+// (s >= 1).  Under the chunked upload, the boundary at s1 is packed again by
+// the next chunk's call once the span after it is emitted; until then only
+// its bytes below own_s1 are final, and nothing reads the others.
+__global__ void k_pack_fix(const Fn* __restrict__ incl, uint64_t s0, uint64_t s1, const uint8_t* __restrict__ cls,
+                           uint32_t* __restrict__ p2, uint8_t* __restrict__ e16) {
+  const uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > s1 || s == 0) return;
+  const unsigned long long own = incl[s - 1].c0;
+  if (!(own & 15ull)) return;                                 // (no shared chunk)
+  const unsigned long long g = own & ~15ull;
+  const uint4 cv = *reinterpret_cast<const uint4*>(cls + g);
+  uint32_t exc;
+  p2[g >> 4] = pack_word(cv, exc);
+  e16[g >> 4] = exc ? 1 : 0;
 }
 
 // The record table from the scan's total (read on the device: no host round
@@ -505,6 +557,8 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     PG_HIP(rocprim::inclusive_scan(c.scratch.p, b, fns, incl, (size_t)upto, FnThen{}, st));
   };
   c.cls.reserve(n + 64);
+  c.p2.reserve(4 * (n / 16 + 8));
+  c.e16.reserve(n / 16 + 32);
   const uint64_t rcap0 = std::max<uint64_t>(c.rec_cap, on_chunk ? 4096 : 64);
   auto reserve_records = [&](uint64_t rcap) {
     c.rec_start.reserve(8 * (rcap + 1));
@@ -520,7 +574,12 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   auto emit = [&](uint64_t s0, uint64_t s1, uint64_t rcap) {
     auto* hdr = c.rec_hdr.as<long long>();
     hipLaunchKernelGGL(k_emit, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta, n, s0,
-                       s1, incl, rcap, c.cls.as<uint8_t>(), c.rec_start.as<long long>(), hdr, hdr + rcap);
+                       s1, incl, rcap, c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>(),
+                       c.rec_start.as<long long>(), hdr, hdr + rcap);
+    PG_HIP(hipGetLastError());
+    // boundaries s0 .. s1 (s1 = nspan: the stream's end, incl[nspan - 1])
+    hipLaunchKernelGGL(k_pack_fix, dim3(grid_for(s1 - s0 + 1, 256, 65535)), dim3(256), 0, st, incl, s0, s1,
+                       c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>());
     PG_HIP(hipGetLastError());
   };
   reserve_records(rcap0);

@@ -59,7 +59,7 @@ from __future__ import annotations
 
 import os
 import sys
-from time import time
+from time import perf_counter, time
 
 import numpy as np
 
@@ -88,32 +88,40 @@ def _comm_device(device, group):
     return stage, (torch.device("cpu") if stage else device)
 
 
-def _route(table, world: int, device, group=None, sentinel_local: bool = False, subparts: int = 1):
+def _route(table, world: int, device, group=None, sentinel_local: bool = False, subparts: int = 1, tm=None):
     """This rank's table -> owner runs of 16-byte records (pg_dbg_partition)
-    -> one all-to-all.  The run lengths go out with this rank's n<k sentinel
-    flag in one small all-to-all (its receive sizes are the only host read).
-    With `subparts` = P > 1 the table is cut into world x P parts (part q:
-    owner q // P, the owner's sub-log q % P; world x P <= 64), so an owner's
-    run from each rank arrives already split into its P sub-logs.  Returns
-    (the records this rank owns as an (n, 2) int64 tensor on `device`, the
-    received counts per (source rank, sub-log) as a (world, P) array, bytes
-    sent to other ranks, whether any rank saw the sentinel)."""
+    -> one all-to-all.  Every rank's run lengths, with its n<k sentinel flag,
+    go to every rank in one small all-gather: the whole (source, owner) count
+    matrix gives this rank's receive sizes, the largest peer message (the
+    piece count of _all_to_all_rows) and the global sentinel, and is the only
+    host read.  With `subparts` = P > 1 the table is cut into world x P parts
+    (part q: owner q // P, the owner's sub-log q % P; world x P <= 64), so an
+    owner's run from each rank arrives already split into its P sub-logs.
+    Returns (the records this rank owns as an (n, 2) int64 tensor on
+    `device`, the received counts per (source rank, sub-log) as a (world, P)
+    array, bytes sent to other ranks, whether any rank saw the sentinel).
+    `tm` (a dict) accumulates the seconds of the partition and of the
+    all-to-all (the collectives are synchronised for it)."""
     import torch
     import torch.distributed as dist
     P = subparts
     stage, comm = _comm_device(device, group)
+    rank = dist.get_rank(group)
+    t0 = perf_counter()
     counts = table.partition(world * P).astype(np.int64).reshape(world, P)
     total = int(counts.sum())
     send = torch.empty((max(total, 1), 2), dtype=torch.int64, device=device)
     if total:
-        table.partition(world * P, send.data_ptr(), total)
+        table.partition(world * P, send.data_ptr(), total)   # (returns after the scatter)
+    t1 = perf_counter()
     head = np.zeros((world, P + 1), np.int64)
     head[:, :P] = counts
     head[:, P] = 1 if sentinel_local else 0
-    send_head = torch.from_numpy(head).to(comm)
-    recv_head = torch.empty_like(send_head)
-    dist.all_to_all_single(recv_head, send_head, group=group)
-    rh = recv_head.cpu().numpy()
+    send_head = torch.from_numpy(head.reshape(-1)).to(comm)
+    heads = [torch.empty_like(send_head) for _ in range(world)]
+    dist.all_gather(heads, send_head, group=group)
+    H = torch.stack(heads).cpu().numpy().reshape(world, world, P + 1)     # [source, owner, sub-log | flag]
+    rh = H[:, rank, :]
     rsplit = rh[:, :P].sum(axis=1).tolist()
     nrecv = int(sum(rsplit))
     recv = torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm)
@@ -123,9 +131,15 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
                                input_split_sizes=ssplit, group=group)
         recv = recv.to(device)
     else:
-        _all_to_all_rows(recv, send, rsplit, ssplit, comm, group)
-    rank = dist.get_rank(group)
-    return recv[:nrecv], rh[:, :P], 16 * (total - int(counts[rank].sum())), bool(rh[:, P].any())
+        _all_to_all_rows(recv, send, rsplit, ssplit, comm, group, big=int(H[:, :, :P].sum(axis=2).max()))
+    if tm is not None:
+        if _is_cuda(device):
+            torch.cuda.synchronize(device)
+        t2 = perf_counter()
+        tm["partition"] = tm.get("partition", 0.0) + (t1 - t0)
+        tm["all_to_all"] = tm.get("all_to_all", 0.0) + (t2 - t1)
+        tm["rows"] = tm.get("rows", 0) + total
+    return recv[:nrecv], rh[:, :P], 16 * (total - int(counts[rank].sum())), bool(H[:, :, P].any())
 
 
 # Records per peer and collective on device backends: RCCL 2.26 (ROCm 7)
@@ -135,17 +149,19 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
 A2A_ROWS = 1 << 25
 
 
-def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None):
+def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None, big=None):
     """all_to_all of (n, 2) int64 rows in pieces of at most A2A_ROWS rows per
     peer (every rank runs the same number of pieces: the largest message of
-    any rank, by one MAX all-reduce, decides).  Views of contiguous runs, no
-    copies."""
+    any rank decides; `big`, when the caller knows it, else one MAX
+    all-reduce finds it).  Views of contiguous runs, no copies."""
     import torch
     import torch.distributed as dist
     world = len(ssplit)
-    big = torch.tensor([max(max(ssplit), max(rsplit)) if world else 0], dtype=torch.int64, device=comm)
-    dist.all_reduce(big, op=dist.ReduceOp.MAX, group=group)
-    npieces = max(1, -(-int(big.item()) // A2A_ROWS))
+    if big is None:
+        b = torch.tensor([max(max(ssplit), max(rsplit)) if world else 0], dtype=torch.int64, device=comm)
+        dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
+        big = int(b.item())
+    npieces = max(1, -(-int(big) // A2A_ROWS))
     if npieces == 1:
         dist.all_to_all_single(recv[:sum(rsplit)], send[:sum(ssplit)], output_split_sizes=rsplit,
                                input_split_sizes=ssplit, group=group)
@@ -170,15 +186,17 @@ def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None):
                 at += x.shape[0]
 
 
-def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None, sentinel_global=None):
+def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None, sentinel_global=None, tm=None):
     """OR-merge the owned records into a fresh owner table, rdBG rule on it;
     global (n_dbg, n_rdbg) by one sum all-reduce.  `sentinel_global`: whether
     any rank saw the n<k sentinel, when the caller already knows (else one MAX
     all-reduce of `sentinel_local` finds out).  Returns (n_dbg_total,
-    n_rdbg_total, n_rdbg_local)."""
+    n_rdbg_total, n_rdbg_local); `tm["merge"]` accumulates the seconds of the
+    merge, the rdBG rule and the count all-reduce."""
     import torch
     import torch.distributed as dist
     _, comm = _comm_device(device, group)
+    t0 = perf_counter()
     if sentinel_global is None:
         flag = torch.tensor([1 if sentinel_local else 0], dtype=torch.int64, device=comm)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
@@ -192,15 +210,18 @@ def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=No
     sums = torch.tensor([st.n_dbg, st.n_rdbg], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
     n_dbg, n_rdbg = sums.tolist()
+    if tm is not None:
+        tm["merge"] = tm.get("merge", 0.0) + (perf_counter() - t0)
     return int(n_dbg), int(n_rdbg), int(st.n_rdbg)
 
 
-def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bool, group=None):
+def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bool, group=None, tm=None):
     """Owner all-to-all + OR-merge + rdBG rule on the owner partition: two
-    host reads (the receive sizes, the global counts).  Returns (n_dbg_total,
-    n_rdbg_total, n_rdbg_local, bytes_sent)."""
-    recv, _, sent, sentinel = _route(table, world, device, group, sentinel_local)
-    return _owner_reduce(table, recv, rank, device, sentinel_local, group, sentinel_global=sentinel) + (sent,)
+    host reads (the count matrix, the global counts) besides the partition's
+    own count read.  Returns (n_dbg_total, n_rdbg_total, n_rdbg_local,
+    bytes_sent); `tm` accumulates partition / all_to_all / merge seconds."""
+    recv, _, sent, sentinel = _route(table, world, device, group, sentinel_local, tm=tm)
+    return _owner_reduce(table, recv, rank, device, sentinel_local, group, sentinel_global=sentinel, tm=tm) + (sent,)
 
 
 def stream_chunks(flags, seq_len, limit: int) -> list:

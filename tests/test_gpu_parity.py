@@ -153,14 +153,15 @@ def test_overflow_and_rerun_paths_vs_oracle(oracle_mod, k):
         ctx.close()
 
 
-@pytest.mark.parametrize("form", [0, 1])
+@pytest.mark.parametrize("form", [0, 1, 2])
 @pytest.mark.parametrize("c", [0, 2])
 def test_k3_reference_dedup_vs_oracle(oracle_mod, c, form):
     """The coverage pass skips a follower window whose k+2 context bytes equal
     the lead record's at some drift: copies of the lead with insertions (drift
     inside and beyond the +-512 search), deletions, SNPs, an N run, lowercase
     bytes, shorter copies (reference windows near its ends) and a reverse
-    complement; both forms of the pass (quad compare, LDS-staged members)."""
+    complement; every form of the pass (packed 2-bit stream, LDS-staged
+    members, quad compare)."""
     from pangenome_amd import synth
     from pangenome_amd._lib import Context, PG_TUNE_K3_COVER
     rng = np.random.default_rng(7 + c)
@@ -201,17 +202,18 @@ def test_k3_reference_dedup_vs_oracle(oracle_mod, c, form):
 
 @pytest.mark.parametrize("k", [5, 15, 21, 27])
 def test_k3_cover_forms_vs_oracle(oracle_mod, k):
-    """Both coverage-pass forms give the oracle's dBG and rdBG at several k
-    (the quad form's window mask depends on k and on each record's start
-    modulo 4: odd line widths and headers shift it), and the quad form leaves
-    no more than 2 % more stage A records than the LDS-staged one."""
+    """Every coverage-pass form gives the oracle's dBG and rdBG at several k
+    (the window masks depend on k and on each record's start modulo 4 (quad
+    form) or 16 (packed form): odd line widths and headers shift it); the
+    packed form, exact per base, leaves no more stage A records than the quad
+    form, and neither leaves more than 2 % more than the LDS-staged one."""
     from pangenome_amd import synth
     from pangenome_amd._lib import Context, PG_TUNE_K3_COVER
     fasta = synth.pangenome(9, 120_000, snp=2e-3, indel=3e-4, seed=400 + k, width=61)
     ref = oracle_mod.OracleRun(fasta, k, 2)
     rk, rm = ref.dbg()
     recs = []
-    for form in (0, 1):
+    for form in (0, 1, 2):
         ctx = Context(k)
         ctx.tune(PG_TUNE_K3_COVER, form)
         ctx.set_fasta(fasta)
@@ -222,7 +224,7 @@ def test_k3_cover_forms_vs_oracle(oracle_mod, k):
         assert np.array_equal(ctx.rdbg(), ref.rdbg()), form
         recs.append(st.n_records_a)
         ctx.close()
-    assert recs[0] <= recs[1] * 1.02 + 64, recs
+    assert recs[0] <= recs[2] and recs[2] <= recs[1] * 1.02 + 64, recs
 
 
 def test_edge_checkpoint_reversal_vs_oracle(km, oracle_mod, tmp_path):

@@ -10,7 +10,7 @@
    recv[torch.argsort(sub, stable=True)] with sub = a hash of the key word,
    on (n, 2) int64 rows, checked against numpy on the host.
 
-    python tools/corruption_bracket.py [a2a|sort|all] > out.json
+    python tools/corruption_bracket.py a2a|sort > out.jsonl
 One JSON line per case on stdout.
 """
 import json
@@ -76,48 +76,71 @@ def a2a_cases(dev):
         torch.cuda.empty_cache()
 
 
-def sort_cases(dev):
+def sort_case(dev, rows, nsub, op):
+    """One (rows, nsub, op) case in this process: op = argsort (stable) and
+    the gather t[idx], or index_select, each synchronised so that an error is
+    attributed to its op."""
     golden = -7046029254386353131                     # 0x9E3779B97F4A7C15 as int64 (wrapping multiply)
-    for rows in (1 << 26, 1 << 27, 125_000_000, 140_000_000, 1 << 28):
-        host = np.random.default_rng(rows).integers(0, 1 << 62, size=(rows, 2), dtype=np.int64)
-        t = torch.from_numpy(host).to(dev)
-        for nsub in (4, 16):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            sub = ((t[:, 0] * golden) >> 20) & (nsub - 1)
-            idx = torch.argsort(sub, stable=True)
-            out = t[idx]
-            torch.cuda.synchronize()
-            ms = 1e3 * (time.perf_counter() - t0)
-            with np.errstate(over="ignore"):
-                hsub = ((host[:, 0] * np.int64(golden)) >> 20) & (nsub - 1)
-            hidx = np.argsort(hsub, kind="stable")
-            idx_ok = bool(np.array_equal(idx.cpu().numpy(), hidx))
-            sub_ok = bool(np.array_equal(sub.cpu().numpy(), hsub))
-            o = out.cpu().numpy()
-            ref = host[hidx]
-            ne = np.flatnonzero((o != ref).any(axis=1))
-            emit(case="sort", rows=rows, bytes=16 * rows, nsub=nsub, sub_ok=sub_ok, argsort_ok=idx_ok,
-                 gather_ok=ne.shape[0] == 0, bad_rows=int(ne.shape[0]),
-                 first_bad_row=int(ne[0]) if ne.shape[0] else -1, ms=round(ms, 2))
-            del sub, idx, out, o, ref
-        del t, host
-        torch.cuda.empty_cache()
+    host = np.random.default_rng(rows).integers(0, 1 << 62, size=(rows, 2), dtype=np.int64)
+    t = torch.from_numpy(host).to(dev)
+    stage = "sub"
+    res = dict(case="sort", rows=rows, bytes=16 * rows, nsub=nsub, op=op)
+    try:
+        sub = ((t[:, 0] * golden) >> 20) & (nsub - 1)
+        torch.cuda.synchronize()
+        stage = "argsort"
+        idx = torch.argsort(sub, stable=True)
+        torch.cuda.synchronize()
+        stage = op
+        out = t[idx] if op == "gather" else torch.index_select(t, 0, idx)
+        torch.cuda.synchronize()
+    except Exception as e:                            # noqa: BLE001 (a launch error is reported, not raised on)
+        res.update(ok=False, error_stage=stage, error=str(e).splitlines()[0])
+        emit(**res)
+        return False
+    with np.errstate(over="ignore"):
+        hsub = ((host[:, 0] * np.int64(golden)) >> 20) & (nsub - 1)
+    hidx = np.argsort(hsub, kind="stable")
+    o = out.cpu().numpy()
+    ne = np.flatnonzero((o != host[hidx]).any(axis=1))
+    res.update(ok=ne.shape[0] == 0, sub_ok=bool(np.array_equal(sub.cpu().numpy(), hsub)),
+               argsort_ok=bool(np.array_equal(idx.cpu().numpy(), hidx)), bad_rows=int(ne.shape[0]),
+               first_bad_row=int(ne[0]) if ne.shape[0] else -1)
+    emit(**res)
+    return res["ok"]
+
+
+def sort_cases(dev):
+    """Ascending sizes, each case in a fresh process (a launch error ends that
+    process only); stops at the first failing size."""
+    import subprocess
+    for rows in (1 << 20, 1 << 22, 1 << 24, (1 << 24) + 1, 1 << 25, (1 << 25) + (1 << 24), (1 << 26) - 1, 1 << 26):
+        fails = 0
+        for op in ("gather", "index_select"):
+            r = subprocess.run([sys.executable, "-u", __file__, "sort1", str(rows), "4", op], timeout=120)
+            fails += r.returncode != 0
+        if fails:
+            break
 
 
 def main():
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
+    if what == "sort1":
+        torch.cuda.set_device(0)
+        ok = sort_case(torch.device("cuda", 0), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4])
+        sys.exit(0 if ok else 1)
+    if what == "sort":                                # (the parent never touches the GPU)
+        emit(case="env", torch=torch.__version__, hip=torch.version.hip)
+        sort_cases(None)
+        return
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=os.environ.get("MASTER_PORT", "29547"))
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     emit(case="env", torch=torch.__version__, hip=torch.version.hip,
          rccl=".".join(map(str, torch.cuda.nccl.version())), device=torch.cuda.get_device_name(0))
-    if what in ("a2a", "all"):
-        dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-        a2a_cases(dev)
-        dist.destroy_process_group()
-    if what in ("sort", "all"):
-        sort_cases(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    a2a_cases(dev)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -20,6 +20,10 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    rehearse2) run bench_rehearse2 900 env PG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 2 --warmup 1 ;;
+    rehearse2c3) run bench_rehearse2c3 600 env PG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --config c3 --steps 3 --warmup 1 ;;
+    cover) run pytest_cover 600 python -u -m pytest tests/test_gpu_parity.py -k "k3" -x -v --timeout 120 --timeout-method thread ;;
+    bracket) run bracket_sort 500 python -u tools/corruption_bracket.py sort ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window ;;
