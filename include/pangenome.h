@@ -56,6 +56,9 @@ typedef struct pg_stats {
   uint64_t n_records_a;    /* K3 stage A records (windows the coverage pass kept)  */
   double ms_split;         /* K3 stage B: k_split pass(es)                         */
   double ms_range;         /* K3 stage C: k_build_range (table + fused K5)         */
+  uint64_t build_flags;    /* bit 0: the last pg_build_host split its records into
+                              the table's partitions chunk by chunk under the upload
+                              (PG_TUNE_EARLY_SPLIT) and stage C read them          */
 } pg_stats;
 
 /* Context on HIP device `device` for k-mer length k (clamped to [1, 27] as
@@ -233,6 +236,11 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 /* PG_TUNE_K3_TAIL: size of the last K3 chunk in 16ths of the others (1..64,
  * 0 = 10: the work pass left behind the last coverage pass is smaller). */
 #define PG_TUNE_K3_TAIL 13
+/* PG_TUNE_EARLY_SPLIT: pg_build_host's stage B under the upload, 1 (default)
+ * = the records of each landed chunk split into the table's fine partitions
+ * as soon as its stage A share is done (geometry from the last build; a
+ * mismatch at the end re-splits everything), 0 = after the last chunk. */
+#define PG_TUNE_EARLY_SPLIT 14
 /* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
  * count asks (0..8): exercises the overflow set, its spill and the re-run
  * with more buckets (results are unchanged). */
@@ -260,7 +268,9 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 /* PG_TUNE_DEVICE_CAP: the most device bytes the library's buffers may hold
  * in this process, over all contexts (0 = no cap): an allocation past it
  * fails with PG_ENOMEM.  Setting it also restarts pg_device_bytes' peak.
- * For tests of a path's memory budget at a scaled-down size. */
+ * PROCESS-WIDE: although it is set through one context's pg_tune, the cap
+ * and the peak it restarts are shared by every context of the process (and
+ * every device).  For tests of a path's memory budget at a scaled-down size. */
 #define PG_TUNE_DEVICE_CAP 9
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 

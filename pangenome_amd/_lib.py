@@ -23,11 +23,12 @@ PG_TUNE_HOST_THREADS = 5
 PG_TUNE_STAGE_PIECE = 6
 PG_TUNE_STAGE_SLOTS = 7
 PG_TUNE_HOST_REGISTER = 8
-PG_TUNE_DEVICE_CAP = 9
+PG_TUNE_DEVICE_CAP = 9          # process-wide: caps (and restarts the peak of) every context's buffers
 PG_TUNE_K3_COVER = 10
 PG_TUNE_K3_WBLK = 11
 PG_TUNE_K3_EMIT = 12
 PG_TUNE_K3_TAIL = 13
+PG_TUNE_EARLY_SPLIT = 14
 
 
 class PgStats(C.Structure):
@@ -38,6 +39,7 @@ class PgStats(C.Structure):
         ("ms_parse", C.c_double), ("ms_clear", C.c_double), ("ms_insert", C.c_double),
         ("ms_scan", C.c_double), ("sentinel", C.c_uint64),
         ("n_records_a", C.c_uint64), ("ms_split", C.c_double), ("ms_range", C.c_double),
+        ("build_flags", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -349,10 +351,17 @@ class Context:
                                             ptr(mi), mk.shape[0], int(next_label), C.byref(n)),
               "pg_labels_from_edges")
         self.n_labels = n.value
+        self.label_gen = getattr(self, "label_gen", 0) + 1
         return n.value
 
-    def labels(self):
-        """(keys, vals, ids) of the device label table, in insertion order."""
+    def labels(self, gen=None):
+        """(keys, vals, ids) of the device label table, in insertion order.
+        `gen`: the label_gen a caller's view was made at; a later label pass
+        (set_labels / labels_from_edges) on this context replaced that table,
+        and reading it then raises instead of returning the newer labels."""
+        if gen is not None and gen != getattr(self, "label_gen", 0):
+            raise RuntimeError("label table: replaced by a later label pass on this context (generation %d, now %d)"
+                               % (gen, getattr(self, "label_gen", 0)))
         n = getattr(self, "n_labels", 0)
         out = [np.empty(n, np.int64) for _ in range(3)]
         if n:
@@ -365,6 +374,7 @@ class Context:
         ids = np.ascontiguousarray(ids, np.int64)
         check(self.lib.pg_set_labels(self.h, ptr(keys), ptr(vals), ptr(ids), keys.shape[0]), "pg_set_labels")
         self.n_labels = keys.shape[0]
+        self.label_gen = getattr(self, "label_gen", 0) + 1
 
     def rows_count(self, rec_flags=None, rc1: bool = False) -> int:
         """pg_rows only: the rows stay on the device (rows_text / rows())."""

@@ -47,6 +47,7 @@ static void fill_stats(const pg::Ctx& c, pg_stats* s) {
   s->ms_split = c.ms_split;
   s->ms_range = c.ms_range;
   s->sentinel = c.sentinel;
+  s->build_flags = c.early_split_used ? 1u : 0u;
 }
 
 extern "C" {
@@ -79,9 +80,9 @@ void pg_destroy(pg_ctx* x) {
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
   pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.n_sel, &c.rec_start, &c.rec_len,
-                        &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.scratch, &c.table, &c.ovf, &c.flags,
+                        &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.p2, &c.e16, &c.scratch, &c.table, &c.ovf, &c.flags,
                         &c.recA_key, &c.recA_mw, &c.ctrA, &c.recS_key[0], &c.recS_key[1], &c.recS_mw[0],
-                        &c.recS_mw[1], &c.ctrS, &c.rseg, &c.k5_ctr, &c.tile_sched, &c.tile_desc, &c.k3_queue,
+                        &c.recS_mw[1], &c.ctrS, &c.snapA, &c.rseg, &c.k5_ctr, &c.tile_sched, &c.tile_desc, &c.k3_queue,
                         &c.k3_hint, &c.part_cnt, &c.tile_cnt, &c.tile_off, &c.occ, &c.edge_tab, &c.pair_tab,
                         &c.edge_out, &c.edge_exp, &c.lab_tab, &c.lab_list, &c.rows_buf, &c.text_len, &c.text_off,
                         &c.text_buf, &c.text_names, &c.preload,
@@ -272,7 +273,7 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         x->c.k3_chunks = (int)value;
         break;
       case PG_TUNE_K3_COVER:
-        if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: K3 cover form must be 0 or 1");
+        if (value < 0 || value > 2) throw pg::Error(PG_EINVAL, "pg_tune: K3 cover form must be 0, 1 or 2");
         x->c.k3_cover = (int)value;
         break;
       case PG_TUNE_K3_WBLK:
@@ -286,6 +287,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
       case PG_TUNE_K3_TAIL:
         if (value < 0 || value > 64) throw pg::Error(PG_EINVAL, "pg_tune: K3 tail must be in [0, 64]");
         x->c.k3_tail = (int)value;
+        break;
+      case PG_TUNE_EARLY_SPLIT:
+        if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: early split must be 0 or 1");
+        x->c.early_split = (int)value;
         break;
       case PG_TUNE_BUCKET_SHIFT:
         if (value < 0 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: bucket shift must be in [0, 8]");

@@ -47,6 +47,28 @@
 
 namespace pg {
 
+// Development (PG_DEBUG_BOUNDS builds only, tools/exp_build.sh -D...): index
+// checks in the coverage / work passes that record the first violation in
+// g_dbg (code, values) and skip the access instead of faulting.
+#ifdef PG_DEBUG_BOUNDS
+// per code slot (code % 16): count g_dbg[slot], then up to 4 entries of 5 words (code, a, b, block, thread)
+__device__ unsigned long long g_dbg[16 + 16 * 4 * 5];
+__device__ __forceinline__ bool pg_bok(bool ok, unsigned code, long long a, long long b) {
+  if (!ok) {
+    const unsigned slot = code % 16;
+    const unsigned long long i = atomicAdd(&g_dbg[slot], 1ull);
+    if (i < 4) {
+      unsigned long long* e = g_dbg + 16 + (slot * 4 + i) * 5;
+      e[0] = code; e[1] = (unsigned long long)a; e[2] = (unsigned long long)b; e[3] = blockIdx.x; e[4] = threadIdx.x;
+    }
+  }
+  return ok;
+}
+#define PG_BOK(ok, code, a, b) pg_bok((ok), (code), (long long)(a), (long long)(b))
+#else
+#define PG_BOK(ok, code, a, b) true
+#endif
+
 constexpr int IBLOCK = 256;
 constexpr int IW = 16;                        // windows per thread (one segment)
 constexpr int CBLOCK = 256;                   // coverage block (one tile)
@@ -315,10 +337,19 @@ __device__ __forceinline__ void cover_search(uint8_t (*s_cls)[SPAN + 16], uint8_
   }
   __syncthreads();
   static_assert(NANCH == 3, "any-anchor test");
-#pragma unroll 1
-  for (int p = 0; p < 2 * QM; ++p) {                          // block-uniform
+  uint32_t need = 0;                                          // (as cover_search_q: decided before any search)
+#pragma unroll
+  for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
-    if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
+    if ((((ri ? dm1 : dm0) >> m) & 1u) && (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) == ~0u)
+      need |= 1u << p;
+  }
+  if (!need) return;                                          // (block-uniform)
+  __syncthreads();
+#pragma unroll 1
+  for (int p = 0; p < 2 * QM; ++p) {
+    const int m = p >> 1, ri = p & 1;
+    if (!((need >> p) & 1u)) continue;
     const MemGeo& G = geo[m];
 #pragma unroll 1
     for (int ai = 0; ai < NANCH; ++ai) {
@@ -750,12 +781,23 @@ __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4
     }
   }
   __syncthreads();
-  bool full = false;                                          // (block-uniform; rare: no barrier without it)
+  // pairs whose three anchors all missed: decided by every wave from the
+  // state the barrier above published, and the barrier below keeps any
+  // wave's search from changing best[] before every wave has decided (a
+  // wave deciding late would otherwise skip the pair and the barriers)
+  uint32_t need = 0;
+#pragma unroll
+  for (int p = 0; p < 2 * QM; ++p) {
+    const int m = p >> 1, ri = p & 1;
+    if ((((ri ? dm1 : dm0) >> m) & 1u) && (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) == ~0u)
+      need |= 1u << p;
+  }
+  if (!need) return;                                          // (block-uniform)
+  __syncthreads();
 #pragma unroll 1
   for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
-    if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
-    full = true;
+    if (!((need >> p) & 1u)) continue;
 #pragma unroll 1
     for (int ai = 0; ai < NANCH; ++ai) {
       const TriGeo g = tri[(m * 2 + ri) * NANCH + ai];
@@ -763,7 +805,7 @@ __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4
         drift_task_anc(s_anc[m][ai], s_ref[ri], g.ibhi, g.lo, g.hi, w, &best[m][ri][ai]);
     }
   }
-  if (full) __syncthreads();
+  __syncthreads();
 }
 
 // (8 waves per SIMD: 78 SGPRs with 24 spilled to VGPR lanes, against 106 and
@@ -1005,6 +1047,7 @@ static_assert(IW * 4 == 64 && CBLOCK == 64 * QM, "a lane owns 4 segments; a wave
 struct Drifts2 {
   int n;
   int U[NANCH], lo[NANCH], hi[NANCH];             // U: s_ref base index of the member's word-grid base
+  int d[NANCH];                                   // the drift (q - p) itself
 };
 // the drift set of one (member, reference): drifts_of's rule, with U = the
 // s_ref base index that member base 16 D (record position pos16) maps to
@@ -1013,7 +1056,7 @@ __device__ __forceinline__ Drifts2 drifts_p(const unsigned* s_best, long long qt
   Drifts2 D;
   D.n = 0;
 #pragma unroll
-  for (int j = 0; j < NANCH; ++j) D.U[j] = D.lo[j] = D.hi[j] = 0;
+  for (int j = 0; j < NANCH; ++j) D.U[j] = D.lo[j] = D.hi[j] = D.d[j] = 0;
   const long long pl = plo + 1 > 1 ? plo + 1 : 1;
   const long long ph = rfn - k - IW < phi - IW - k ? rfn - k - IW : phi - IW - k;
 #pragma unroll
@@ -1030,7 +1073,7 @@ __device__ __forceinline__ Drifts2 drifts_p(const unsigned* s_best, long long qt
     const int l32 = (int)(lo < -(1ll << 30) ? -(1ll << 30) : lo), h32 = (int)(hi > (1ll << 30) ? (1ll << 30) : hi);
 #pragma unroll
     for (int j = 0; j <= ai; ++j)
-      if (j == D.n) { D.lo[j] = l32; D.hi[j] = h32; D.U[j] = u; }
+      if (j == D.n) { D.lo[j] = l32; D.hi[j] = h32; D.U[j] = u; D.d[j] = d; }
     ++D.n;
   }
   return D;
@@ -1043,6 +1086,7 @@ __device__ __forceinline__ uint32_t p2_word(const uint32_t* p2, long long i, uin
 // within [lo, hi]: its 32 bases against the reference's 32 from ib
 __device__ __forceinline__ void drift_task_p(uint32_t A0, uint32_t A1, const uint32_t* R, int ibhi, int lo, int hi,
                                              int w, unsigned* best) {
+  if (!PG_BOK(w >= 0 && w + 2 < RDW, 16, w, hi)) return;
   const uint32_t W0 = R[w], W1 = R[w + 1], W2 = R[w + 2];
   uint32_t hit = 0;
 #pragma unroll
@@ -1078,12 +1122,23 @@ __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2]
     }
   }
   __syncthreads();
-  bool full = false;                                          // (block-uniform; rare)
+  // pairs whose three anchors all missed: decided by every wave from the
+  // state the barrier above published, and the barrier below keeps any
+  // wave's search from changing best[] before every wave has decided (a
+  // wave deciding late would otherwise skip the pair and the barriers)
+  uint32_t need = 0;
+#pragma unroll
+  for (int p = 0; p < 2 * QM; ++p) {
+    const int m = p >> 1, ri = p & 1;
+    if ((((ri ? dm1 : dm0) >> m) & 1u) && (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) == ~0u)
+      need |= 1u << p;
+  }
+  if (!need) return;                                          // (block-uniform)
+  __syncthreads();
 #pragma unroll 1
   for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
-    if (!((((ri ? dm1 : dm0) >> m) & 1u)) || (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) != ~0u) continue;
-    full = true;
+    if (!((need >> p) & 1u)) continue;
 #pragma unroll 1
     for (int ai = 0; ai < NANCH; ++ai) {
       const TriGeo g = tri[(m * 2 + ri) * NANCH + ai];
@@ -1091,7 +1146,7 @@ __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2]
         drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo, g.hi, w, &best[m][ri][ai]);
     }
   }
-  if (full) __syncthreads();
+  __syncthreads();
 }
 
 // 8 words of s_ref from word index idx (idx & 3 the same on every lane: a
@@ -1127,7 +1182,7 @@ __device__ __forceinline__ uint32_t even_bits(uint32_t x) {
 
 __global__ void __launch_bounds__(CBLOCK, 8)
 k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint64_t n_p2,
-          const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue, unsigned long long* __restrict__ qcount,
+          const uint8_t* __restrict__ cls_dbg, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue, unsigned long long* __restrict__ qcount,
           unsigned long long qcap, int k, int ref, long long rfs, long long rfn, int ref2, long long r2s,
           long long r2n, int* __restrict__ hints, int nrec, uint64_t ngroups, uint32_t b0, uint32_t b1, uint32_t bt) {
   __shared__ __attribute__((aligned(16))) uint32_t s_ref[2][RDW];
@@ -1212,14 +1267,17 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
       for (int h = 0; h < 2; ++h) {
         const int i = t + h * CBLOCK;
         v[ri][h] = i < nw ? p2_word(p2, rd0[ri] + i, n_p2) : 0u;
-        if (i < nw && e16[rd0[ri] + i]) ex |= 1u << ri;
+        if (i < nw && PG_BOK(rd0[ri] + i >= 0 && (uint64_t)(rd0[ri] + i) < n_p2, 12, rd0[ri] + i, n_p2) &&
+            e16[rd0[ri] + i])
+          ex |= 1u << ri;
       }
     }
 #pragma unroll
     for (int ri = 0; ri < 2; ++ri)
 #pragma unroll
       for (int h = 0; h < 2; ++h)
-        if (t + h * CBLOCK < rnw[ri]) s_ref[ri][RPADW + t + h * CBLOCK] = v[ri][h];
+        if (t + h * CBLOCK < rnw[ri] && PG_BOK(RPADW + t + h * CBLOCK < RDW, 13, rnw[ri], t))
+          s_ref[ri][RPADW + t + h * CBLOCK] = v[ri][h];
     if (ex) atomicOr(&s_rexc, ex);
   }
   __syncthreads();
@@ -1238,6 +1296,7 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
 #pragma unroll
       for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
       r = descs[QM * g + m].r;
+      (void)PG_BOK(r >= 0 && r < nrec, 52, (long long)r, (long long)nrec);
       publish_hint(s_best[m][ri], hints + (size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + r);
       const RefGeo R = ri ? rg[1] : rg[0];
       const long long pos16 = 16 * ((rs + qt - 1) >> 4) - rs;   // record position of the member's word grid
@@ -1266,6 +1325,7 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
 #pragma unroll
       for (int i = 0; i < 3; ++i)
         if (a + 4 * i >= 0 && (uint64_t)(a + 4 * i + 4) <= n_p2 + 16) e |= *reinterpret_cast<const uint32_t*>(e16 + a + 4 * i);
+      (void)PG_BOK(wb + LW <= (long long)n_p2 + 4 || wb > (long long)n_p2, 11, wb, n_p2);
       mex = e != 0u;
     }
     const int L = k + 2;                           // context bases of a window
@@ -1283,6 +1343,7 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
         const int hi = __builtin_amdgcn_readfirstlane(s_dr[m][ri].hi[j]);
         int iw = (U >> 4) + 4 * l;
         if (iw < 0 || iw + 12 > RDW) iw &= 3;      // (an invalid lane: in-bounds words, same alignment)
+        if (!PG_BOK(iw >= 0 && iw + 12 <= RDW, 14, iw, U)) iw = 0;
         uint32_t Rw[8];
         lds_words8(s_ref[ri], iw, Rw);
         const uint32_t bs = 2u * (uint32_t)(U & 15);
@@ -1308,6 +1369,21 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
           const int rel = 64 * l + 16 * s;
           const uint32_t S = T[s] | __builtin_amdgcn_alignbit(T[s + 1], T[s], rsh);
           covS[s] |= (rel >= lo && rel <= hi) ? ~S & 0x55555555u : 0u;
+#ifdef PG_DEBUG_BOUNDS
+          {                                        // every window this drift covers, against the class bytes
+            const long long q0 = qt + rel;
+            const int dd = __builtin_amdgcn_readfirstlane(s_dr[m][ri].d[j]);
+            const long long fs = ri ? r2s : rfs;
+            const uint32_t cvd = (rel >= lo && rel <= hi && q0 > 0 && q0 + IW <= last) ? (~S & 0x55555555u) : 0u;
+            for (int i = 0; i < 16; ++i)
+              if ((cvd >> (2 * i)) & 1u) {
+                const long long q = q0 + i;
+                bool eq = true;
+                for (int x = -1; x <= k; ++x) eq &= cls_dbg[rs + q + x] == cls_dbg[fs + q - dd + x];
+                (void)pg_bok(eq, 31, (long long)q, (long long)dd);
+              }
+          }
+#endif
         }
       }
     }
@@ -1325,12 +1401,31 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
   uint32_t nwork;
   uint32_t pos = block_excl_scan<CBLOCK>(nwk, s_scan, nwork);
   const unsigned sub = blockIdx.x % NQ;
-  if (t == 0) s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
+  if (t == 0) {
+    s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
+    (void)PG_BOK(nwork <= QM * CBLOCK && s_qbase + nwork <= qcap, 42, (long long)nwork, (long long)s_qbase);
+  }
   __syncthreads();
 #pragma unroll
   for (int s = 0; s < 4; ++s)
-    if ((wmask >> s) & 1u) queue[sub * qcap + s_qbase + pos++] = WorkItem{rs, rn - k, qt + 64 * l + 16 * s, cov[s], 0u};
+    if ((wmask >> s) & 1u) {
+      if (PG_BOK(s_qbase + pos < qcap && rs >= 0 && qt + 64 * l + 16 * s <= rn, 15, s_qbase + pos, rs))
+        queue[sub * qcap + s_qbase + pos] = WorkItem{rs, rn - k, qt + 64 * l + 16 * s, cov[s], 0u};
+      ++pos;
+    }
 }
+
+#ifdef PG_DEBUG_BOUNDS
+// every sub-queue counter of a chunk at most `lim` (code: which check point)
+__global__ void k_dbg_counters(const unsigned long long* __restrict__ qcount, unsigned long long lim, unsigned code,
+                               unsigned chunk) {
+  const unsigned sub = threadIdx.x;
+  if (sub < NQ) {
+    const unsigned long long v = qcount[QSTRIDE * sub];
+    (void)pg_bok(v <= lim, code, (long long)v, (long long)(chunk * 1000 + sub));
+  }
+}
+#endif
 
 // ---------------------------------------------------------------- stage A
 // Records go to NBIN coarse bins (h >> shift: the top bits of the bucket
@@ -1425,6 +1520,7 @@ __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[
         O.key[at] = hv;
         O.mw[at] = st_mw[e];
       } else {
+        (void)PG_BOK(false, 51, (long long)pos, (long long)O.cap);
         atomicOr(O.flags + 1, F_A_OVER);
       }
     }
@@ -1491,6 +1587,8 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
       for (int step = NQ / 2; step > 0; step >>= 1)
         if (s_pre[lo + step] <= i) lo += step;
       w = queue[(unsigned long long)lo * qcap + (i - s_pre[lo])];
+      if (!PG_BOK(i - s_pre[lo] < qcap && w.rs >= 0 && w.q0 >= 0 && w.q0 <= w.last + 1, 21, w.rs, w.q0))
+        w = WorkItem{0, -1, 0, 0u, 0u};
       const long long from = w.rs + w.q0 - 2;
       aligned = from > 0 ? from & ~15ll : 0;
       uint32_t* s32 = reinterpret_cast<uint32_t*>(slot);          // (4-byte aligned rows)
@@ -1666,76 +1764,89 @@ __device__ __forceinline__ uint64_t part_at(const Recs& I, uint32_t p, const uns
 // coalesced.  3 blocks (24 waves) per CU.
 constexpr int SB = 512, SR = 8, SCH = SB * SR;
 constexpr int SMAXB = 128;                    // <= 7 bits per pass
+// start (NULL: 0): per input region, the records below it are already split
+// (pg_build_host's early split); a block loops over its region's records in
+// steps of bpr * SCH.
 __global__ void __launch_bounds__(SB, 6)
-k_split(Recs I, Recs O, uint32_t shift, uint32_t nb, uint32_t bpr, unsigned* __restrict__ flags) {
+k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t shift, uint32_t nb, uint32_t bpr,
+        unsigned* __restrict__ flags) {
   __shared__ uint32_t s_cnt[SMAXB], s_pos[SMAXB];
   __shared__ unsigned long long s_base[SMAXB];
   __shared__ unsigned long long s_key[SCH];
   __shared__ uint32_t s_mw[SCH];
   const uint32_t g = blockIdx.x / bpr, j = blockIdx.x % bpr, p = g / I.nsub;
   const unsigned long long nr = I.cursor[CSTRIDE * (uint64_t)g];
-  const uint64_t n = nr < I.cap ? nr : I.cap, b0 = (uint64_t)j * SCH;
-  if (b0 >= n) return;                                         // block-uniform
-  if (threadIdx.x < SMAXB) s_cnt[threadIdx.x] = 0u;
-  const uint32_t cnt = (uint32_t)(n - b0 < (uint64_t)SCH ? n - b0 : (uint64_t)SCH);
-  const uint64_t in0 = (uint64_t)g * I.cap + b0;
-  unsigned long long key[SR];
-  uint32_t mw[SR], rk[SR];
+  const uint64_t n = nr < I.cap ? nr : I.cap;
+  uint64_t s0 = start ? start[g] : 0ull;
+  s0 = s0 < n ? s0 : n;
+  for (uint64_t b0 = s0 + (uint64_t)j * SCH; b0 < n; b0 += (uint64_t)bpr * SCH) {   // block-uniform
+    __syncthreads();                                           // (the last round's LDS reads are done)
+    if (threadIdx.x < SMAXB) s_cnt[threadIdx.x] = 0u;
+    const uint32_t cnt = (uint32_t)(n - b0 < (uint64_t)SCH ? n - b0 : (uint64_t)SCH);
+    const uint64_t in0 = (uint64_t)g * I.cap + b0;
+    unsigned long long key[SR];
+    uint32_t mw[SR], rk[SR];
 #pragma unroll
-  for (int e = 0; e < SR; ++e) {
-    const uint32_t i = (uint32_t)e * SB + threadIdx.x;
-    key[e] = i < cnt ? I.key[in0 + i] : 0ull;
-    mw[e] = i < cnt ? I.mw[in0 + i] : 0u;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int e = 0; e < SR; ++e) {
-    const uint32_t i = (uint32_t)e * SB + threadIdx.x;
-    rk[e] = i < cnt ? atomicAdd(&s_cnt[(uint32_t)(key[e] >> shift) & (nb - 1)], 1u) : 0u;
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {                     // exclusive scan of the bin counts, two bins per lane
-    const uint32_t l = threadIdx.x;
-    const uint32_t a = 2 * l < nb ? s_cnt[2 * l] : 0u, b = 2 * l + 1 < nb ? s_cnt[2 * l + 1] : 0u;
-    uint32_t x = a + b;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(x, o, 64);
-      if ((int)l >= o) x += y;
+    for (int e = 0; e < SR; ++e) {
+      const uint32_t i = (uint32_t)e * SB + threadIdx.x;
+      key[e] = i < cnt ? I.key[in0 + i] : 0ull;
+      mw[e] = i < cnt ? I.mw[in0 + i] : 0u;
     }
-    const uint32_t ex = x - a - b;
-    if (2 * l < nb) s_pos[2 * l] = ex;
-    if (2 * l + 1 < nb) s_pos[2 * l + 1] = ex + a;
-  }
-  if (threadIdx.x < nb) {
-    const uint32_t c = s_cnt[threadIdx.x];
-    s_base[threadIdx.x] = c ? atomicAdd(O.cursor + CSTRIDE * ((uint64_t)p * nb + threadIdx.x), (unsigned long long)c)
-                            : 0ull;
-  }
-  __syncthreads();
+    __syncthreads();
 #pragma unroll
-  for (int e = 0; e < SR; ++e) {
-    const uint32_t i = (uint32_t)e * SB + threadIdx.x;
-    if (i < cnt) {
-      const uint32_t b = (uint32_t)(key[e] >> shift) & (nb - 1);
-      const uint32_t d = s_pos[b] + rk[e];
-      s_key[d] = key[e];
-      s_mw[d] = mw[e];
+    for (int e = 0; e < SR; ++e) {
+      const uint32_t i = (uint32_t)e * SB + threadIdx.x;
+      rk[e] = i < cnt ? atomicAdd(&s_cnt[(uint32_t)(key[e] >> shift) & (nb - 1)], 1u) : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {                   // exclusive scan of the bin counts, two bins per lane
+      const uint32_t l = threadIdx.x;
+      const uint32_t a = 2 * l < nb ? s_cnt[2 * l] : 0u, b = 2 * l + 1 < nb ? s_cnt[2 * l + 1] : 0u;
+      uint32_t x = a + b;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if ((int)l >= o) x += y;
+      }
+      const uint32_t ex = x - a - b;
+      if (2 * l < nb) s_pos[2 * l] = ex;
+      if (2 * l + 1 < nb) s_pos[2 * l + 1] = ex + a;
+    }
+    if (threadIdx.x < nb) {
+      const uint32_t c = s_cnt[threadIdx.x];
+      s_base[threadIdx.x] = c ? atomicAdd(O.cursor + CSTRIDE * ((uint64_t)p * nb + threadIdx.x), (unsigned long long)c)
+                              : 0ull;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < SR; ++e) {
+      const uint32_t i = (uint32_t)e * SB + threadIdx.x;
+      if (i < cnt) {
+        const uint32_t b = (uint32_t)(key[e] >> shift) & (nb - 1);
+        const uint32_t d = s_pos[b] + rk[e];
+        s_key[d] = key[e];
+        s_mw[d] = mw[e];
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += SB) {
+      const unsigned long long kk = s_key[i];
+      const uint32_t b = (uint32_t)(kk >> shift) & (nb - 1);
+      const unsigned long long pos = s_base[b] + (i - s_pos[b]);
+      if (pos < O.cap) {
+        const uint64_t at = ((uint64_t)p * nb + b) * O.cap + pos;
+        O.key[at] = kk;
+        O.mw[at] = s_mw[i];
+      } else {
+        atomicOr(flags + 4, F_SPLIT_OVER);
+      }
     }
   }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < cnt; i += SB) {
-    const unsigned long long kk = s_key[i];
-    const uint32_t b = (uint32_t)(kk >> shift) & (nb - 1);
-    const unsigned long long pos = s_base[b] + (i - s_pos[b]);
-    if (pos < O.cap) {
-      const uint64_t at = ((uint64_t)p * nb + b) * O.cap + pos;
-      O.key[at] = kk;
-      O.mw[at] = s_mw[i];
-    } else {
-      atomicOr(flags + 4, F_SPLIT_OVER);
-    }
-  }
+}
+// the stage A cursors as the early split's next start
+__global__ void k_snap(const unsigned long long* __restrict__ cursor, unsigned long long* __restrict__ snap, uint32_t n) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g < n) snap[g] = cursor[CSTRIDE * (uint64_t)g];
 }
 
 // ---------------------------------------------------------------- stage C
@@ -1815,6 +1926,9 @@ __device__ __forceinline__ uint64_t part_count(const Recs& I, uint32_t f, uint32
   const unsigned long long n = I.cursor[CSTRIDE * (uint64_t)f + z];
   return n < I.cap ? n : I.cap;
 }
+// s_waitcnt vmcnt(0), leaving the LDS / scalar counter alone (gfx9 encoding:
+// vmcnt 0, expcnt 7, lgkmcnt 15)
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
 __global__ void __launch_bounds__(RB_T, 4)
 k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, unsigned* __restrict__ flags) {
@@ -1850,6 +1964,15 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
   uint64_t n_cur = f < nparts ? part_count(I, f, z) : 0;
   uint64_t n_nxt = f + G < nparts ? part_count(I, f + G, z) : 0;
   load(f, n_cur, ch, cm);
+  // Vector memory counts (vmcnt) are in order and count stores too: a wait for
+  // a load issued before stores of unknown number is a wait for those stores.
+  // So the loads are waited for explicitly at points where nothing else is in
+  // flight - here, and in the loop before the range goes out - and never where
+  // the compiler would put the wait itself: at the loop head, where the first
+  // partition's loads from here meet the back edge (which made every
+  // iteration wait for its own prefetch right after issuing it), and at the
+  // end, behind the range's stores.
+  wait_vm();
   uint32_t created = 0, ndbg = 0;
   const uint64_t mseg = (uint64_t)blockIdx.x * R.cap;
   // rdBG members: each wave queues h (| 1 << 63 for the rc orientation) in its
@@ -1869,7 +1992,7 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       const uint64_t c = T.unperm(e & ~(1ull << 63));
       const uint64_t o = base + lane;
       if (o < R.cap) R.keys[mseg + o] = (e >> 63) ? T.rc(c) : c;
-      else atomicOr(flags + 4, F_RSEG_OVER);
+      else { (void)PG_BOK(false, 53, (long long)o, (long long)R.cap); atomicOr(flags + 4, F_RSEG_OVER); }
     }
     mp = 0;
   };
@@ -1888,7 +2011,7 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
   __syncthreads();
   for (; f < nparts; f += G) {                                 // block-uniform
     if (!(PG_EXP_BITS & 4)) load(f + G, n_nxt, nh, nm);       // in flight during this partition
-    const uint64_t n_nn = f + 2 * G < nparts ? part_count(I, f + 2 * G, z) : 0;
+    unsigned long long n_nn = f + 2 * G < nparts ? I.cursor[CSTRIDE * (uint64_t)(f + 2 * G) + z] : 0ull;  // (raw)
 #pragma unroll
     for (int e = 0; e < RB_R; ++e)
       if (cm[e] && !(PG_EXP_BITS & 2))
@@ -1898,7 +2021,25 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       range_or(W, OK, OM, T, h, I.mw[(uint64_t)f * I.cap + r], (uint32_t)(h >> T.qbits) & (rng - 1), qmask, flags);
     }
     __syncthreads();
-    // the range out whole; counts; members queued; LDS zeroed
+    wait_vm();                                                   // the prefetch landed under the merge
+    asm volatile("" : "+v"(n_nn));
+    n_nn = n_nn < I.cap ? n_nn : I.cap;
+    // the LDS overflow set first (its HBM probes wait on vmcnt: before the
+    // range's stores, not behind them), then the range out whole; counts;
+    // members queued; LDS zeroed
+    static_assert(OVL % 64 == 0, "whole waves");
+    for (uint32_t i = threadIdx.x; i < OVL; i += RB_T) {
+      const unsigned long long kk = OK[i];
+      const uint32_t m = OM[i];
+      if (kk) {
+        ovf_or(T, T.unperm(kk - 1ull), m, flags + 4);
+        ++created;
+        ndbg += ((m >> 12) & 1u) + ((m >> 25) & 1u);
+        OK[i] = 0ull;
+        OM[i] = 0u;
+      }
+      push(kk - 1ull, kk ? member_bits(m) : 0u);
+    }
     const uint64_t b0 = (uint64_t)f << rbits;
     for (uint32_t i0 = 0; i0 < rng; i0 += RB_T) {              // every lane runs every trip (wave scans)
       const uint32_t i = i0 + threadIdx.x;
@@ -1917,19 +2058,6 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
         push(((b0 + i) << T.qbits) | (x >> MW_BITS), bx);
         push(((b0 + i) << T.qbits) | (y >> MW_BITS), by);
       }
-    }
-    static_assert(OVL % 64 == 0, "whole waves");
-    for (uint32_t i = threadIdx.x; i < OVL; i += RB_T) {
-      const unsigned long long kk = OK[i];
-      const uint32_t m = OM[i];
-      if (kk) {
-        ovf_or(T, T.unperm(kk - 1ull), m, flags + 4);
-        ++created;
-        ndbg += ((m >> 12) & 1u) + ((m >> 25) & 1u);
-        OK[i] = 0ull;
-        OM[i] = 0u;
-      }
-      push(kk - 1ull, kk ? member_bits(m) : 0u);
     }
     __syncthreads();
     if (PG_EXP_BITS & 4) load(f + G, n_nxt, nh, nm);
@@ -2247,7 +2375,7 @@ static BinOut stageA_begin(Ctx& c, uint64_t cap, FillList& fl, bool reset = true
 
 struct ACount {
   uint64_t total = 0, maxreg = 0, maxbin = 0;
-  unsigned sentinel = 0, bits = 0;
+  unsigned sentinel = 0, bits = 0, bits_bc = 0;     // bits: flags[1] (stage A), bits_bc: flags[4] (stages B/C)
 };
 // stage A's counts and flags from a pinned copy of ctrA and the flags
 static ACount stageA_counts(const unsigned long long* h, const unsigned* fl, int stride = CSTRIDE) {
@@ -2264,6 +2392,7 @@ static ACount stageA_counts(const unsigned long long* h, const unsigned* fl, int
   }
   a.sentinel = fl[0];
   a.bits = fl[1];
+  a.bits_bc = fl[4];
   return a;
 }
 
@@ -2291,10 +2420,52 @@ static uint64_t region_cap(uint64_t est) { return est / NREG + est / (NREG * 10)
 // counts and flags come back with the same sync.  Returns false (with the
 // exact counts in `a`) if stage A overflowed a region; a B/C flag re-runs B/C
 // with the exact counts.
-static bool finish_build(Ctx& c, ACount& a, bool spec) {
+// The table geometry finish_build picks for `total` stage A records: bucket
+// bits bb, fine partition bits fp.
+static void table_bits(const Ctx& c, uint64_t total, int& bb, int& fp) {
+  bb = std::max(1, log2u(std::max<uint64_t>(total, 1)));
+  bb = std::min(std::max({bb - c.bb_shift, c.cbits, c.kb - 38}), c.kb);
+  fp = std::max(c.cbits, bb - RANGE_BITS);
+}
+// pg_build_host's early split (stage B under the upload): made for bucket
+// bits bb, one split level of S bits into partitions of `cap` records, in
+// c.recS_*[0] with cursors at c.ctrS
+struct Presplit {
+  int bb;
+  uint32_t S;
+  uint64_t cap;
+};
+
+#ifdef PG_DEBUG_BOUNDS
+static void debug_report(const char* where) {
+  static unsigned long long h[16 + 16 * 4 * 5];
+  PG_HIP(hipDeviceSynchronize());
+  PG_HIP(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_dbg), sizeof(h)));
+  bool any = false;
+  for (int sl = 0; sl < 16; ++sl) {
+    if (!h[sl]) continue;
+    any = true;
+    std::fprintf(stderr, "PG_DEBUG_BOUNDS %s: slot %d: %llu violations\n", where, sl, h[sl]);
+    for (unsigned long long i = 0; i < h[sl] && i < 4; ++i) {
+      const unsigned long long* e = h + 16 + (sl * 4 + i) * 5;
+      std::fprintf(stderr, "  check %llu a=%lld b=%lld block=%llu thread=%llu\n", e[0], (long long)e[1], (long long)e[2],
+                   e[3], e[4]);
+    }
+  }
+  if (any) {
+    static unsigned long long z[16 + 16 * 4 * 5] = {};
+    PG_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), z, sizeof(z)));
+  }
+}
+#else
+static void debug_report(const char*) {}
+#endif
+
+static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nullptr) {
   const int kb = c.kb, cb = c.cbits;
-  int bb = std::max(1, log2u(std::max<uint64_t>(a.total, 1)));
-  bb = std::min(std::max({bb - c.bb_shift, cb, kb - 38}), kb);
+  int bb, fp0;
+  table_bits(c, a.total, bb, fp0);
+  (void)fp0;
   double capx = 1.15;
   uint64_t ovf_mult = 1;
   double rseg_frac = c.r_ratio > 0 ? std::min(2.0, 1.5 * c.r_ratio + 0.002) : 2.0;
@@ -2304,6 +2475,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
   std::vector<uint64_t> lv_exact;
   int lv_exact_bb = -1;
   c.t6.init();
+  debug_report("stage A");
   for (int attempt = 0; attempt < 8; ++attempt) {
     const int fp = std::max(cb, bb - RANGE_BITS);
     const uint32_t rbits = (uint32_t)(bb - fp);
@@ -2323,12 +2495,16 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
     std::vector<Lv> lv;
     uint64_t maxin = a.maxbin, maxreg = a.maxreg, nsub = 8, ctr_words = 0;
     // (no split needed: one S = 0 pass still gathers each bin's 8 regions into one)
+    // the early split's partitions, when they are this attempt's only level
+    const bool use_pre = pre && attempt == 0 && pre->bb == bb && fp - cb == (int)pre->S && fp > cb &&
+                         fp - cb <= 7 && !spec;
     for (int L = cb; L < fp || lv.empty();) {
       const int S = std::min(7, fp - L);
       const uint64_t pin = 1ull << L, nb = 1ull << S;
       uint64_t capo = (uint64_t)((double)maxin / (double)nb * capx) + 64;
       if (lv_exact_bb == bb && lv.size() < lv_exact.size())
         capo = std::max(capo, lv_exact[lv.size()] + lv_exact[lv.size()] / 16 + 64);
+      if (use_pre) capo = pre->cap;
       lv.push_back(Lv{L, S, pin, capo, pin * nsub, std::max<uint64_t>(1, (maxreg + SCH - 1) / SCH), ctr_words});
       ctr_words += CSTRIDE * pin * nb;
       maxin = maxreg = capo;
@@ -2351,8 +2527,10 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
     c.k5_ctr.reserve(8 * RB_CTR * grid);
     FillList fl;
     fl.add(c.ovf.p, sizeof(Slot) * ovf);
-    fl.add(c.ctrS.p, 8 * ctr_words);
-    fl.add(c.flags.as<unsigned>() + 4, 16);                   // stage B/C bits (not the sentinel)
+    if (!use_pre) {                                           // (the early split's counts are in ctrS)
+      fl.add(c.ctrS.p, 8 * ctr_words);
+      fl.add(c.flags.as<unsigned>() + 4, 16);                 // stage B/C bits (not the sentinel)
+    }
     // the fills (C3: the 64 MB overflow table, 12 us) go on the side stream,
     // behind its share of stage A (which touches none of them), so that they
     // run beside stage A's last work pass; stage B waits for them
@@ -2373,9 +2551,14 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
       const uint32_t nb = 1u << l.S;
       Recs out{c.recS_key[i & 1].as<unsigned long long>(), c.recS_mw[i & 1].as<uint32_t>(),
                c.ctrS.as<unsigned long long>() + l.ctr_off, l.cap, 1};
+      if (use_pre) {                                          // split already, chunk by chunk
+        in = out;
+        continue;
+      }
       if (l.nreg * l.bpr >= (1ull << 31)) throw Error(-22, "build: split grid too large");
       hipLaunchKernelGGL(k_split, dim3((unsigned)(l.nreg * l.bpr)), dim3(SB), 0, c.stream, in, out,
-                         (uint32_t)(kb - l.L - l.S), nb, (uint32_t)l.bpr, c.flags.as<unsigned>());
+                         (const unsigned long long*)nullptr, (uint32_t)(kb - l.L - l.S), nb, (uint32_t)l.bpr,
+                         c.flags.as<unsigned>());
       PG_HIP(hipGetLastError());
       in = out;
     }
@@ -2454,6 +2637,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec) {
     c.n_rdbg = nr + c.sentinel;               // key 2^64-1, mask 32: always an rdBG member
     c.r_ratio = a.total ? (double)nr / (double)a.total : 0.0;
     c.built = c.reduced = true;
+    c.early_split_used = use_pre;
     ++c.build_gen;
     return true;
   }
@@ -2524,6 +2708,12 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   c.t1.init();
   c.t1.start(s0);
   fl.launch(s0);
+#ifdef PG_DEBUG_BOUNDS
+  for (int i = 0; i < nch; ++i)
+    hipLaunchKernelGGL(k_dbg_counters, dim3(1), dim3(64), 0, s0,
+                       reinterpret_cast<const unsigned long long*>(c.k3_queue.as<uint8_t>() + qbytes) + (cbytes / 8) * i,
+                       0ull, 41u, (unsigned)i);
+#endif
   const unsigned wgrid = (unsigned)c.n_cu * (c.k3_wblk & 15 ? c.k3_wblk & 15 : K3_WBLK);
   const unsigned wgrid_last = c.k3_wblk >> 4 ? (unsigned)c.n_cu * (c.k3_wblk >> 4) : wgrid;
   auto* q = c.k3_queue.as<WorkItem>();
@@ -2548,10 +2738,15 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
                          c.k3_hint.as<int>(), (int)c.n_records, ntiles, cb[i], cb[i + 1], cbt);
     else if (gc[i])
       hipLaunchKernelGGL(k_cover_p, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, c.p2.as<uint32_t>(),
-                         c.e16.as<uint8_t>(), (uint64_t)(c.p2.cap / 4), td, qi, qni, (unsigned long long)qcapc[i], c.k,
+                         c.e16.as<uint8_t>(), (uint64_t)(c.p2.cap / 4), cls, td, qi, qni, (unsigned long long)qcapc[i], c.k,
                          c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
                          cb[i], cb[i + 1], cbt);
     PG_HIP(hipGetLastError());
+#ifdef PG_DEBUG_BOUNDS
+    for (int j = 0; j < nch; ++j)                 // this chunk's counters in range, the later ones still zero
+      hipLaunchKernelGGL(k_dbg_counters, dim3(1), dim3(64), 0, s0, qn + (cbytes / 8) * j,
+                         j <= i ? (unsigned long long)qcapc[j] : 0ull, j <= i ? 43u : 44u, (unsigned)(i * 10 + j));
+#endif
     hipStream_t ws = s1;
     if (nch > 1 && i + 1 == nch) {
       ws = s0;
@@ -2590,6 +2785,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
 
 void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   if (!c.parsed) throw Error(-22, "build_dbg: no parsed FASTA (call pg_parse first)");
+  c.early_split_used = false;
   const uint64_t R = c.n_records;
   c.rc0 = rc0;
   c.built = c.reduced = false;
@@ -2791,6 +2987,7 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
 // the records, then stages B and C as a build).
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, int sentinel) {
   init_hash(c);
+  c.early_split_used = false;
   uint64_t cap = region_cap(n + 64);
   ACount a;
   // every record count is known here (n): stages B/C go right behind stage A
@@ -2857,6 +3054,53 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
   uint64_t done = 0;
   bool started = false, broken = c.n_preload != 0;
   c.t1.init();
+  // Stage B under the upload: after each chunk's stage A share, the records
+  // it added are split into the table's fine partitions (k_split from the
+  // stage A cursors' last snapshot, on the main stream, where no stage A
+  // kernel runs beside it), so that after the last chunk only its own records
+  // are left to split.  The geometry comes from the last build (records per
+  // window, windows per byte); at the end finish_build uses the partitions if
+  // the exact count gives the same table and nothing overflowed, and splits
+  // everything again from stage A's regions (still intact) otherwise.
+  Presplit pre{-1, 0u, 0};
+  uint32_t pre_bpr = 1;
+  if (c.early_split && c.u_ratio > 0 && c.w_ratio > 0 && !broken) {
+    const uint64_t est = (uint64_t)(c.u_ratio * c.w_ratio * (double)n) + 4096;
+    int bb, fp;
+    table_bits(c, est, bb, fp);
+    if (fp > c.cbits && fp - c.cbits <= 7) {
+      pre.bb = bb;
+      pre.S = (uint32_t)(fp - c.cbits);
+      const uint64_t maxbin = est / NBIN + est / (NBIN * 8) + 1024;      // bins are even: h is a bijective hash
+      pre.cap = (uint64_t)((double)maxbin / (double)(1u << pre.S) * 1.3) + 256;
+      const uint64_t recs = (1ull << c.cbits) * (1ull << pre.S) * pre.cap;
+      c.recS_key[0].reserve(8 * recs);
+      c.recS_mw[0].reserve(4 * recs);
+      c.ctrS.reserve(8 * CSTRIDE * (1ull << fp));
+      c.snapA.reserve(8 * NREG);
+      pre_bpr = 2;
+    }
+  }
+  bool pre_started = false;
+  auto early_split = [&]() {
+    if (pre.bb < 0) return;
+    if (!pre_started) {
+      PG_HIP(hipMemsetAsync(c.ctrS.p, 0, 8 * CSTRIDE * (1ull << (c.cbits + pre.S)), c.stream));
+      PG_HIP(hipMemsetAsync(c.snapA.p, 0, 8 * NREG, c.stream));
+      pre_started = true;
+    }
+    const Recs in{c.recA_key.as<unsigned long long>(), c.recA_mw.as<uint32_t>(), c.ctrA.as<unsigned long long>(),
+                  c.capA, 8};
+    const Recs out{c.recS_key[0].as<unsigned long long>(), c.recS_mw[0].as<uint32_t>(),
+                   c.ctrS.as<unsigned long long>(), pre.cap, 1};
+    hipLaunchKernelGGL(k_split, dim3((unsigned)(NREG * pre_bpr)), dim3(SB), 0, c.stream, in, out,
+                       c.snapA.as<unsigned long long>(), (uint32_t)(c.kb - c.cbits - (int)pre.S), 1u << pre.S, pre_bpr,
+                       c.flags.as<unsigned>());
+    PG_HIP(hipGetLastError());
+    hipLaunchKernelGGL(k_snap, dim3((NREG + 255) / 256), dim3(256), 0, c.stream, c.ctrA.as<unsigned long long>(),
+                       c.snapA.as<unsigned long long>(), (uint32_t)NREG);
+    PG_HIP(hipGetLastError());
+  };
   std::function<void(uint64_t)> on_chunk = [&](uint64_t rc) {
     if (broken) return;
     if (rc == ~0ull) { broken = true; return; }               // the parse could not stream
@@ -2873,9 +3117,13 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
       const uint64_t nt = make_tiles(c, flag);
       enqueue_stageA(c, cap, nt, rc0, 0, SA_FIRST);
       started = true;
+      early_split();
     } else {
       const uint64_t nt = make_tiles(c, flag, true);
-      if (nt) enqueue_stageA(c, cap, nt, rc0, 0, SA_MORE);
+      if (nt) {
+        enqueue_stageA(c, cap, nt, rc0, 0, SA_MORE);
+        early_split();
+      }
     }
     done = rc;
   };
@@ -2897,14 +3145,17 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
     c.last_extra = 0;
     c.dump_ready = false;
     enqueue_stageA(c, cap, 0, rc0, 0, SA_TAIL);
+    if (pre_started) early_split();                           // the last chunk's records and the short ones
     ACount a = stageA_read(c);
     if (!(a.bits & F_A_OVER)) {
       c.ms_insert = c.t1.ms();
       c.ms_clear = 0;
       c.sentinel = a.sentinel ? 1 : 0;
       c.n_records_a = a.total;
-      finish_build(c, a, false);
+      const bool pre_ok = pre_started && !(a.bits_bc & F_SPLIT_OVER);
+      finish_build(c, a, false, pre_ok ? &pre : nullptr);
       if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
+      if (n) c.w_ratio = (double)c.windows_fw / (double)n;
       c.tile_sig_len.clear();                                 // (the tile list holds the last batch only)
       return;
     }

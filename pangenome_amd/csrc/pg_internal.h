@@ -144,6 +144,7 @@ struct Ctx {
   int k3_emit = 0;                // pg_tune: work pass (0 = two halves per segment, 1 = one)
   int k3_tail = 0;                // pg_tune: last K3 chunk in 16ths of the others (0 = 16)
   int k3_cover = 0;               // pg_tune: coverage pass (0 = packed form, 1 = LDS-staged members, 2 = quad form)
+  int early_split = 1;            // pg_tune: pg_build_host splits each landed chunk's records (stage B under the upload)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
   int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
   uint64_t stage_piece = 32ull << 20;  // pg_tune: bytes per staging-ring slot (one DMA)
@@ -198,6 +199,9 @@ struct Ctx {
   uint64_t capA = 0;                  // records per stage A region
   DevBuf recS_key[2], recS_mw[2];     // stage B outputs (ping-pong)
   DevBuf ctrS;                        // stage B cursors, all levels
+  DevBuf snapA;                       // pg_build_host's early split: stage A cursors already split
+  double w_ratio = 0;                 // last host build: forward windows per input byte
+  bool early_split_used = false;      // the last pg_build_host's stage C read the early split's partitions
   DevBuf rseg;                        // rdBG keys: one segment of rseg_cap per stage C block
   DevBuf k5_ctr;                      // per stage C block: key / dBG / member counts
   uint64_t rseg_cap = 0, rseg_nseg = 0;

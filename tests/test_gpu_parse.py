@@ -322,3 +322,26 @@ def test_build_device_one_call(oracle_mod):
         assert np.array_equal(ctx.rdbg(), rk), i
     ctx.close()
 
+
+
+def test_build_host_early_split():
+    """Stage B under the upload (PG_TUNE_EARLY_SPLIT): a warm pg_build_host
+    splits each landed chunk's records into the table's partitions (geometry
+    from the first build) and stage C reads them (build_flags bit 0) - the
+    oracle's dBG and rdBG either way, and with the early split turned off."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context, PG_TUNE_EARLY_SPLIT, PG_TUNE_H2D_CHUNK
+    buf = synth.pangenome(24, 250_000, snp=1e-2, indel=1e-3, seed=31)   # > 2^19 stage A records: a split level
+    ref = _oracle_ref(buf)
+    ctx = Context(27)
+    ctx.tune(PG_TUNE_H2D_CHUNK, 256 * 1024)
+    used = []
+    for early in (1, 1, 1, 0, 1):
+        ctx.tune(PG_TUNE_EARLY_SPLIT, early)
+        st = ctx.build_host(buf, True)
+        _check_build(ctx, st, ref)
+        used.append(int(st.build_flags) & 1)
+    ctx.close()
+    # build 1 may still fall back (its capacity estimate comes from build 0's
+    # ratios alone); from build 2 on the estimate holds
+    assert used[0] == 0 and used[2] == 1 and used[3] == 0 and used[4] == 1, used

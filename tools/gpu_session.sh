@@ -22,13 +22,16 @@ for step in "$@"; do
     benchq) run bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     rehearse2) run bench_rehearse2 900 env PG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 2 --warmup 1 ;;
     rehearse2c3) run bench_rehearse2c3 600 env PG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --config c3 --steps 3 --warmup 1 ;;
-    cover) run pytest_cover 600 python -u -m pytest tests/test_gpu_parity.py -k "k3" -x -v --timeout 120 --timeout-method thread ;;
+    cover) run pytest_cover 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parse.py tests/test_gpu_rccl.py -k "k3 or early_split or build_host or rccl" -v --timeout 120 --timeout-method thread ;;
+    dbgc3) run dbg_c3 400 env PG_LIB_NAME=libpangenome_hip_dbg.so python -u tools/dbg_host_c3.py 0 2 ;;
+    missing) run dbg_missing 400 env PG_LIB_NAME=libpangenome_hip_dbg.so python -u tools/dbg_missing.py gpurun_out/missing.npz ;;
     bracket) run bracket_sort 500 python -u tools/corruption_bracket.py sort ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window ;;
     pmc) bash tools/pmc_kernels.sh "k_span_sum|k_emit|k_records|k_cover|k_short_emit|k_split|k_build_range|rocprim" tr traffic ;;
     parity) run pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -v --timeout 120 --timeout-method thread ;;
+    abcover) run ab_cover 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=2 ;;
     ab) run ab_k3 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=1 ;;
     listctr) run listctr 300 rocprofv3 -L ;;
     *) echo "unknown step $step"; exit 2 ;;
