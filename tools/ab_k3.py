@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Development A/B of K3 variants on the C3 batch c3a, HBM-resident input
-(pg_build_device), alternating the variants step by step in one process.
+(pg_build_device; --host: pg_build_host from the mmap), alternating the variants step by step in one process.
 
     python tools/ab_k3.py [--steps 12] [--tune WHAT=V,WHAT=V ...] ...
 
@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--genomes", type=int, default=100)
     ap.add_argument("--tune", action="append", default=[])
+    ap.add_argument("--host", action="store_true", help="pg_build_host from the page-cache-warm mmap instead")
     args = ap.parse_args()
     import torch
     from pangenome_amd import _lib, kmer, synth
@@ -37,7 +38,8 @@ def main():
     print("generated %.1f s" % (time.time() - t0), flush=True)
     mm = kmer.seq2bytes(p)
     d = torch.from_numpy(np.array(mm)).to("cuda:0")
-    os.unlink(p)
+    if not args.host:
+        os.unlink(p)
     dig = json.load(open(os.path.join(ROOT, "tests", "golden", "scale", "c3a.json"))) if args.genomes == 100 else None
     ctxs = []
     for v in variants:
@@ -52,7 +54,10 @@ def main():
         for v, ctx in zip(variants, ctxs):
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            st = ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d)
+            if args.host:
+                st = ctx.build_host(mm, True)
+            else:
+                st = ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d)
             ms = 1e3 * (time.perf_counter() - t1)
             ok = dig is None or (st.n_dbg, st.n_rdbg) == (dig["n_dbg"], dig["n_rdbg"])
             if step >= 2:

@@ -28,10 +28,12 @@ for step in "$@"; do
     bracket) run bracket_sort 500 python -u tools/corruption_bracket.py sort ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
-    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window ;;
-    pmc) bash tools/pmc_kernels.sh "k_span_sum|k_emit|k_records|k_cover|k_short_emit|k_split|k_build_range|rocprim" tr traffic ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange ;;
+    pmc) bash tools/pmc_kernels.sh "k_span_sum|k_emit|k_records|k_pack_fix|k_cover|k_short_emit|k_split|k_build_range|rocprim" tr traffic ;;
     parity) run pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -v --timeout 120 --timeout-method thread ;;
     abcover) run ab_cover 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=2 ;;
+    abhost) run ab_host 600 python -u tools/ab_k3.py --host --steps 12 --tune base --tune EARLY_SPLIT=0 --tune K3_COVER=2 --tune EARLY_SPLIT=0,K3_COVER=2 ;;
+    abdev) run ab_dev 600 python -u tools/ab_k3.py --steps 12 --tune base --tune EARLY_SPLIT=0 --tune K3_COVER=2 ;;
     ab) run ab_k3 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=1 ;;
     listctr) run listctr 300 rocprofv3 -L ;;
     *) echo "unknown step $step"; exit 2 ;;
