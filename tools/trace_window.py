@@ -1,28 +1,44 @@
 #!/usr/bin/env python3
-"""Development trace (not part of the product): 6 host-window builds of C3
-batch A (pg_build_host from a populated mmap), for rocprofv3 --kernel-trace
---memory-copy-trace; tools/trace_step.py-style analysis reads the db."""
-import os
+"""The last pg_build_host window of a rocprofv3 --kernel-trace
+--memory-copy-trace run (gpurun_out/<dir>/): every copy and kernel from the
+window's first H2D chunk on, relative to it, and the tail - what runs after
+the last H2D chunk has landed.  Development tool.
+
+    rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tw -o run \\
+        --output-format csv -- python tools/ab_k3.py --host --steps 3
+    python tools/trace_window.py gpurun_out/tw"""
+import csv
+import glob
+import re
 import sys
-import tempfile
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "tests"))
-
-
-def main():
-    from pangenome_amd import kmer, synth
-    from pangenome_amd._lib import Context
-    d = tempfile.mkdtemp()
-    q = os.path.join(d, "c3.fa")
-    synth.write_pangenome(q, 100, 5_000_000, workers=8)
-    mm = kmer.seq2bytes(q)
-    ctx = Context(27)
-    for _ in range(6):
-        st = ctx.build_host(mm, True)
-    print(st.n_dbg, st.n_rdbg, flush=True)
-
-
-if __name__ == "__main__":
-    main()
+d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/tw"
+kt = list(csv.DictReader(open(glob.glob(d + "/**/*kernel_trace.csv", recursive=True)[0])))
+mf = glob.glob(d + "/**/*memory_copy_trace.csv", recursive=True)
+mt = list(csv.DictReader(open(mf[0]))) if mf else []
+ev = []
+for r in kt:
+    ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K", re.sub(r"\(.*", "", r["Kernel_Name"])[-44:],
+               r.get("Queue_Id", "")))
+for r in mt:
+    kind = r.get("Direction") or r.get("Operation") or "COPY"
+    n = int(r.get("Bytes", 0) or 0) if "Bytes" in r else 0
+    ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C", "%s %d MB" % (kind, n >> 20), ""))
+ev.sort()
+# the last window: from the last k_span_sum that follows a large H2D copy
+h2d = [e for e in ev if e[2] == "C" and "HOST_TO_DEVICE" in e[3].upper() and int(e[3].split()[-2]) >= 16]
+if not h2d:
+    sys.exit("no H2D chunk copies in the trace (run with --memory-copy-trace)")
+# windows start where consecutive big copies are separated by > 1 ms
+starts = [h2d[0][0]] + [b[0] for a, b in zip(h2d, h2d[1:]) if b[0] - a[1] > 1_000_000]
+t0 = starts[-1]
+win = [e for e in ev if e[0] >= t0]
+last_copy_end = max(e[1] for e in h2d if e[0] >= t0)
+end = max(e[1] for e in win if e[2] == "K" and e[0] < last_copy_end + 5_000_000)
+print("window: first chunk at 0, last chunk landed at %.1f us, last kernel ends at %.1f us (tail %.1f us)"
+      % ((last_copy_end - t0) / 1e3, (end - t0) / 1e3, (end - last_copy_end) / 1e3))
+for s, e, kind, name, q in win:
+    if s > end:
+        break
+    mark = " *" if s >= last_copy_end else ""
+    print("%9.1f %9.1f %8.1f %s q%-3s %s%s" % ((s - t0) / 1e3, (e - t0) / 1e3, (e - s) / 1e3, kind, q, name, mark))
