@@ -140,6 +140,15 @@ int pg_rdbg_export(pg_ctx* ctx, uint64_t* keys, uint64_t cap, uint64_t* n);
  * find_prime(cap * 1.62) while size > 0.75 * cap, :423-474).  keys == NULL
  * only sets *capacity and *size (call again with arrays of *capacity). */
 int pg_dbg_dump(pg_ctx* ctx, uint64_t* capacity, uint64_t* keys, uint16_t* values, uint8_t* counts, uint64_t* size);
+/* pg_dbg_dump straight into an open file (dump() :243-261 without a host
+ * copy of the slot arrays): the keys / values / counts arrays (8, 2 and 1 B
+ * per slot) are written at file offsets offsets[0..2] of descriptor fd
+ * (pwrite, in 16 MiB pieces streamed from the device through pinned buffers
+ * by up to 16 host threads) and crcs[0..2] receive each array's CRC-32.  The
+ * .npy headers and the zip framing around them are the caller's
+ * (host.write_db_npz).  fd < 0 only sets *capacity and *size. */
+int pg_dbg_dump_fd(pg_ctx* ctx, uint64_t* capacity, int fd, const uint64_t* offsets, uint32_t* crcs,
+                   uint64_t* size);
 /* Stage (oriented key, 12-bit mask, count) pairs — the counts > 0 slots of a
  * loaded npz — to be OR-merged into every following pg_build_dbg (-d: a dBG
  * with no records inserted; -D: rdBG keys with mask 0, members by the rdBG
@@ -241,6 +250,9 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * as soon as its stage A share is done (geometry from the last build; a
  * mismatch at the end re-splits everything), 0 = after the last chunk. */
 #define PG_TUNE_EARLY_SPLIT 14
+/* PG_TUNE_K3_HEAD: size of the first K3 chunk in 16ths of the middle ones
+ * (1..64, 0 = 16: the coverage pass that runs before any work pass). */
+#define PG_TUNE_K3_HEAD 15
 /* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
  * count asks (0..8): exercises the overflow set, its spill and the re-run
  * with more buckets (results are unchanged). */

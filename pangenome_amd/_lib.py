@@ -29,6 +29,7 @@ PG_TUNE_K3_WBLK = 11
 PG_TUNE_K3_EMIT = 12
 PG_TUNE_K3_TAIL = 13
 PG_TUNE_EARLY_SPLIT = 14
+PG_TUNE_K3_HEAD = 15
 
 
 class PgStats(C.Structure):
@@ -81,6 +82,7 @@ SIGNATURES = {
     "pg_get_stats": (C.c_int, [_P, _SP]),
     "pg_tune": (C.c_int, [_P, C.c_int, C.c_int64]),
     "pg_dbg_dump": (C.c_int, [_P, _U64P, _P, _P, _P, _U64P]),
+    "pg_dbg_dump_fd": (C.c_int, [_P, _U64P, C.c_int, _P, _P, _U64P]),
     "pg_dbg_load": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_oakht_capacity": (C.c_uint64, [C.c_uint64]),
     "pg_device_bytes": (C.c_uint64, [C.c_int]),
@@ -279,6 +281,22 @@ class Context:
         check(self.lib.pg_dbg_dump(self.h, C.byref(cap), ptr(keys), ptr(values), ptr(counts), C.byref(size)),
               "pg_dbg_dump")
         return cap.value, size.value, keys, values, counts
+
+    def dbg_dump_size(self, capacity: int = 0):
+        """(capacity, size) of dbg_dump without placing or copying anything."""
+        cap, size = C.c_uint64(capacity), C.c_uint64()
+        check(self.lib.pg_dbg_dump_fd(self.h, C.byref(cap), -1, None, None, C.byref(size)), "pg_dbg_dump_fd")
+        return cap.value, size.value
+
+    def dbg_dump_fd(self, fd: int, offsets, capacity: int):
+        """The slot arrays of dbg_dump(capacity) written into the open file
+        `fd` at offsets[0..2] (keys, values, counts); their CRC-32s."""
+        cap, size = C.c_uint64(capacity), C.c_uint64()
+        off = np.ascontiguousarray(offsets, dtype=np.uint64)
+        crc = np.zeros(3, np.uint32)
+        check(self.lib.pg_dbg_dump_fd(self.h, C.byref(cap), int(fd), ptr(off), ptr(crc), C.byref(size)),
+              "pg_dbg_dump_fd")
+        return [int(x) for x in crc]
 
     def dbg_load(self, keys, masks=None, counts=None):
         """Stage oriented (key, mask, count) slots for the following builds."""

@@ -94,6 +94,7 @@ void pg_destroy(pg_ctx* x) {
   c.h_pin.release();
   c.h_out.release();
   c.tile_pin.release();
+  for (auto& b : c.dump_pin) b.release();
   c.t0.destroy();
   c.t1.destroy();
   c.t6.destroy();
@@ -288,6 +289,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || value > 64) throw pg::Error(PG_EINVAL, "pg_tune: K3 tail must be in [0, 64]");
         x->c.k3_tail = (int)value;
         break;
+      case PG_TUNE_K3_HEAD:
+        if (value < 0 || value > 64) throw pg::Error(PG_EINVAL, "pg_tune: K3 head must be in [0, 64]");
+        x->c.k3_head = (int)value;
+        break;
       case PG_TUNE_EARLY_SPLIT:
         if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: early split must be 0 or 1");
         x->c.early_split = (int)value;
@@ -372,6 +377,14 @@ int pg_dbg_dump(pg_ctx* x, uint64_t* capacity, uint64_t* keys, uint16_t* values,
     if (!x || !capacity || !size) throw pg::Error(PG_EINVAL, "pg_dbg_dump: bad arguments");
     PG_HIP(hipSetDevice(x->c.device));
     *size = pg::dbg_dump(x->c, *capacity, keys, values, counts);
+  });
+}
+
+int pg_dbg_dump_fd(pg_ctx* x, uint64_t* capacity, int fd, const uint64_t* offsets, uint32_t* crcs, uint64_t* size) {
+  return guard([&] {
+    if (!x || !capacity || !size) throw pg::Error(PG_EINVAL, "pg_dbg_dump_fd: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    *size = pg::dbg_dump_fd(x->c, *capacity, fd, offsets, crcs);
   });
 }
 

@@ -2497,7 +2497,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
     // (no split needed: one S = 0 pass still gathers each bin's 8 regions into one)
     // the early split's partitions, when they are this attempt's only level
     const bool use_pre = pre && attempt == 0 && pre->bb == bb && fp - cb == (int)pre->S && fp > cb &&
-                         fp - cb <= 7 && !spec;
+                         fp - cb <= 7;
     for (int L = cb; L < fp || lv.empty();) {
       const int S = std::min(7, fp - L);
       const uint64_t pin = 1ull << L, nb = 1ull << S;
@@ -2685,8 +2685,9 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   // leaves a smaller work pass behind the last coverage pass: C3 stage A
   // 0.566 / 0.568 / 0.581 ms at 10 / 12 / 8 against 0.586 at 16)
   const uint32_t tailw = c.k3_tail ? (uint32_t)c.k3_tail : 10u;
+  const uint32_t headw = c.k3_head ? (uint32_t)c.k3_head : 16u;
   uint32_t cb[8] = {};
-  for (int i = 1; i <= nch; ++i) cb[i] = cb[i - 1] + (i == nch ? tailw : 16u);
+  for (int i = 1; i <= nch; ++i) cb[i] = cb[i - 1] + (i == nch ? tailw : i == 1 ? headw : 16u);
   const uint32_t cbt = nch ? cb[nch] : 1u;
   uint64_t gc[8] = {}, qoff[8] = {}, qcapc[8] = {}, items = 0;
   for (int i = 0; i < nch; ++i) {
@@ -3146,18 +3147,44 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
     c.dump_ready = false;
     enqueue_stageA(c, cap, 0, rc0, 0, SA_TAIL);
     if (pre_started) early_split();                           // the last chunk's records and the short ones
-    ACount a = stageA_read(c);
-    if (!(a.bits & F_A_OVER)) {
-      c.ms_insert = c.t1.ms();
-      c.ms_clear = 0;
-      c.sentinel = a.sentinel ? 1 : 0;
-      c.n_records_a = a.total;
-      const bool pre_ok = pre_started && !(a.bits_bc & F_SPLIT_OVER);
-      finish_build(c, a, false, pre_ok ? &pre : nullptr);
-      if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
-      if (n) c.w_ratio = (double)c.windows_fw / (double)n;
-      c.tile_sig_len.clear();                                 // (the tile list holds the last batch only)
-      return;
+    if (pre_started) {
+      // stage C queued right behind the last split, with no host round trip
+      // (finish_build's spec form: the table from the early split's plan;
+      // stage A's exact counts and every flag come back with the build's one
+      // readback - a split overflow re-runs B/C from stage A's regions, a
+      // stage A overflow the whole build)
+      ACount a;
+      a.total = (uint64_t)(c.u_ratio * c.w_ratio * (double)n) + 4096;          // the early split's plan
+      a.total = std::max<uint64_t>(a.total, (uint64_t)(c.u_ratio * 1.02 * (double)c.windows_fw) + 4 * R + 64);
+      {
+        int bbp, fpp;                          // (never past the plan's table: its partitions are what is split)
+        table_bits(c, a.total, bbp, fpp);
+        if (bbp != pre.bb) a.total = (uint64_t)(c.u_ratio * c.w_ratio * (double)n) + 4096;
+      }
+      a.maxreg = cap;
+      a.maxbin = 8 * cap;
+      if (finish_build(c, a, true, &pre)) {
+        c.ms_insert = c.t1.ms();
+        c.ms_clear = 0;
+        c.n_records_a = a.total;
+        if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
+        if (n) c.w_ratio = (double)c.windows_fw / (double)n;
+        c.tile_sig_len.clear();
+        return;
+      }
+    } else {
+      ACount a = stageA_read(c);
+      if (!(a.bits & F_A_OVER)) {
+        c.ms_insert = c.t1.ms();
+        c.ms_clear = 0;
+        c.sentinel = a.sentinel ? 1 : 0;
+        c.n_records_a = a.total;
+        finish_build(c, a, false);
+        if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
+        if (n) c.w_ratio = (double)c.windows_fw / (double)n;
+        c.tile_sig_len.clear();                               // (the tile list holds the last batch only)
+        return;
+      }
     }
   }
   c.tile_sig_len.clear();

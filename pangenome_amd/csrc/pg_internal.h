@@ -142,7 +142,8 @@ struct Ctx {
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
   int k3_wblk = 0;                // pg_tune: work blocks per CU, low 4 bits; last chunk's, high 4 bits (0 = 2)
   int k3_emit = 0;                // pg_tune: work pass (0 = two halves per segment, 1 = one)
-  int k3_tail = 0;                // pg_tune: last K3 chunk in 16ths of the others (0 = 16)
+  int k3_tail = 0;                // pg_tune: last K3 chunk in 16ths of the others (0 = 10)
+  int k3_head = 0;                // pg_tune: first K3 chunk in 16ths of the others (0 = 16)
   int k3_cover = 0;               // pg_tune: coverage pass (0 = packed form, 1 = LDS-staged members, 2 = quad form)
   int early_split = 1;            // pg_tune: pg_build_host splits each landed chunk's records (stage B under the upload)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
@@ -252,6 +253,7 @@ struct Ctx {
   std::vector<uint8_t> last_flag; // record flags / extra empties / strands of the last build
   int last_extra = 0;
   DevBuf dump_cnt;                // uint32 occurrence count per (entry, orientation) of the last build
+  std::vector<PinBuf> dump_pin;   // pg_dbg_dump_fd: one pinned piece buffer per writer thread
   bool dump_ready = false;
   uint64_t dump_size = 0, dump_sentinel = 0;
 
@@ -328,6 +330,7 @@ struct PreEnt {                   // one staged oakht slot: oriented key, 12-bit
 };
 void dbg_load(Ctx& c, const uint64_t* keys, const uint16_t* masks, const uint8_t* counts, uint64_t n);
 uint64_t dbg_dump(Ctx& c, uint64_t& capacity, uint64_t* keys, uint16_t* values, uint8_t* counts);
+uint64_t dbg_dump_fd(Ctx& c, uint64_t& capacity, int fd, const uint64_t* off, uint32_t* crc);
 uint64_t oakht_capacity(uint64_t size);
 // pg_walk.hip
 uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1);

@@ -37,6 +37,8 @@
 
 #include <mutex>
 
+#include <memory>
+
 #include "pg_internal.h"
 
 namespace pg {
@@ -584,11 +586,16 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   };
   reserve_records(rcap0);
   bool streaming = on_chunk != nullptr;
+  // (kept to the end: the stager's last work - waiting for the DMAs and
+  // unregistering the chunks' pages, ~50 us on C3 - runs beside the record
+  // table's round trip and the caller's last stage A share instead of before)
+  std::unique_ptr<Upload> upload;
   if (h_src) {
     const uint64_t C = std::max<uint64_t>(WSPAN, c.h2d_chunk / WSPAN * WSPAN);
     // pinned source: DMA up to 8 chunks ahead; pageable (an mmap): through
     // the pinned staging ring (pg_stage.hip)
-    Upload up(c, c.fasta_own.as<uint8_t>(), h_src, n, C);
+    upload.reset(new Upload(c, c.fasta_own.as<uint8_t>(), h_src, n, C));
+    Upload& up = *upload;
     const uint64_t nch = up.chunks();
     for (uint64_t i = 0; i < nch; ++i) {
       up.wait_queued(i);
@@ -620,7 +627,6 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
       c.n_records = Rc;
       (*on_chunk)(Rc);
     }
-    up.finish();
   } else {
     hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
     PG_HIP(hipGetLastError());
@@ -662,6 +668,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   if (tot.nl == 0) {                                        // no line at all (:126-132)
     c.parsed = true;
     if (on_chunk) (*on_chunk)(streaming ? 0 : ~0ull);
+    if (upload) upload->finish();
     return;
   }
   const bool has_tail = (long long)n - 1 > tot.last + 1;
@@ -673,6 +680,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   c.n_bases = nb;
   c.parsed = true;
   if (on_chunk) (*on_chunk)(streaming ? R : ~0ull);          // ~0: the stream broke off
+  if (upload) upload->finish();
 }
 
 }  // namespace pg

@@ -13,7 +13,15 @@
 //       mod capacity, then j, j+1, j+4, j+9, ... .  Any insertion order gives a
 //       layout lookups accept: a key's earlier probes were occupied when it
 //       was placed and nothing is ever removed.
+#include <unistd.h>
+#include <zlib.h>
+
+#include <atomic>
+#include <cerrno>
 #include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
 
 #include "pg_internal.h"
 
@@ -26,6 +34,13 @@ constexpr uint64_t CCHUNK = (uint64_t)PBLK * CW;   // windows per block
 __device__ __forceinline__ void count_at(const TableView& T, unsigned* cnt, uint64_t c, int orient, unsigned add) {
   const uint64_t e = tab_find(T, c);
   if (e != ~0ull) atomicAdd(cnt + 2 * e + orient, add);
+}
+// both orientation counters of c's entry at once (one lookup, one 64-bit
+// atomic: the low word is orientation 0, the high word orientation 1; a
+// counter stays far below 2^32, so no carry crosses into the other)
+__device__ __forceinline__ void count_pair(const TableView& T, unsigned* cnt, uint64_t c, unsigned long long add) {
+  const uint64_t e = tab_find(T, c);
+  if (e != ~0ull) atomicAdd(reinterpret_cast<unsigned long long*>(cnt) + e, add);
 }
 
 // windows [j*CCHUNK, (j+1)*CCHUNK) of record r (n >= k+2): the forward
@@ -57,9 +72,10 @@ k_count_windows(const uint8_t* __restrict__ cls, const unsigned long long* __res
       Kr = (Kr - (uint64_t)digit_rc(dout) * shift) * 5 + digit_rc(din);
     }
     const uint64_t c = K <= Kr ? K : Kr;
-    if (RC && K == Kr) { count_at(T, cnt, c, 0, 2u); continue; }   // palindrome: one key, twice
-    count_at(T, cnt, c, K <= Kr ? 0 : 1, 1u);
-    if (RC) count_at(T, cnt, c, Kr <= K ? 0 : 1, 1u);
+    // with rc a window and its twin add one to each orientation of c (a
+    // palindrome: two to orientation 0); without, its own orientation
+    const unsigned long long one = K <= Kr ? 1ull : 1ull << 32;
+    count_pair(T, cnt, c, RC ? (K == Kr ? 2ull : 1ull | 1ull << 32) : one);
   }
 }
 
@@ -244,45 +260,135 @@ static void dump_counts(Ctx& c) {
   c.dump_ready = true;
 }
 
-uint64_t dbg_dump(Ctx& c, uint64_t& capacity, uint64_t* keys, uint16_t* values, uint8_t* counts) {
+// the oakht slot arrays of capacity M on the device (keys 8 B, values 2 B,
+// counts 1 B per slot), the n<k sentinel included
+struct DumpSlots {
+  DevBuf ok, ov, oc;
+};
+static void dump_place(Ctx& c, uint64_t M, DumpSlots& d) {
+  const uint64_t nw = 2 * c.cap, ntot = nw + c.ovf_cap;
+  DevBuf occ, fail;
+  occ.reserve(4 * M); d.ok.reserve(8 * M); d.ov.reserve(2 * M); d.oc.reserve(M); fail.reserve(4);
+  PG_HIP(hipMemsetAsync(occ.p, 0, 4 * M, c.stream));
+  PG_HIP(hipMemsetAsync(d.ok.p, 0, 8 * M, c.stream));
+  PG_HIP(hipMemsetAsync(d.ov.p, 0, 2 * M, c.stream));
+  PG_HIP(hipMemsetAsync(d.oc.p, 0, M, c.stream));
+  PG_HIP(hipMemsetAsync(fail.p, 0, 4, c.stream));
+  hipLaunchKernelGGL(k_dump_place, dim3(grid_for(ntot, 256, 8192)), dim3(256), 0, c.stream, c.tv, nw, ntot,
+                     c.dump_cnt.as<unsigned>(), M, occ.as<unsigned>(), d.ok.as<unsigned long long>(),
+                     d.ov.as<unsigned short>(), d.oc.as<unsigned char>(), fail.as<unsigned>());
+  PG_HIP(hipGetLastError());
+  unsigned failed = 0;
+  PG_HIP(hipMemcpyAsync(&failed, fail.p, 4, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  occ.release();
+  fail.release();
+  if (failed) throw Error(-34, "pg_dbg_dump: a key found no free slot on its probe sequence");
+  if (c.sentinel) {                                  // key 2^64-1, mask '$' (:1087-1088)
+    const uint64_t j0 = oak_fnv(SENTINEL) % M;
+    uint64_t kk = 0, s = j0;
+    for (; kk < M; ++kk) {                           // (a probe or two at load <= 0.75)
+      s = (j0 + kk * kk) % M;
+      uint8_t taken = 0;
+      PG_HIP(hipMemcpy(&taken, d.oc.as<uint8_t>() + s, 1, hipMemcpyDeviceToHost));
+      if (taken == 0) break;
+    }
+    if (kk == M) throw Error(-34, "pg_dbg_dump: no free slot for the n<k sentinel");
+    const uint64_t key = SENTINEL;
+    const uint16_t val = 32;
+    const uint8_t cnt = (uint8_t)(c.dump_sentinel > 255 ? 255 : (c.dump_sentinel ? c.dump_sentinel : 1));
+    PG_HIP(hipMemcpy(d.ok.as<uint64_t>() + s, &key, 8, hipMemcpyHostToDevice));
+    PG_HIP(hipMemcpy(d.ov.as<uint16_t>() + s, &val, 2, hipMemcpyHostToDevice));
+    PG_HIP(hipMemcpy(d.oc.as<uint8_t>() + s, &cnt, 1, hipMemcpyHostToDevice));
+  }
+}
+
+static uint64_t dump_capacity(Ctx& c, uint64_t& capacity) {
   if (!c.built) throw Error(-22, "pg_dbg_dump: no dBG (call pg_build_dbg first)");
   if (!c.dump_ready) dump_counts(c);
   const uint64_t M = capacity ? capacity : oakht_capacity(c.dump_size);
   if (M < c.dump_size) throw Error(-34, "pg_dbg_dump: capacity below the key count");
   capacity = M;
+  return M;
+}
+
+uint64_t dbg_dump(Ctx& c, uint64_t& capacity, uint64_t* keys, uint16_t* values, uint8_t* counts) {
+  const uint64_t M = dump_capacity(c, capacity);
   if (!keys) return c.dump_size;
   if (!values || !counts) throw Error(-22, "pg_dbg_dump: values and counts are required with keys");
-  const uint64_t nw = 2 * c.cap, ntot = nw + c.ovf_cap;
-  DevBuf occ, ok, ov, oc, fail;
-  occ.reserve(4 * M); ok.reserve(8 * M); ov.reserve(2 * M); oc.reserve(M); fail.reserve(4);
-  PG_HIP(hipMemsetAsync(occ.p, 0, 4 * M, c.stream));
-  PG_HIP(hipMemsetAsync(ok.p, 0, 8 * M, c.stream));
-  PG_HIP(hipMemsetAsync(ov.p, 0, 2 * M, c.stream));
-  PG_HIP(hipMemsetAsync(oc.p, 0, M, c.stream));
-  PG_HIP(hipMemsetAsync(fail.p, 0, 4, c.stream));
-  hipLaunchKernelGGL(k_dump_place, dim3(grid_for(ntot, 256, 8192)), dim3(256), 0, c.stream, c.tv, nw, ntot,
-                     c.dump_cnt.as<unsigned>(), M, occ.as<unsigned>(), ok.as<unsigned long long>(),
-                     ov.as<unsigned short>(), oc.as<unsigned char>(), fail.as<unsigned>());
-  PG_HIP(hipGetLastError());
-  unsigned failed = 0;
-  PG_HIP(hipMemcpyAsync(&failed, fail.p, 4, hipMemcpyDeviceToHost, c.stream));
-  PG_HIP(hipMemcpyAsync(keys, ok.p, 8 * M, hipMemcpyDeviceToHost, c.stream));
-  PG_HIP(hipMemcpyAsync(values, ov.p, 2 * M, hipMemcpyDeviceToHost, c.stream));
-  PG_HIP(hipMemcpyAsync(counts, oc.p, M, hipMemcpyDeviceToHost, c.stream));
+  DumpSlots d;
+  dump_place(c, M, d);
+  PG_HIP(hipMemcpyAsync(keys, d.ok.p, 8 * M, hipMemcpyDeviceToHost, c.stream));
+  PG_HIP(hipMemcpyAsync(values, d.ov.p, 2 * M, hipMemcpyDeviceToHost, c.stream));
+  PG_HIP(hipMemcpyAsync(counts, d.oc.p, M, hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  occ.release(); ok.release(); ov.release(); oc.release(); fail.release();
-  if (failed) throw Error(-34, "pg_dbg_dump: a key found no free slot on its probe sequence");
-  if (c.sentinel) {                                  // key 2^64-1, mask '$' (:1087-1088)
-    const uint64_t j0 = oak_fnv(SENTINEL) % M;
-    uint64_t kk = 0, s = j0;
-    for (; kk < M; ++kk) {
-      s = (j0 + kk * kk) % M;
-      if (counts[s] == 0) break;
+  return c.dump_size;
+}
+
+// dump() straight into a file: the slot arrays go from the device to `fd` at
+// off[0..2] (keys, values, counts) in DUMP_PIECE pieces, each piece through a
+// worker thread's own pinned buffer and stream (copy, CRC-32, pwrite), so the
+// copies, the CRCs and the page-cache writes of different pieces overlap and
+// no host array of the whole table is ever allocated (C3: 886 MB; C4: ~5 GB).
+constexpr uint64_t DUMP_PIECE = 16ull << 20;
+uint64_t dbg_dump_fd(Ctx& c, uint64_t& capacity, int fd, const uint64_t* off, uint32_t* crc) {
+  const uint64_t M = dump_capacity(c, capacity);
+  if (fd < 0) return c.dump_size;
+  if (!off || !crc) throw Error(-22, "pg_dbg_dump_fd: offsets and crcs are required with a descriptor");
+  DumpSlots d;
+  dump_place(c, M, d);
+  const uint8_t* src[3] = {d.ok.as<uint8_t>(), d.ov.as<uint8_t>(), d.oc.as<uint8_t>()};
+  const uint64_t len[3] = {8 * M, 2 * M, M};
+  struct Piece { int m; uint64_t at, n; };
+  std::vector<Piece> jobs;
+  for (int m = 0; m < 3; ++m)
+    for (uint64_t a = 0; a < len[m]; a += DUMP_PIECE) jobs.push_back(Piece{m, a, std::min(DUMP_PIECE, len[m] - a)});
+  std::vector<uint32_t> pc(jobs.size(), 0u);
+  std::atomic<size_t> next{0};
+  std::atomic<bool> bad{false};
+  std::mutex em;
+  std::string err;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const size_t nt = std::min<size_t>(std::min<size_t>(16, hw), jobs.size());
+  if (c.dump_pin.size() < nt) c.dump_pin.resize(nt);
+  for (size_t t = 0; t < nt; ++t) c.dump_pin[t].reserve(DUMP_PIECE);
+  auto worker = [&](size_t t) {
+    hipStream_t st = nullptr;
+    try {
+      PG_HIP(hipSetDevice(c.device));
+      PG_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      uint8_t* buf = c.dump_pin[t].as<uint8_t>();
+      for (size_t j; !bad && (j = next++) < jobs.size();) {
+        const Piece& p = jobs[j];
+        PG_HIP(hipMemcpyAsync(buf, src[p.m] + p.at, p.n, hipMemcpyDeviceToHost, st));
+        PG_HIP(hipStreamSynchronize(st));
+        pc[j] = (uint32_t)crc32(0ul, buf, (uInt)p.n);
+        for (uint64_t w = 0; w < p.n;) {
+          const ssize_t r = pwrite(fd, buf + w, p.n - w, (off_t)(off[p.m] + p.at + w));
+          if (r < 0) {
+            if (errno == EINTR) continue;
+            throw Error(-5, std::string("pg_dbg_dump_fd: write failed: ") + std::strerror(errno));
+          }
+          w += (uint64_t)r;
+        }
+      }
+    } catch (const std::exception& e) {
+      std::lock_guard<std::mutex> g(em);
+      if (!bad.exchange(true)) err = e.what();
     }
-    if (kk == M) throw Error(-34, "pg_dbg_dump: no free slot for the n<k sentinel");
-    keys[s] = SENTINEL;
-    values[s] = 32;
-    counts[s] = (uint8_t)(c.dump_sentinel > 255 ? 255 : (c.dump_sentinel ? c.dump_sentinel : 1));
+    if (st) (void)hipStreamDestroy(st);
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(worker, t);
+  worker(0);
+  for (auto& x : th) x.join();
+  if (bad) throw Error(-5, err);
+  for (int m = 0; m < 3; ++m) crc[m] = 0u;
+  std::vector<bool> first(3, true);
+  for (size_t j = 0; j < jobs.size(); ++j) {          // pieces are in member order, ascending
+    const int m = jobs[j].m;
+    crc[m] = first[m] ? pc[j] : (uint32_t)crc32_combine(crc[m], pc[j], (z_off_t)jobs[j].n);
+    first[m] = false;
   }
   return c.dump_size;
 }

@@ -331,7 +331,16 @@ def _crc32_combine():
     return f
 
 
-def savez_stored(fn: str, **arrays) -> None:
+class Deferred:
+    """A savez_stored member whose data a native writer puts into the file:
+    `n` elements of `dtype` (a 1-D array)."""
+
+    def __init__(self, dtype, n: int):
+        self.dtype = np.dtype(dtype)
+        self.n = int(n)
+
+
+def savez_stored(fn: str, fill=None, **arrays) -> None:
     """np.savez(fn, **arrays) (a zip of stored .npy members, what np.load and
     the reference's load_on_disk read, :289-335), written in parallel: every
     member's bytes go to the file in NPZ_PIECE pieces by a thread pool
@@ -339,7 +348,9 @@ def savez_stored(fn: str, **arrays) -> None:
     (zlib.crc32, GIL released; pieces joined with crc32_combine); then the
     local headers, the central directory and the ZIP64 end records.  The
     single-threaded zipfile CRC and write of np.savez took 0.67 s for C3's
-    dump (0.45 s of it CRC)."""
+    dump (0.45 s of it CRC).  A `Deferred` member's data is written by
+    `fill(fd, offsets)` (its data offsets in member order), which returns
+    their CRC-32s."""
     import struct
     import zlib
     from concurrent.futures import ThreadPoolExecutor
@@ -348,22 +359,29 @@ def savez_stored(fn: str, **arrays) -> None:
     members = []
     off = 0
     for name, arr in arrays.items():
-        a = np.ascontiguousarray(arr)
+        if isinstance(arr, Deferred):
+            hd = {"descr": np.lib.format.dtype_to_descr(arr.dtype), "fortran_order": False, "shape": (arr.n,)}
+            body, blen = None, arr.n * arr.dtype.itemsize
+        else:
+            a = np.ascontiguousarray(arr)
+            hd = np.lib.format.header_data_from_array_1_0(a)
+            body = a.reshape(-1).view(np.uint8) if a.size else np.zeros(0, np.uint8)
+            blen = body.shape[0]
         hb = io.BytesIO()
-        np.lib.format.write_array_header_1_0(hb, np.lib.format.header_data_from_array_1_0(a))
+        np.lib.format.write_array_header_1_0(hb, hd)
         head = hb.getvalue()
-        body = a.reshape(-1).view(np.uint8) if a.size else np.zeros(0, np.uint8)
         zname = (name + ".npy").encode()
         lh = 30 + len(zname) + 20                       # local header + ZIP64 extra (sizes)
-        members.append([zname, head, body, off, lh])
-        off += lh + len(head) + body.shape[0]
+        members.append([zname, head, body, off, lh, blen])
+        off += lh + len(head) + blen
     fd = os.open(fn, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
     try:
         tasks = []
-        for mi, (zname, head, body, moff, lh) in enumerate(members):
+        for mi, (zname, head, body, moff, lh, blen) in enumerate(members):
             d0 = moff + lh + len(head)
-            for p in range(0, body.shape[0], NPZ_PIECE):
-                tasks.append((mi, p, body[p:p + NPZ_PIECE], d0 + p))
+            if body is not None:
+                for p in range(0, blen, NPZ_PIECE):
+                    tasks.append((mi, p, body[p:p + NPZ_PIECE], d0 + p))
 
         def work(t):
             mi, p, piece, at = t
@@ -377,14 +395,19 @@ def savez_stored(fn: str, **arrays) -> None:
             with ThreadPoolExecutor(max_workers=min(16, len(tasks), os.cpu_count() or 4)) as ex:
                 for mi, p, c, n in ex.map(work, tasks):
                     crcs[(mi, p)] = (c, n)
+        deferred = [mi for mi, m in enumerate(members) if m[2] is None]
+        if deferred:
+            got = fill(fd, [members[mi][3] + members[mi][4] + len(members[mi][1]) for mi in deferred])
+            for mi, c in zip(deferred, got):
+                crcs[(mi, 0)] = (int(c), members[mi][5])
         cdir = bytearray()
         dt = (0 << 11) | (0 << 5), (1 << 5) | 1        # 00:00:00, 1980-01-01
-        for mi, (zname, head, body, moff, lh) in enumerate(members):
+        for mi, (zname, head, body, moff, lh, blen) in enumerate(members):
             crc = zlib.crc32(head)
-            for p in range(0, body.shape[0], NPZ_PIECE):
+            for p in (range(0, blen, NPZ_PIECE) if body is not None else [0] if blen else []):
                 c, n = crcs[(mi, p)]
                 crc = comb(crc, c, n)
-            size = len(head) + body.shape[0]
+            size = len(head) + blen
             local = struct.pack("<IHHHHHIIIHH", 0x04034B50, 45, 0, 0, dt[0], dt[1], crc, 0xFFFFFFFF, 0xFFFFFFFF,
                                 len(zname), 20) + zname + struct.pack("<HHQQ", 1, 16, size, size) + head
             done = 0
@@ -414,6 +437,15 @@ def write_db_npz(fn: str, capacity: int, size: int, keys, values, counts, offset
     # np.load / the reference's load_on_disk, ~1.4x the bytes, but deflate ran
     # at ~30 MB/s on the slot arrays (C3: 26 s of a 42 s CLI run)
     savez_stored(fn, parameters=params, keys=keys, values=values, counts=counts)
+
+
+def write_db_npz_from(fn: str, capacity: int, size: int, fill, offset: int = 0):
+    """write_db_npz with the slot arrays written by `fill(fd, offsets)` (the
+    device's pg_dbg_dump_fd): the same file, no host copy of the arrays."""
+    fn = fn[:-4] if fn.endswith(".npz") else fn
+    params = np.asarray([capacity, DB_LOAD, size, 1, 1, offset], dtype=np.uint64)
+    savez_stored(fn, fill, parameters=params, keys=Deferred(np.uint64, capacity),
+                 values=Deferred(np.uint16, capacity), counts=Deferred(np.uint8, capacity))
 
 
 def read_db_npz(fn: str):

@@ -220,8 +220,8 @@ class _Background:
 
 def dump(g: DeviceGraph, fn="./tmp"):
     """:243-261 — `fn`.npz as an oakht the reference's load_on_disk accepts."""
-    cap, size, keys, values, counts = g.ctx.dbg_dump()
-    host.write_db_npz(fn, cap, size, keys, values, counts)
+    cap, size = g.ctx.dbg_dump_size()
+    host.write_db_npz_from(fn, cap, size, lambda fd, offs: g.ctx.dbg_dump_fd(fd, offs, cap))
     return 0
 
 

@@ -59,6 +59,23 @@ def test_dump_matches_reference_dump(name, tmp_path):
     assert off == 0 and k2.shape[0] == int(params[2])
 
 
+@pytest.mark.parametrize("name", _graph_fixtures())
+def test_native_dump_file_equals_host_write(name, tmp_path):
+    """pg_dbg_dump_fd (slot arrays streamed from the device into the file,
+    kmer.dump) writes the same bytes as pg_dbg_dump + host.write_db_npz,
+    the n<k sentinel's slot included."""
+    from pangenome_amd import host, kmer
+    fx = Fixture(name)
+    q = tmp_path / "input.fsa"
+    q.write_bytes(fx.fasta)
+    Ns = fx.ns if fx.ns is not None else 2 ** 63
+    g = kmer.seq2rdbg(str(q), fx.k, 5, Ns, brkpt="", chunk=2 ** 33, rc=(fx.c >> 1) == 1)
+    kmer.dump(g, str(tmp_path / "a_db"))
+    cap, size, keys, vals, cnts = g.ctx.dbg_dump()
+    host.write_db_npz(str(tmp_path / "b_db"), cap, size, keys, vals, cnts)
+    assert (tmp_path / "a_db.npz").read_bytes() == (tmp_path / "b_db.npz").read_bytes()
+
+
 def _run_cli(argv):
     from pangenome_amd import kmer
     out = io.StringIO()

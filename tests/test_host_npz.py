@@ -27,6 +27,32 @@ def test_savez_stored_roundtrip(tmp_path, piece, monkeypatch):
             assert z[k].dtype == v.dtype and z[k].shape == v.shape and np.array_equal(z[k], v), k
 
 
+def test_savez_stored_deferred_members_match_savez(tmp_path):
+    """Members written by a fill callback (what pg_dbg_dump_fd does from the
+    device) give the same file as the arrays themselves: same bytes."""
+    import os
+    import zlib
+    from pangenome_amd import host
+    rng = np.random.default_rng(5)
+    keys = rng.integers(0, 2 ** 63, size=70_001, dtype=np.uint64)
+    vals = rng.integers(0, 4096, size=70_001).astype(np.uint16)
+    cnts = rng.integers(0, 256, size=70_001).astype(np.uint8)
+    host.write_db_npz(str(tmp_path / "a_db"), 70_001, 123, keys, vals, cnts, offset=9)
+
+    def fill(fd, offs):
+        out = []
+        for a, o in zip((keys, vals, cnts), offs):
+            b = a.view(np.uint8).tobytes()
+            assert os.pwrite(fd, b, o) == len(b)
+            out.append(zlib.crc32(b))
+        return out
+    host.write_db_npz_from(str(tmp_path / "b_db"), 70_001, 123, fill, offset=9)
+    a = open(tmp_path / "a_db.npz", "rb").read()
+    b = open(tmp_path / "b_db.npz", "rb").read()
+    assert a == b
+    assert zipfile.ZipFile(str(tmp_path / "b_db.npz")).testzip() is None
+
+
 def test_write_db_npz_reads_back(tmp_path):
     from pangenome_amd import host
     keys = np.array([0, 11, 0, 42], np.uint64)

@@ -35,6 +35,7 @@ for step in "$@"; do
     abcover) run ab_cover 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=2 ;;
     abhost) run ab_host 600 python -u tools/ab_k3.py --host --steps 12 --tune base --tune EARLY_SPLIT=0 --tune K3_COVER=2 --tune EARLY_SPLIT=0,K3_COVER=2 ;;
     abchunks) run ab_chunks 900 python -u tools/ab_k3.py --steps 10 --tune base --tune K3_HEAD=8 --tune K3_HEAD=8,K3_TAIL=6 --tune K3_CHUNKS=4,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=4 --tune K3_CHUNKS=5,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=2 ;;
+    npz) run pytest_npz 600 python -u -m pytest tests/test_gpu_npz.py -x -v --timeout 300 --timeout-method thread ;;
     savebd) run save_bd 300 python -u tools/save_breakdown.py ;;
     tracewin) run trace_win 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tw -o run --output-format csv -- python tools/ab_k3.py --host --steps 3 --tune base ;;
     abdev) run ab_dev 600 python -u tools/ab_k3.py --steps 12 --tune base --tune EARLY_SPLIT=0 --tune K3_COVER=2 ;;

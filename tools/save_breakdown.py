@@ -32,10 +32,16 @@ def main():
         t0 = time.perf_counter()
         cap, size, keys, values, counts = g.ctx.dbg_dump()
         t1 = time.perf_counter()
-        host.write_db_npz(os.path.join(d, "db"), cap, size, keys, values, counts)
+        host.write_db_npz(os.path.join(d, "db%d" % rep), cap, size, keys, values, counts)
         t2 = time.perf_counter()
         res.setdefault("dump_ms", []).append(round(1e3 * (t1 - t0), 1))
         res.setdefault("write_ms", []).append(round(1e3 * (t2 - t1), 1))
+    for rep in range(3):
+        fn = os.path.join(d, "nat%d_db" % rep)
+        t0 = time.perf_counter()
+        kmer.dump(g, fn)
+        res.setdefault("native_dump_ms", []).append(round(1e3 * (time.perf_counter() - t0), 1))
+        os.unlink(fn + ".npz")
     nbytes = keys.nbytes + values.nbytes + counts.nbytes
     pieces = [a.reshape(-1).view(np.uint8)[p:p + host.NPZ_PIECE] for a in (keys, values, counts)
               for p in range(0, a.nbytes, host.NPZ_PIECE)]

@@ -21,12 +21,12 @@ for r in kt:
     ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "K", re.sub(r"\(.*", "", r["Kernel_Name"])[-44:],
                r.get("Queue_Id", "")))
 for r in mt:
-    kind = r.get("Direction") or r.get("Operation") or "COPY"
-    n = int(r.get("Bytes", 0) or 0) if "Bytes" in r else 0
-    ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C", "%s %d MB" % (kind, n >> 20), ""))
+    kind = (r.get("Direction") or r.get("Operation") or "COPY").replace("MEMORY_COPY_", "")
+    ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), "C", kind, ""))
 ev.sort()
-# the last window: from the last k_span_sum that follows a large H2D copy
-h2d = [e for e in ev if e[2] == "C" and "HOST_TO_DEVICE" in e[3].upper() and int(e[3].split()[-2]) >= 16]
+# the chunk uploads: H2D copies of more than 200 us (no byte counts in the
+# trace; a 64 MiB chunk takes ~1.2 ms, record tables and flags a few us)
+h2d = [e for e in ev if e[2] == "C" and "HOST_TO_DEVICE" in e[3] and e[1] - e[0] > 200_000]
 if not h2d:
     sys.exit("no H2D chunk copies in the trace (run with --memory-copy-trace)")
 # windows start where consecutive big copies are separated by > 1 ms
