@@ -253,6 +253,10 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 /* PG_TUNE_K3_HEAD: size of the first K3 chunk in 16ths of the middle ones
  * (1..64, 0 = 16: the coverage pass that runs before any work pass). */
 #define PG_TUNE_K3_HEAD 15
+/* PG_TUNE_H2D_TAIL: bytes of pg_build_host's last H2D chunk (default 8 MiB;
+ * 0 = every chunk PG_TUNE_H2D_CHUNK bytes): what runs after the last byte has
+ * landed starts from that chunk. */
+#define PG_TUNE_H2D_TAIL 16
 /* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
  * count asks (0..8): exercises the overflow set, its spill and the re-run
  * with more buckets (results are unchanged). */

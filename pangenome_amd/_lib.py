@@ -30,6 +30,7 @@ PG_TUNE_K3_EMIT = 12
 PG_TUNE_K3_TAIL = 13
 PG_TUNE_EARLY_SPLIT = 14
 PG_TUNE_K3_HEAD = 15
+PG_TUNE_H2D_TAIL = 16
 
 
 class PgStats(C.Structure):

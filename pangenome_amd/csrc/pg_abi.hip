@@ -293,6 +293,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || value > 64) throw pg::Error(PG_EINVAL, "pg_tune: K3 head must be in [0, 64]");
         x->c.k3_head = (int)value;
         break;
+      case PG_TUNE_H2D_TAIL:
+        if (value < 0) throw pg::Error(PG_EINVAL, "pg_tune: H2D tail must be >= 0");
+        x->c.h2d_tail = (uint64_t)value;
+        break;
       case PG_TUNE_EARLY_SPLIT:
         if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: early split must be 0 or 1");
         x->c.early_split = (int)value;

@@ -1344,14 +1344,35 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
         int iw = (U >> 4) + 4 * l;
         if (iw < 0 || iw + 12 > RDW) iw &= 3;      // (an invalid lane: in-bounds words, same alignment)
         if (!PG_BOK(iw >= 0 && iw + 12 <= RDW, 14, iw, U)) iw = 0;
-        uint32_t Rw[8];
-        lds_words8(s_ref[ri], iw, Rw);
+        // the reference words iw .. iw + 7 out of three aligned 16-byte reads;
+        // iw & 3 is the same on every lane, and the compare runs inside the
+        // uniform branch that knows it, so the words are used where they were
+        // loaded (selecting them first cost 32 register moves per drift)
+        uint32_t raw[12];
+        {
+          const uint4* r16 = reinterpret_cast<const uint4*>(s_ref[ri]);
+#pragma unroll
+          for (int q = 0; q < 3; ++q) {
+            uint4 v = r16[(iw >> 2) + q];
+            asm volatile("" : "+v"(v.x), "+v"(v.y), "+v"(v.z), "+v"(v.w));
+            raw[4 * q] = v.x; raw[4 * q + 1] = v.y; raw[4 * q + 2] = v.z; raw[4 * q + 3] = v.w;
+          }
+        }
         const uint32_t bs = 2u * (uint32_t)(U & 15);
         uint32_t Z[LW];
+        auto zrun = [&](auto W) {
+          constexpr int w = decltype(W)::value;
 #pragma unroll
-        for (int i = 0; i < LW; ++i) {
-          const uint32_t x = M[i] ^ __builtin_amdgcn_alignbit(Rw[i + 1], Rw[i], bs);
-          Z[i] = (x | (x >> 1)) & 0x55555555u;     // even bit of each base: mismatch
+          for (int i = 0; i < LW; ++i) {
+            const uint32_t x = M[i] ^ __builtin_amdgcn_alignbit(raw[w + i + 1], raw[w + i], bs);
+            Z[i] = (x | (x >> 1)) & 0x55555555u;   // even bit of each base: mismatch
+          }
+        };
+        switch (__builtin_amdgcn_readfirstlane(iw & 3)) {
+          case 0: zrun(std::integral_constant<int, 0>{}); break;
+          case 1: zrun(std::integral_constant<int, 1>{}); break;
+          case 2: zrun(std::integral_constant<int, 2>{}); break;
+          default: zrun(std::integral_constant<int, 3>{}); break;
         }
         uint32_t T[LW - 1];                         // from the lane's first context base (sh bases in)
 #pragma unroll
@@ -1763,7 +1784,11 @@ __device__ __forceinline__ uint64_t part_at(const Recs& I, uint32_t p, const uns
 // with one global atomic, sorts them by bin in LDS and writes the runs
 // coalesced.  3 blocks (24 waves) per CU.
 constexpr int SB = 512, SR = 8, SCH = SB * SR;
-constexpr int SMAXB = 128;                    // <= 7 bits per pass
+// (experiment bit 20: 2048-bucket stage C partitions, 3 blocks per CU, behind
+// 8-bit split passes)
+constexpr bool EXP_R11 = (PG_EXP_BITS & (1 << 20)) != 0;
+constexpr int SPLIT_BITS = EXP_R11 ? 8 : 7;   // bits per split pass
+constexpr int SMAXB = 1 << SPLIT_BITS;
 // start (NULL: 0): per input region, the records below it are already split
 // (pg_build_host's early split); a block loops over its region's records in
 // steps of bpr * SCH.
@@ -1799,18 +1824,27 @@ k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t s
       rk[e] = i < cnt ? atomicAdd(&s_cnt[(uint32_t)(key[e] >> shift) & (nb - 1)], 1u) : 0u;
     }
     __syncthreads();
-    if (threadIdx.x < 64) {                   // exclusive scan of the bin counts, two bins per lane
+    if (threadIdx.x < 64) {                   // exclusive scan of the bin counts, SMAXB / 64 bins per lane
+      constexpr int BPL = SMAXB / 64;
       const uint32_t l = threadIdx.x;
-      const uint32_t a = 2 * l < nb ? s_cnt[2 * l] : 0u, b = 2 * l + 1 < nb ? s_cnt[2 * l + 1] : 0u;
-      uint32_t x = a + b;
+      uint32_t v[BPL], x = 0;
+#pragma unroll
+      for (int q = 0; q < BPL; ++q) {
+        v[q] = BPL * l + q < nb ? s_cnt[BPL * l + q] : 0u;
+        x += v[q];
+      }
+      const uint32_t own = x;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, 64);
         if ((int)l >= o) x += y;
       }
-      const uint32_t ex = x - a - b;
-      if (2 * l < nb) s_pos[2 * l] = ex;
-      if (2 * l + 1 < nb) s_pos[2 * l + 1] = ex + a;
+      uint32_t ex = x - own;
+#pragma unroll
+      for (int q = 0; q < BPL; ++q) {
+        if (BPL * l + q < nb) s_pos[BPL * l + q] = ex;
+        ex += v[q];
+      }
     }
     if (threadIdx.x < nb) {
       const uint32_t c = s_cnt[threadIdx.x];
@@ -1865,8 +1899,9 @@ __global__ void k_snap(const unsigned long long* __restrict__ cursor, unsigned l
 // rdBG members to its own output segment (no global atomics at all) and
 // leaves its key / dBG / member counts in its own counter slot.
 constexpr int RB_T = 512;                     // 2 blocks (16 waves) per CU: 70 KiB of LDS each
-constexpr int RB_R = 8;                       // records per thread and partition held in registers
-constexpr int RANGE_BITS = 12;                // <= 4096 buckets (64 KiB of LDS) per partition
+constexpr int RB_R = EXP_R11 ? 4 : 8;         // records per thread and partition held in registers
+constexpr int RANGE_BITS = EXP_R11 ? 11 : 12; // <= 4096 buckets (64 KiB of LDS) per partition
+constexpr int RB_PER_CU = EXP_R11 ? 3 : 2;    // persistent range blocks per CU
 constexpr int OVL = 512;                      // LDS overflow slots per partition
 constexpr int RB_CTR = 4;                     // per-block counters: keys, dBG entries, members
 constexpr uint32_t MQ = 64;                   // queued rdBG members per wave
@@ -2497,9 +2532,9 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
     // (no split needed: one S = 0 pass still gathers each bin's 8 regions into one)
     // the early split's partitions, when they are this attempt's only level
     const bool use_pre = pre && attempt == 0 && pre->bb == bb && fp - cb == (int)pre->S && fp > cb &&
-                         fp - cb <= 7;
+                         fp - cb <= SPLIT_BITS;
     for (int L = cb; L < fp || lv.empty();) {
-      const int S = std::min(7, fp - L);
+      const int S = std::min(SPLIT_BITS, fp - L);
       const uint64_t pin = 1ull << L, nb = 1ull << S;
       uint64_t capo = (uint64_t)((double)maxin / (double)nb * capx) + 64;
       if (lv_exact_bb == bb && lv.size() < lv_exact.size())
@@ -2519,7 +2554,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
     }
     c.ctrS.reserve(8 * std::max<uint64_t>(ctr_words, 1));
     const uint64_t nparts = 1ull << fp;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(nparts, 2ull * (uint64_t)c.n_cu);   // persistent: 2 per CU
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nparts, (uint64_t)RB_PER_CU * (uint64_t)c.n_cu);   // persistent
     const uint64_t rcap = (uint64_t)(rseg_frac * (double)a.total / grid) + 4096;
     c.rseg.reserve(8 * grid * rcap);
     c.rseg_cap = rcap;
@@ -2665,7 +2700,9 @@ static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, const B
 // part: 0 = a whole stage A; pg_build_host's parts: SA_FIRST starts it (the
 // regions reset, no short records yet), SA_MORE adds tiles, SA_TAIL adds the
 // short records, the n<k flag and the staged slots (no tiles).
-enum { SA_WHOLE = 0, SA_FIRST = 1, SA_MORE = 2, SA_TAIL = 3 };
+// SA_FIRST_TAIL / SA_MORE_TAIL: SA_FIRST / SA_MORE and SA_TAIL in one call
+// (the last batch of records, once the record table is final).
+enum { SA_WHOLE = 0, SA_FIRST = 1, SA_MORE = 2, SA_TAIL = 3, SA_FIRST_TAIL = 4, SA_MORE_TAIL = 5 };
 // join = false: the side stream is joined (and t1 stopped) by finish_build,
 // behind the stage B/C fills it queues on the side stream.
 static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int extra_empty, int part = SA_WHOLE,
@@ -2673,7 +2710,9 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   const uint64_t shift = pow5(c.k - 1);
   hipStream_t s0 = c.stream, s1 = c.stream2;
   FillList fl;
-  const BinOut O = stageA_begin(c, cap, fl, part == SA_WHOLE || part == SA_FIRST);
+  const bool begin = part == SA_WHOLE || part == SA_FIRST || part == SA_FIRST_TAIL;
+  const bool tail = part == SA_WHOLE || part == SA_TAIL || part == SA_FIRST_TAIL || part == SA_MORE_TAIL;
+  const BinOut O = stageA_begin(c, cap, fl, begin);
   if (part == SA_TAIL) ntiles = 0;
   const uint8_t* cls = c.cls.as<uint8_t>();
   const dim3 b(IBLOCK);
@@ -2751,7 +2790,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     hipStream_t ws = s1;
     if (nch > 1 && i + 1 == nch) {
       ws = s0;
-      if (part == SA_WHOLE) {
+      if (tail) {
         launch_short(c, s1, rc0, shift, O);                    // k_short beside the last work pass
         short_done = true;
       }
@@ -2767,7 +2806,6 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     hipLaunchKernelGGL(kw, dim3(gw), b, 0, ws, cls, qi, qni, (unsigned long long)qcapc[i], c.k, shift, c.tv, O);
     PG_HIP(hipGetLastError());
   }
-  const bool tail = part == SA_WHOLE || part == SA_TAIL;
   if (!short_done && tail) launch_short(c, s0, rc0, shift, O);
   if (extra_empty && tail) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, s0, c.flags.as<unsigned>());
   if (c.n_preload && tail) {
@@ -3069,7 +3107,7 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
     const uint64_t est = (uint64_t)(c.u_ratio * c.w_ratio * (double)n) + 4096;
     int bb, fp;
     table_bits(c, est, bb, fp);
-    if (fp > c.cbits && fp - c.cbits <= 7) {
+    if (fp > c.cbits && fp - c.cbits <= SPLIT_BITS) {
       pre.bb = bb;
       pre.S = (uint32_t)(fp - c.cbits);
       const uint64_t maxbin = est / NBIN + est / (NBIN * 8) + 1024;      // bins are even: h is a bijective hash
@@ -3102,6 +3140,23 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
                        c.snapA.as<unsigned long long>(), (uint32_t)NREG);
     PG_HIP(hipGetLastError());
   };
+  // the record table is final: every record flagged for the short-record pass
+  auto final_records = [&]() {
+    const uint64_t R = c.n_records;
+    if (R) PG_HIP(hipMemsetAsync(c.rec_flag.p, 1, R, c.stream));
+    c.dev_flag.assign(R, 1);
+    c.dev_flag_p = c.rec_flag.p;
+    c.windows_fw = 0;
+    for (uint64_t r = 0; r < R; ++r) {
+      const int64_t m = c.h_rec_len[r];
+      c.windows_fw += m > c.k ? (uint64_t)(m - c.k + 1) : 1;
+    }
+    c.windows_total = c.windows_fw * (rc0 ? 2 : 1);
+    c.last_flag.assign(R, 1);
+    c.last_extra = 0;
+    c.dump_ready = false;
+  };
+  bool tail_done = false;
   std::function<void(uint64_t)> on_chunk = [&](uint64_t rc) {
     if (broken) return;
     if (rc == ~0ull) { broken = true; return; }               // the parse could not stream
@@ -3112,17 +3167,23 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
       flag[r] = 1;
       nlong += c.h_rec_len[r] >= c.k + 2;
     }
-    const bool final_call = c.parsed;
+    // the last batch (the record table final: every record counted) also
+    // takes the short records - one stage A call and one split fewer after
+    // the last chunk
+    const bool final_call = c.parsed && rc == c.n_records;
+    if (final_call) final_records();
     if (!started) {
       if (nlong < 3 && !final_call) return;                   // wait for three long records
       const uint64_t nt = make_tiles(c, flag);
-      enqueue_stageA(c, cap, nt, rc0, 0, SA_FIRST);
+      enqueue_stageA(c, cap, nt, rc0, 0, final_call ? SA_FIRST_TAIL : SA_FIRST);
       started = true;
+      tail_done = final_call;
       early_split();
     } else {
       const uint64_t nt = make_tiles(c, flag, true);
-      if (nt) {
-        enqueue_stageA(c, cap, nt, rc0, 0, SA_MORE);
+      if (nt || final_call) {
+        enqueue_stageA(c, cap, nt, rc0, 0, final_call ? SA_MORE_TAIL : SA_MORE);
+        tail_done = final_call;
         early_split();
       }
     }
@@ -3133,20 +3194,11 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
   std::vector<uint8_t> all(R, 1);
   if (!broken && (done != R || !started)) broken = true;
   if (!broken) {
-    if (R) PG_HIP(hipMemsetAsync(c.rec_flag.p, 1, R, c.stream));
-    c.dev_flag.assign(R, 1);
-    c.dev_flag_p = c.rec_flag.p;
-    c.windows_fw = 0;
-    for (uint64_t r = 0; r < R; ++r) {
-      const int64_t m = c.h_rec_len[r];
-      c.windows_fw += m > c.k ? (uint64_t)(m - c.k + 1) : 1;
+    if (!tail_done) {
+      final_records();
+      enqueue_stageA(c, cap, 0, rc0, 0, SA_TAIL);
+      if (pre_started) early_split();                         // the short records
     }
-    c.windows_total = c.windows_fw * (rc0 ? 2 : 1);
-    c.last_flag = all;
-    c.last_extra = 0;
-    c.dump_ready = false;
-    enqueue_stageA(c, cap, 0, rc0, 0, SA_TAIL);
-    if (pre_started) early_split();                           // the last chunk's records and the short ones
     if (pre_started) {
       // stage C queued right behind the last split, with no host round trip
       // (finish_build's spec form: the table from the early split's plan;

@@ -147,6 +147,7 @@ struct Ctx {
   int k3_cover = 0;               // pg_tune: coverage pass (0 = packed form, 1 = LDS-staged members, 2 = quad form)
   int early_split = 1;            // pg_tune: pg_build_host splits each landed chunk's records (stage B under the upload)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
+  uint64_t h2d_tail = 8ull << 20;     // pg_tune: bytes of pg_build_host's last H2D chunk (0: uniform chunks)
   int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
   uint64_t stage_piece = 32ull << 20;  // pg_tune: bytes per staging-ring slot (one DMA)
   uint64_t stage_slots = 4;       // pg_tune: staging-ring slots (2..8)
@@ -287,6 +288,10 @@ struct Ctx {
 class Upload {
  public:
   Upload(Ctx& c, uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t chunk);
+  // chunk i = bytes [bounds[i], bounds[i+1]) (bounds[0] = 0, back() = n)
+  Upload(Ctx& c, uint8_t* dst, const uint8_t* src, uint64_t n, std::vector<uint64_t> bounds);
+  uint64_t off(uint64_t i) const { return bounds_[i]; }
+  uint64_t len(uint64_t i) const { return bounds_[i + 1] - bounds_[i]; }
   ~Upload();
   Upload(const Upload&) = delete;
   Upload& operator=(const Upload&) = delete;
@@ -300,7 +305,8 @@ class Upload {
   Ctx& c_;
   uint8_t* dst_;
   const uint8_t* src_;
-  uint64_t n_, C_, nch_;
+  uint64_t nch_;
+  std::vector<uint64_t> bounds_;
   HostPool* P_ = nullptr;
   uint64_t issued_ = 0;
   bool done_ = false;

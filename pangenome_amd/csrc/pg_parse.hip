@@ -592,14 +592,24 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   std::unique_ptr<Upload> upload;
   if (h_src) {
     const uint64_t C = std::max<uint64_t>(WSPAN, c.h2d_chunk / WSPAN * WSPAN);
+    // chunks of C bytes (whole spans); pg_build_host's last one small
+    // (h2d_tail): what follows the last byte's arrival - that chunk's K1 and
+    // its records' stage A share - then covers a few MB instead of up to C
+    std::vector<uint64_t> bounds{0};
+    const uint64_t tl = on_chunk ? (std::min(c.h2d_tail, C / 2) + WSPAN - 1) / WSPAN * WSPAN : 0;
+    const uint64_t body = tl && n > C + tl ? (n - tl) / WSPAN * WSPAN : n;
+    for (uint64_t o = 0; o < body; o += C) bounds.push_back(std::min(body, o + C));
+    if (bounds.size() > 2 && bounds.back() - bounds[bounds.size() - 2] < C / 4)
+      bounds.erase(bounds.end() - 2);                       // no sliver: the body's remainder joins its neighbour
+    if (body < n) bounds.push_back(n);
     // pinned source: DMA up to 8 chunks ahead; pageable (an mmap): through
     // the pinned staging ring (pg_stage.hip)
-    upload.reset(new Upload(c, c.fasta_own.as<uint8_t>(), h_src, n, C));
+    upload.reset(new Upload(c, c.fasta_own.as<uint8_t>(), h_src, n, bounds));
     Upload& up = *upload;
     const uint64_t nch = up.chunks();
     for (uint64_t i = 0; i < nch; ++i) {
       up.wait_queued(i);
-      const uint64_t off = i * C, len = std::min(C, n - off);
+      const uint64_t off = up.off(i), len = up.len(i);
       const uint64_t s0 = off / WSPAN, s1 = std::min(nspan, (off + len + WSPAN - 1) / WSPAN);
       PG_HIP(hipStreamWaitEvent(st, c.cev[i & 15], 0));
       up.consumed(i);

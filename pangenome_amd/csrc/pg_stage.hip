@@ -51,7 +51,8 @@ struct HostPool {
   bool job = false, abort = false, failed = false;
   uint8_t* dst = nullptr;
   const uint8_t* src = nullptr;
-  uint64_t n = 0, C = 0, nch = 0, nslots = 0, S = 0;   // S: bytes per slot (one piece)
+  uint64_t n = 0, nch = 0, nslots = 0, S = 0;          // S: bytes per slot (one piece)
+  std::vector<uint64_t> bounds;          // chunk i = [bounds[i], bounds[i+1])
   uint8_t* slots = nullptr;              // the ring (allocated when a chunk is staged)
   PinBuf* pin = nullptr;
   bool reg = false;                      // register chunks and DMA them directly
@@ -129,7 +130,7 @@ struct HostPool {
           // the chunk in pieces of one slot: the DMA of a piece starts as
           // soon as it is in pinned memory, so the ring fills in one piece's
           // copy time and the link never waits for a whole chunk
-          const uint64_t off = i * C, len = std::min(C, n - off);
+          const uint64_t off = bounds[i], len = bounds[i + 1] - bounds[i];
           bool direct = false;
           if (reg) {
             // register the chunk's pages for this upload and DMA them directly:
@@ -233,8 +234,17 @@ static bool is_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
+static std::vector<uint64_t> uniform_bounds(uint64_t n, uint64_t chunk) {
+  std::vector<uint64_t> b{0};
+  for (uint64_t o = 0; o < n; o += chunk) b.push_back(std::min(n, o + chunk));
+  return b;
+}
+
 Upload::Upload(Ctx& c, uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t chunk)
-    : c_(c), dst_(dst), src_(src), n_(n), C_(chunk), nch_(n ? (n + chunk - 1) / chunk : 0) {
+    : Upload(c, dst, src, n, uniform_bounds(n, chunk)) {}
+
+Upload::Upload(Ctx& c, uint8_t* dst, const uint8_t* src, uint64_t n, std::vector<uint64_t> bounds)
+    : c_(c), dst_(dst), src_(src), nch_(n ? bounds.size() - 1 : 0), bounds_(std::move(bounds)) {
   staged = nch_ && !(is_pinned(src) && is_pinned(src + n - 1));
   if (!staged) return;
   const uint64_t S = std::min(c.stage_piece, n);
@@ -243,7 +253,7 @@ Upload::Upload(Ctx& c, uint8_t* dst, const uint8_t* src, uint64_t n, uint64_t ch
   if (!c.host_register) c.stage_pin.reserve(nslots * S);
   P_ = pool_of(c);
   std::lock_guard<std::mutex> g(P_->mu);
-  P_->dst = dst; P_->src = src; P_->n = n; P_->C = C_; P_->nch = nch_;
+  P_->dst = dst; P_->src = src; P_->n = n; P_->bounds = bounds_; P_->nch = nch_;
   P_->nslots = nslots;
   P_->S = S;
   P_->slots = c.host_register ? nullptr : c.stage_pin.as<uint8_t>();
@@ -263,7 +273,7 @@ void Upload::wait_queued(uint64_t i) {
     // copies run up to 8 chunks ahead of the caller (an event is recorded
     // again only after the caller's wait on it was queued)
     while (issued_ < nch_ && issued_ < i + 8) {
-      const uint64_t off = issued_ * C_, len = std::min(C_, n_ - off);
+      const uint64_t off = bounds_[issued_], len = bounds_[issued_ + 1] - off;
       PG_HIP(hipMemcpyAsync(dst_ + off, src_ + off, len, hipMemcpyHostToDevice, c_.stream3));
       PG_HIP(hipEventRecord(c_.cev[issued_ & 15], c_.stream3));
       ++issued_;

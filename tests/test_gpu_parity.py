@@ -227,6 +227,46 @@ def test_k3_cover_forms_vs_oracle(oracle_mod, k):
     assert recs[0] <= recs[2] and recs[2] <= recs[1] * 1.02 + 64, recs
 
 
+@pytest.mark.parametrize("k", [15, 27])
+def test_k3_packed_exceptions_vs_oracle(oracle_mod, k):
+    """The packed coverage pass around bases that are not ACGT (their 2-bit
+    code is not their class): N runs, IUPAC codes in both cases and '$' in
+    members and in the lead and second reference records, at every alignment
+    of a 16-base word - the oracle's dBG and rdBG in every form."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context, PG_TUNE_K3_COVER
+    fasta = bytearray(synth.pangenome(8, 90_000, snp=2e-3, indel=3e-4, seed=700 + k, width=57))
+    rng = np.random.default_rng(k)
+    seq = np.zeros(len(fasta), bool)                 # sequence bytes (not headers, not newlines)
+    hdr = False
+    for i, b in enumerate(fasta):
+        if b == ord(">") and (i == 0 or fasta[i - 1] == ord("\n")):
+            hdr = True
+        if b == ord("\n"):
+            hdr = False
+        seq[i] = not hdr and b != ord("\n")
+    pos = np.flatnonzero(seq)
+    for p in rng.choice(pos, 400, replace=False).tolist():        # single odd bases
+        fasta[p] = rng.choice([ord(c) for c in "NnRYkmSWbdhv$"])
+    for p in rng.choice(pos[: pos.shape[0] // 8], 6, replace=False).tolist():   # N runs, some in the lead
+        for q in range(p, min(p + int(rng.integers(1, 70)), len(fasta))):
+            if seq[q]:
+                fasta[q] = ord("N")
+    fasta = bytes(fasta)
+    ref = oracle_mod.OracleRun(fasta, k, 2)
+    rk, rm = ref.dbg()
+    for form in (0, 1, 2):
+        ctx = Context(k)
+        ctx.tune(PG_TUNE_K3_COVER, form)
+        ctx.set_fasta(fasta)
+        ctx.parse()
+        ctx.build(None, 0, True)
+        keys, masks = ctx.dbg()
+        assert np.array_equal(keys, rk) and np.array_equal(masks, rm), form
+        assert np.array_equal(ctx.rdbg(), ref.rdbg()), form
+        ctx.close()
+
+
 def test_edge_checkpoint_reversal_vs_oracle(km, oracle_mod, tmp_path):
     from pangenome_amd import synth
     fasta = b"junk before header\n" + synth.pangenome(9, 20_000, snp=0.01, indel=1e-3, seed=5)
