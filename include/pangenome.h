@@ -58,7 +58,9 @@ typedef struct pg_stats {
   double ms_range;         /* K3 stage C: k_build_range (table + fused K5)         */
   uint64_t build_flags;    /* bit 0: the last pg_build_host split its records into
                               the table's partitions chunk by chunk under the upload
-                              (PG_TUNE_EARLY_SPLIT) and stage C read them          */
+                              (PG_TUNE_EARLY_SPLIT) and stage C read them; bits
+                              8..15: stages B/C re-runs of the last build (a plan
+                              or a capacity that did not hold)                     */
 } pg_stats;
 
 /* Context on HIP device `device` for k-mer length k (clamped to [1, 27] as
@@ -253,9 +255,10 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
 /* PG_TUNE_K3_HEAD: size of the first K3 chunk in 16ths of the middle ones
  * (1..64, 0 = 16: the coverage pass that runs before any work pass). */
 #define PG_TUNE_K3_HEAD 15
-/* PG_TUNE_H2D_TAIL: bytes of pg_build_host's last H2D chunk (default 8 MiB;
- * 0 = every chunk PG_TUNE_H2D_CHUNK bytes): what runs after the last byte has
- * landed starts from that chunk. */
+/* PG_TUNE_H2D_TAIL: bytes of pg_build_host's last H2D chunk (0, the default:
+ * every chunk PG_TUNE_H2D_CHUNK bytes).  A small last chunk puts two chunks'
+ * K1, record round trip and stage A share behind the last copy (C3: 9.91 ms
+ * at 8 MiB, 9.86 at 16, 9.80 uniform). */
 #define PG_TUNE_H2D_TAIL 16
 /* PG_TUNE_BUCKET_SHIFT: size the table 2^value times smaller than the record
  * count asks (0..8): exercises the overflow set, its spill and the re-run

@@ -47,7 +47,7 @@ static void fill_stats(const pg::Ctx& c, pg_stats* s) {
   s->ms_split = c.ms_split;
   s->ms_range = c.ms_range;
   s->sentinel = c.sentinel;
-  s->build_flags = c.early_split_used ? 1u : 0u;
+  s->build_flags = (c.early_split_used ? 1u : 0u) | ((uint64_t)std::min(255, std::max(0, c.bc_attempts - 1)) << 8);
 }
 
 extern "C" {

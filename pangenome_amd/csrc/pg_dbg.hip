@@ -1784,10 +1784,7 @@ __device__ __forceinline__ uint64_t part_at(const Recs& I, uint32_t p, const uns
 // with one global atomic, sorts them by bin in LDS and writes the runs
 // coalesced.  3 blocks (24 waves) per CU.
 constexpr int SB = 512, SR = 8, SCH = SB * SR;
-// (experiment bit 20: 2048-bucket stage C partitions, 3 blocks per CU, behind
-// 8-bit split passes)
-constexpr bool EXP_R11 = (PG_EXP_BITS & (1 << 20)) != 0;
-constexpr int SPLIT_BITS = EXP_R11 ? 8 : 7;   // bits per split pass
+constexpr int SPLIT_BITS = 7;                 // bits per split pass
 constexpr int SMAXB = 1 << SPLIT_BITS;
 // start (NULL: 0): per input region, the records below it are already split
 // (pg_build_host's early split); a block loops over its region's records in
@@ -1899,9 +1896,11 @@ __global__ void k_snap(const unsigned long long* __restrict__ cursor, unsigned l
 // rdBG members to its own output segment (no global atomics at all) and
 // leaves its key / dBG / member counts in its own counter slot.
 constexpr int RB_T = 512;                     // 2 blocks (16 waves) per CU: 70 KiB of LDS each
-constexpr int RB_R = EXP_R11 ? 4 : 8;         // records per thread and partition held in registers
-constexpr int RANGE_BITS = EXP_R11 ? 11 : 12; // <= 4096 buckets (64 KiB of LDS) per partition
-constexpr int RB_PER_CU = EXP_R11 ? 3 : 2;    // persistent range blocks per CU
+constexpr int RB_R = 8;                       // records per thread and partition held in registers
+// <= 4096 buckets (64 KiB of LDS) per partition (2048-bucket partitions at 3
+// blocks per CU behind 8-bit split passes: range 0.42 vs 0.31 ms on C3)
+constexpr int RANGE_BITS = 12;
+constexpr int RB_PER_CU = 2;                  // persistent range blocks per CU
 constexpr int OVL = 512;                      // LDS overflow slots per partition
 constexpr int RB_CTR = 4;                     // per-block counters: keys, dBG entries, members
 constexpr uint32_t MQ = 64;                   // queued rdBG members per wave
@@ -2512,6 +2511,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
   c.t6.init();
   debug_report("stage A");
   for (int attempt = 0; attempt < 8; ++attempt) {
+    c.bc_attempts = attempt + 1;
     const int fp = std::max(cb, bb - RANGE_BITS);
     const uint32_t rbits = (uint32_t)(bb - fp);
     const uint64_t buckets = 1ull << bb;

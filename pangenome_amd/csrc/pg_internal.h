@@ -147,7 +147,7 @@ struct Ctx {
   int k3_cover = 0;               // pg_tune: coverage pass (0 = packed form, 1 = LDS-staged members, 2 = quad form)
   int early_split = 1;            // pg_tune: pg_build_host splits each landed chunk's records (stage B under the upload)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
-  uint64_t h2d_tail = 8ull << 20;     // pg_tune: bytes of pg_build_host's last H2D chunk (0: uniform chunks)
+  uint64_t h2d_tail = 0;              // pg_tune: bytes of pg_build_host's last H2D chunk (0: uniform chunks)
   int host_threads = 0;           // pg_tune: memcpy threads of the staging ring (0 = by CPU affinity)
   uint64_t stage_piece = 32ull << 20;  // pg_tune: bytes per staging-ring slot (one DMA)
   uint64_t stage_slots = 4;       // pg_tune: staging-ring slots (2..8)
@@ -204,6 +204,7 @@ struct Ctx {
   DevBuf snapA;                       // pg_build_host's early split: stage A cursors already split
   double w_ratio = 0;                 // last host build: forward windows per input byte
   bool early_split_used = false;      // the last pg_build_host's stage C read the early split's partitions
+  int bc_attempts = 0;                // stages B/C runs of the last build (1: no re-run)
   DevBuf rseg;                        // rdBG keys: one segment of rseg_cap per stage C block
   DevBuf k5_ctr;                      // per stage C block: key / dBG / member counts
   uint64_t rseg_cap = 0, rseg_nseg = 0;

@@ -586,9 +586,11 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   };
   reserve_records(rcap0);
   bool streaming = on_chunk != nullptr;
-  // (kept to the end: the stager's last work - waiting for the DMAs and
-  // unregistering the chunks' pages, ~50 us on C3 - runs beside the record
-  // table's round trip and the caller's last stage A share instead of before)
+  // (the stager's last work - waiting for the DMAs and unregistering the
+  // chunks' pages - is waited for right after the last chunk's K1 is queued:
+  // left to run beside the last record round trip and stage A share, its
+  // runtime calls made those steps slower and uneven, 9.81 ms (max 9.92)
+  // against 9.77 (max 9.80) on C3 with alternating inputs)
   std::unique_ptr<Upload> upload;
   if (h_src) {
     const uint64_t C = std::max<uint64_t>(WSPAN, c.h2d_chunk / WSPAN * WSPAN);
@@ -637,6 +639,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
       c.n_records = Rc;
       (*on_chunk)(Rc);
     }
+    upload->finish();
   } else {
     hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
     PG_HIP(hipGetLastError());

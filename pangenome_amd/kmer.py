@@ -179,43 +179,16 @@ def seq2rdbg(qry, kmer=13, bits=5, Ns=1e6, chunk=2 ** 32, brkpt="./breakpoint", 
         resume = host.resume_position(offset, g.rec_ptr)
     flags, extra, ckpt = host.plan_dbg(g.seq_len, g.shape, bool(rc), int(Ns), int(chunk), resume=resume,
                                        checkpoint=True)
-    writer = None
     if ckpt is not None:
         cf, ce, last = ckpt
         g.ctx.build_dbg(cf, ce, bool(rc))
-        cap, size, keys, values, counts = g.ctx.dbg_dump()
-        # the checkpoint file goes to disk on a host thread while the GPU
-        # builds the whole pass (C4: ~2.7 GB of slot arrays)
-        writer = _Background(host.write_db_npz, qry + "_db_brkpt", cap, size, keys, values, counts,
-                             offset=int(g.rec_ptr[last]))
-        del keys, values, counts
-    try:
-        g.stats = g.ctx.build_dbg(flags, extra, bool(rc))
-    finally:
-        if writer is not None:
-            writer.join()
+        # the checkpoint file streamed from the device (pg_dbg_dump_fd: no
+        # host copy of the slot arrays; C4: ~2.7 GB of them), then the pass
+        cap, size = g.ctx.dbg_dump_size()
+        host.write_db_npz_from(qry + "_db_brkpt", cap, size, lambda fd, offs: g.ctx.dbg_dump_fd(fd, offs, cap),
+                               offset=int(g.rec_ptr[last]))
+    g.stats = g.ctx.build_dbg(flags, extra, bool(rc))
     return g
-
-
-class _Background:
-    """fn(*a, **kw) on a thread; join() waits and re-raises its error."""
-
-    def __init__(self, fn, *a, **kw):
-        import threading
-        self.err = None
-
-        def run():
-            try:
-                fn(*a, **kw)
-            except BaseException as e:              # noqa: BLE001 (re-raised by join)
-                self.err = e
-        self.th = threading.Thread(target=run, daemon=True)
-        self.th.start()
-
-    def join(self):
-        self.th.join()
-        if self.err is not None:
-            raise self.err
 
 
 def dump(g: DeviceGraph, fn="./tmp"):

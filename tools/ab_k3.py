@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--genomes", type=int, default=100)
     ap.add_argument("--tune", action="append", default=[])
     ap.add_argument("--host", action="store_true", help="pg_build_host from the page-cache-warm mmap instead")
+    ap.add_argument("--alt", action="store_true", help="(--host) alternate two batches (genomes 0-99, 100-199)")
+    ap.add_argument("--env", action="append", default=[], help="per-variant environment NAME=V (index-aligned with --tune)")
     args = ap.parse_args()
     import torch
     from pangenome_amd import _lib, kmer, synth
@@ -37,10 +39,16 @@ def main():
     synth.write_pangenome(p, args.genomes, 5_000_000, first_index=0, workers=16)
     print("generated %.1f s" % (time.time() - t0), flush=True)
     mm = kmer.seq2bytes(p)
+    mms = [mm]
+    if args.alt:
+        p2 = os.path.join(tmp, "c3b.fa")
+        synth.write_pangenome(p2, args.genomes, 5_000_000, first_index=args.genomes, workers=16)
+        mms.append(kmer.seq2bytes(p2))
     d = torch.from_numpy(np.array(mm)).to("cuda:0")
     if not args.host:
         os.unlink(p)
-    dig = json.load(open(os.path.join(ROOT, "tests", "golden", "scale", "c3a.json"))) if args.genomes == 100 else None
+    digs = [json.load(open(os.path.join(ROOT, "tests", "golden", "scale", n + ".json"))) for n in ("c3a", "c3b")] \
+        if args.genomes == 100 else [None, None]
     ctxs = []
     for v in variants:
         ctx = _lib.Context(27, 0)
@@ -49,24 +57,34 @@ def main():
                 what, val = kv.split("=")
                 ctx.tune(getattr(_lib, "PG_TUNE_" + what), int(val))
         ctxs.append(ctx)
-    res = {v: [] for v in variants}
+    res = [[] for _ in variants]
+    envs = dict(e.split("=", 1) for e in args.env)
     for step in range(args.steps + 2):
-        for v, ctx in zip(variants, ctxs):
+        for vi, (v, ctx) in enumerate(zip(variants, ctxs)):
+            for e in envs:
+                os.environ.pop(e, None)
+            if vi < len(args.env):
+                name, val = args.env[vi].split("=", 1)
+                if val:
+                    os.environ[name] = val
+            b = step % len(mms)
+            dig = digs[b]
             torch.cuda.synchronize()
             t1 = time.perf_counter()
             if args.host:
-                st = ctx.build_host(mm, True)
+                st = ctx.build_host(mms[b], True)
             else:
                 st = ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d)
             ms = 1e3 * (time.perf_counter() - t1)
             ok = dig is None or (st.n_dbg, st.n_rdbg) == (dig["n_dbg"], dig["n_rdbg"])
             if step >= 2:
-                res[v].append((ms, st.ms_parse, st.ms_insert, st.ms_split, st.ms_range, st.n_records_a, ok))
-    for v in variants:
-        a = np.array([r[:6] for r in res[v]])
+                res[vi].append((ms, st.ms_parse, st.ms_insert, st.ms_split, st.ms_range, st.n_records_a, ok))
+    for vi, v in enumerate(variants):
+        a = np.array([r[:6] for r in res[vi]])
         med = np.median(a, axis=0)
-        print("%-40s step %.3f  parse %.3f  stageA %.3f  split %.3f  range %.3f  recA %d  ok %s" %
-              (v, med[0], med[1], med[2], med[3], med[4], int(med[5]), all(r[6] for r in res[v])), flush=True)
+        print("%-40s step %.3f (max %.3f)  parse %.3f  stageA %.3f  split %.3f  range %.3f  recA %d  ok %s" %
+              (v + (" " + args.env[vi] if vi < len(args.env) else ""), med[0], a[:, 0].max(), med[1], med[2],
+               med[3], med[4], int(med[5]), all(r[6] for r in res[vi])), flush=True)
 
 
 if __name__ == "__main__":

@@ -33,12 +33,12 @@ for step in "$@"; do
     pmc) bash tools/pmc_kernels.sh "k_span_sum|k_emit|k_records|k_pack_fix|k_cover|k_short_emit|k_split|k_build_range|rocprim" tr traffic ;;
     parity) run pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -v --timeout 120 --timeout-method thread ;;
     abcover) run ab_cover 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=2 ;;
-    abhost) run ab_host 600 python -u tools/ab_k3.py --host --steps 12 --tune base --tune H2D_TAIL=0 --tune H2D_TAIL=16777216 --tune H2D_CHUNK=134217728 --tune EARLY_SPLIT=0 ;;
+    abhost) run ab_host 600 python -u tools/ab_k3.py --host --steps 12 --tune base --tune EARLY_SPLIT=0 ;;
     abchunks) run ab_chunks 900 python -u tools/ab_k3.py --steps 10 --tune base --tune K3_HEAD=8 --tune K3_HEAD=8,K3_TAIL=6 --tune K3_CHUNKS=4,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=4 --tune K3_CHUNKS=5,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=2 ;;
     npz) run pytest_npz 600 python -u -m pytest tests/test_gpu_npz.py -x -v --timeout 300 --timeout-method thread ;;
     savebd) run save_bd 300 python -u tools/save_breakdown.py ;;
     tracewin) run trace_win 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tw -o run --output-format csv -- python tools/ab_k3.py --host --steps 3 --tune base ;;
-    abr11) run ab_r11_base 400 python -u tools/ab_k3.py --steps 12 --tune base && run ab_r11_exp 400 env PG_LIB_NAME=libpangenome_hip_e1048576.so python -u tools/ab_k3.py --steps 12 --tune base && run ab_r11_hbase 400 python -u tools/ab_k3.py --host --steps 8 --tune base && run ab_r11_hexp 400 env PG_LIB_NAME=libpangenome_hip_e1048576.so python -u tools/ab_k3.py --host --steps 8 --tune base ;;
+    abfin) run ab_fin 600 python -u tools/ab_k3.py --host --alt --steps 16 --tune base --tune base --env PG_EXP_FINISH_EARLY= --env PG_EXP_FINISH_EARLY=1 ;;
     abdev) run ab_dev 600 python -u tools/ab_k3.py --steps 12 --tune base --tune EARLY_SPLIT=0 --tune K3_COVER=2 ;;
     ab) run ab_k3 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=1 ;;
     listctr) run listctr 300 rocprofv3 -L ;;
