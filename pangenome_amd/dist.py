@@ -149,25 +149,41 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
 A2A_ROWS = 1 << 25
 
 
-def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None, big=None):
+def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None, big=None, self_copy=True):
     """all_to_all of (n, 2) int64 rows in pieces of at most A2A_ROWS rows per
     peer (every rank runs the same number of pieces: the largest message of
     any rank decides; `big`, when the caller knows it, else one MAX
-    all-reduce finds it).  Views of contiguous runs, no copies."""
+    all-reduce finds it).  Views of contiguous runs; the rank's own run is a
+    device copy and never goes through the collective (`self_copy=False`:
+    it does, tests/test_gpu_rccl.py's way to drive RCCL at world 1)."""
     import torch
     import torch.distributed as dist
     world = len(ssplit)
+    me = dist.get_rank(group) if world > 1 else 0
+    if not self_copy:
+        me = -1
+    # the rank's own run: a device copy (at world 1 nothing else moves).  C5's
+    # streamed exchange at world 1 came back wrong in some runs when its
+    # ~16 GB per round went to self through RCCL in 512 MiB pieces
+    # (nondeterministic, box-dependent) and never with the copy.
+    if me >= 0 and ssplit[me]:
+        so_me = int(np.sum(ssplit[:me])) if me else 0
+        ro_me = int(np.sum(rsplit[:me])) if me else 0
+        recv[ro_me:ro_me + rsplit[me]].copy_(send[so_me:so_me + ssplit[me]])
+    if world == 1 and me == 0:
+        return
+    ssplit, rsplit = list(ssplit), list(rsplit)
+    ssplit_me, rsplit_me = (ssplit[me], rsplit[me]) if me >= 0 else (0, 0)
+    if me >= 0:
+        ssplit[me] = rsplit[me] = 0
     if big is None:
         b = torch.tensor([max(max(ssplit), max(rsplit)) if world else 0], dtype=torch.int64, device=comm)
         dist.all_reduce(b, op=dist.ReduceOp.MAX, group=group)
         big = int(b.item())
+    # (offsets from the real run lengths: the own run keeps its place)
+    so = np.concatenate([[0], np.cumsum([x if i != me else ssplit_me for i, x in enumerate(ssplit)])]).astype(np.int64)
+    ro = np.concatenate([[0], np.cumsum([x if i != me else rsplit_me for i, x in enumerate(rsplit)])]).astype(np.int64)
     npieces = max(1, -(-int(big) // A2A_ROWS))
-    if npieces == 1:
-        dist.all_to_all_single(recv[:sum(rsplit)], send[:sum(ssplit)], output_split_sizes=rsplit,
-                               input_split_sizes=ssplit, group=group)
-        return
-    so = np.concatenate([[0], np.cumsum(ssplit)]).astype(np.int64)
-    ro = np.concatenate([[0], np.cumsum(rsplit)]).astype(np.int64)
     lists = dist.get_backend(group) != "gloo"             # (gloo has no list all_to_all: pieces copied)
     for j in range(npieces):
         lo = j * A2A_ROWS

@@ -56,6 +56,9 @@ def _c5_rank(rank, world, port, q, path, backend, chunk_bases, compact_at, whole
         dist.init_process_group("gloo", rank=rank, world_size=world)
     out = {"backend": dist.get_backend()}
     sh = GpuShard(27, 0)
+    if os.environ.get("PG_TEST_K3_COVER"):          # (tools/c5_forms.py: the coverage form under test)
+        from pangenome_amd._lib import PG_TUNE_K3_COVER
+        sh.ctx.tune(PG_TUNE_K3_COVER, int(os.environ["PG_TEST_K3_COVER"]))
     t0 = time.time()
     meta = sh.load(kmer.seq2bytes(path))
     R = int(meta["seq_len"].shape[0])

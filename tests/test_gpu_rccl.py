@@ -36,9 +36,13 @@ def _rank(rank, world, port, q):
         send = torch.arange(2 * rows, dtype=torch.int64, device=dev).view(rows, 2)
         send.mul_(-7046029254386353131).add_(12345)
         recv = torch.empty((rows, 2), dtype=torch.int64, device=dev)
-        pdist._all_to_all_rows(recv, send, [rows], [rows], dev)
+        pdist._all_to_all_rows(recv, send, [rows], [rows], dev, self_copy=False)   # through RCCL
         torch.cuda.synchronize()
         out[tag] = bool(torch.equal(recv, send))
+        recv.zero_()
+        pdist._all_to_all_rows(recv, send, [rows], [rows], dev)                    # the product path: a copy
+        torch.cuda.synchronize()
+        out[tag + "_copy"] = bool(torch.equal(recv, send))
         if tag == "past_limit":
             recv.zero_()
             dist.all_to_all_single(recv, send, output_split_sizes=[rows], input_split_sizes=[rows])
@@ -54,4 +58,4 @@ def _rank(rank, world, port, q):
 def test_all_to_all_rows_pieces_over_rccl():
     out = spawn_ranks(1, _rank, (), timeout=240)[0]
     print("rccl all_to_all: %s" % out)
-    assert out["just_over"] and out["past_limit"]
+    assert out["just_over"] and out["past_limit"] and out["just_over_copy"] and out["past_limit_copy"]

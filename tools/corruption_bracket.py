@@ -10,7 +10,10 @@
    recv[torch.argsort(sub, stable=True)] with sub = a hash of the key word,
    on (n, 2) int64 rows, checked against numpy on the host.
 
-    python tools/corruption_bracket.py a2a|sort > out.jsonl
+3. torch.cat / clone of (n, 2) int64 row tensors past 2^31 elements (the
+   streamed exchange's sub-log concatenation at C5 size).
+
+    python tools/corruption_bracket.py a2a|sort|cat > out.jsonl
 One JSON line per case on stdout.
 """
 import json
@@ -123,12 +126,81 @@ def sort_cases(dev):
             break
 
 
+def same(a, b, piece=1 << 26):
+    """a == b row for row, compared in pieces (no full-size temporaries)."""
+    n = a.shape[0]
+    for o in range(0, n, piece):
+        if not torch.equal(a[o:o + piece], b[o:o + piece]):
+            ne = (a[o:o + piece] != b[o:o + piece]).any(dim=1)
+            return o + int(torch.argmax(ne.to(torch.uint8)))
+    return -1
+
+
+def cat_case(dev, rows_a, rows_b, op):
+    res = dict(case="cat", op=op, rows=rows_a + rows_b, elements=2 * (rows_a + rows_b),
+               bytes=16 * (rows_a + rows_b))
+    try:
+        a = fill(16 * rows_a, dev).view(torch.int64).view(-1, 2)
+        if op == "cat":
+            b = fill(16 * rows_b, dev).view(torch.int64).view(-1, 2).flip(0).contiguous()
+            c = torch.cat([a, b])
+            torch.cuda.synchronize()
+            fa, fb = same(c[:rows_a], a), same(c[rows_a:], b)
+            res.update(ok=fa < 0 and fb < 0, first_bad_row=fa if fa >= 0 else (rows_a + fb if fb >= 0 else -1))
+        else:                                          # clone of a row slice (the sub-log pieces)
+            c = a[1:].clone()
+            torch.cuda.synchronize()
+            f = same(c, a[1:])
+            res.update(ok=f < 0, first_bad_row=f)
+    except Exception as e:                            # noqa: BLE001
+        res.update(ok=False, error=str(e).splitlines()[0])
+    emit(**res)
+    return res["ok"]
+
+
+def cat_cases():
+    import subprocess
+    G = 1 << 30
+    for rows in ((G // 2, G // 2 - 1), (G // 2, G // 2), (G // 2, G // 2 + 1), (G // 2 + G // 8, G // 2),
+                 (G, G // 2)):
+        for op in ("cat", "clone"):
+            subprocess.run([sys.executable, "-u", __file__, "cat1", str(rows[0]), str(rows[1]), op], timeout=300)
+
+
+def repeat_cases(dev, reps=64, rows=1 << 25):
+    """The exchange's per-piece pattern at world 1: all_to_all(list) of one
+    A2A_ROWS-row piece (512 MiB) to self, `reps` times from different
+    offsets of one large buffer, each checked."""
+    n = rows * 8
+    src = fill(16 * n, dev).view(torch.int64).view(-1, 2)
+    dst = torch.zeros_like(src)
+    bad = []
+    for r in range(reps):
+        o = (r % 8) * rows
+        dist.all_to_all([dst[o:o + rows]], [src[o:o + rows]])
+        torch.cuda.synchronize()
+        f = same(dst[o:o + rows], src[o:o + rows])
+        if f >= 0:
+            bad.append((r, f))
+        dst[o:o + rows].zero_()
+    emit(case="repeat", op="all_to_all_list", rows=rows, bytes=16 * rows, reps=reps, ok=not bad, bad=bad[:8],
+         n_bad=len(bad))
+
+
 def main():
     what = sys.argv[1] if len(sys.argv) > 1 else "all"
     if what == "sort1":
         torch.cuda.set_device(0)
         ok = sort_case(torch.device("cuda", 0), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4])
         sys.exit(0 if ok else 1)
+    if what == "cat1":
+        torch.cuda.set_device(0)
+        ok = cat_case(torch.device("cuda", 0), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4])
+        sys.exit(0 if ok else 1)
+    if what == "cat":
+        emit(case="env", torch=torch.__version__, hip=torch.version.hip)
+        cat_cases()
+        return
     if what == "sort":                                # (the parent never touches the GPU)
         emit(case="env", torch=torch.__version__, hip=torch.version.hip)
         sort_cases(None)
@@ -139,7 +211,10 @@ def main():
     emit(case="env", torch=torch.__version__, hip=torch.version.hip,
          rccl=".".join(map(str, torch.cuda.nccl.version())), device=torch.cuda.get_device_name(0))
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    a2a_cases(dev)
+    if what == "repeat":
+        repeat_cases(dev)
+    else:
+        a2a_cases(dev)
     dist.destroy_process_group()
 
 

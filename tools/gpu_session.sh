@@ -25,6 +25,8 @@ for step in "$@"; do
     cover) run pytest_cover 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parse.py tests/test_gpu_rccl.py -k "k3 or early_split or build_host or rccl" -v --timeout 120 --timeout-method thread ;;
     dbgc3) run dbg_c3 400 env PG_LIB_NAME=libpangenome_hip_dbg.so python -u tools/dbg_host_c3.py 0 2 ;;
     missing) run dbg_missing 400 env PG_LIB_NAME=libpangenome_hip_dbg.so python -u tools/dbg_missing.py gpurun_out/missing.npz ;;
+    bracketrep) run bracket_rep 600 python -u tools/corruption_bracket.py repeat ;;
+    bracketcat) run bracket_cat 900 python -u tools/corruption_bracket.py cat ;;
     bracket) run bracket_sort 500 python -u tools/corruption_bracket.py sort ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
@@ -39,6 +41,9 @@ for step in "$@"; do
     savebd) run save_bd 300 python -u tools/save_breakdown.py ;;
     tracewin) run trace_win 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tw -o run --output-format csv -- python tools/ab_k3.py --host --steps 3 --tune base ;;
     abfin) run ab_fin 600 python -u tools/ab_k3.py --host --alt --steps 16 --tune base --tune base --env PG_EXP_FINISH_EARLY= --env PG_EXP_FINISH_EARLY=1 ;;
+    c5diag) run c5_diag 900 env C5_DIAG=1 python -u tools/c5_forms.py 0:30 0:30 0:30 ;;
+    c5rep) run c5_rep 900 python -u tools/c5_forms.py 0:30 0:30 0:30 0:30 2:30 ;;
+    c5forms) run c5_forms 900 python -u tools/c5_forms.py ;;
     abdev) run ab_dev 600 python -u tools/ab_k3.py --steps 12 --tune base --tune EARLY_SPLIT=0 --tune K3_COVER=2 ;;
     ab) run ab_k3 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=1 ;;
     listctr) run listctr 300 rocprofv3 -L ;;
