@@ -140,6 +140,27 @@ __device__ __forceinline__ void init_keys(const uint8_t* sc, uint32_t o, int k, 
   Kr = (uint64_t)rlo + rhi * 1220703125ull;
 }
 
+// init_keys for k = 27 from seven dword reads of the row (realigned by
+// v_alignbyte) instead of 2 x 27 byte reads: the digits come out of registers
+// at constant positions (the work pass's LDS instructions were half these
+// byte reads)
+__device__ __forceinline__ void init_keys27(const uint8_t* sc, uint32_t o, uint64_t& K, uint64_t& Kr) {
+  uint32_t w[7];
+  lds_bytes(sc, o, w);
+  uint32_t lo = 0, rlo = 0;
+  uint64_t hi = 0, rhi = 0;
+#pragma unroll
+  for (int j = 12; j >= 0; --j) lo = lo * 5u + digit_fw(byte_at(w, j));
+#pragma unroll
+  for (int j = 26; j >= 13; --j) hi = hi * 5u + digit_fw(byte_at(w, j));
+#pragma unroll
+  for (int j = 0; j < 14; ++j) rhi = rhi * 5u + digit_rc(byte_at(w, j));
+#pragma unroll
+  for (int j = 14; j < 27; ++j) rlo = rlo * 5u + digit_rc(byte_at(w, j));
+  K = (uint64_t)lo + hi * 1220703125ull;         // 5^13
+  Kr = (uint64_t)rlo + rhi * 1220703125ull;
+}
+
 // K3 tile: record r's windows [stripe*TILE, (stripe+1)*TILE), with the
 // record's compacted start and length carried along (one load per block).
 struct TileDesc {
@@ -175,7 +196,10 @@ __device__ __forceinline__ void segment_records(const uint8_t* s_cls, long long 
                                                 int k, uint64_t shift, const TableView& T, uint32_t covered,
                                                 uint64_t& K, uint64_t& Kr, uint64_t (&hh)[NX], uint32_t (&mm)[NX]) {
   static_assert(X0 % 4 == 0 && NX % 4 == 0 && X0 + NX <= IW, "whole dwords of the segment");
-  if (X0 == 0) init_keys(s_cls, (uint32_t)(base + q0), k, K, Kr);
+  if (X0 == 0) {
+    if (k == 27) init_keys27(s_cls, (uint32_t)(base + q0), K, Kr);
+    else init_keys(s_cls, (uint32_t)(base + q0), k, K, Kr);
+  }
   if (q0 > 0 && q0 + IW <= last) {
     // interior segment (no window 0, no last window, all IW live): the context
     // bytes come from LDS once, into registers; P(i) = S(q-1), D(i) = S(q+k-1)

@@ -42,9 +42,11 @@ for step in "$@"; do
     tracewin) run trace_win 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tw -o run --output-format csv -- python tools/ab_k3.py --host --steps 3 --tune base ;;
     abfin) run ab_fin 600 python -u tools/ab_k3.py --host --alt --steps 16 --tune base --tune base --env PG_EXP_FINISH_EARLY= --env PG_EXP_FINISH_EARLY=1 ;;
     c5diag) run c5_diag 900 env C5_DIAG=1 python -u tools/c5_forms.py 0:30 0:30 0:30 ;;
+    c4cli) run c4_cli 900 env PG_TIMING_LOG=gpurun_out/c4_timing.jsonl python -u -m pytest tests/test_gpu_scale.py -k c4 -x -v --timeout 800 --timeout-method thread ;;
+    c4ckpt) run c4_ckpt 900 python -u tools/c4_ckpt_times.py ;;
     c5rep) run c5_rep 900 python -u tools/c5_forms.py 0:30 0:30 0:30 0:30 2:30 ;;
     c5forms) run c5_forms 900 python -u tools/c5_forms.py ;;
-    abdev) run ab_dev 600 python -u tools/ab_k3.py --steps 12 --tune base --tune EARLY_SPLIT=0 --tune K3_COVER=2 ;;
+    abdev) run ab_dev 600 python -u tools/ab_k3.py --steps 16 --tune base ;;
     ab) run ab_k3 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=1 ;;
     listctr) run listctr 300 rocprofv3 -L ;;
     *) echo "unknown step $step"; exit 2 ;;
