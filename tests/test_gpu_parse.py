@@ -265,6 +265,32 @@ def test_build_host_mmap_and_pinned(tmp_path, threads, register):
     ctx.close()
 
 
+@pytest.mark.parametrize("tail", [16384, 3 * 16384, 100_000])
+def test_build_host_small_last_chunk(tmp_path, tail):
+    """pg_build_host with a last H2D chunk smaller than the others
+    (PG_TUNE_H2D_TAIL: the chunk bounds are no longer uniform, a body
+    remainder shorter than a quarter chunk joins its neighbour), from the mmap
+    and from pinned memory, three builds each (the early split and the
+    speculative stage C of the warm builds): the oracle's dBG and rdBG."""
+    import torch
+    from pangenome_amd import kmer, synth
+    from pangenome_amd._lib import Context, PG_TUNE_H2D_CHUNK, PG_TUNE_H2D_TAIL
+    buf = synth.pangenome(12, 90_000, snp=2e-3, indel=2e-4, seed=23)
+    q = tmp_path / "in.fa"
+    q.write_bytes(buf)
+    ref = _oracle_ref(buf)
+    mm = kmer.seq2bytes(str(q))
+    pin = torch.empty(len(buf) + 64, dtype=torch.uint8, pin_memory=True)
+    pin.numpy()[:len(buf)] = np.frombuffer(buf, np.uint8)
+    ctx = Context(27)
+    ctx.tune(PG_TUNE_H2D_CHUNK, 8 * 16384)
+    ctx.tune(PG_TUNE_H2D_TAIL, tail)
+    for _ in range(3):
+        _check_build(ctx, ctx.build_host(mm, True), ref)
+        _check_build(ctx, ctx.build_host_ptr(pin.data_ptr(), len(buf), True), ref)
+    ctx.close()
+
+
 def test_cli_build_uses_streamed_path(tmp_path):
     """kmer.seq2rdbg on a file no -n / checkpoint touches builds through
     pg_build_host (the stats of a streamed build: stage A records counted

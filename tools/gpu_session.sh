@@ -22,7 +22,7 @@ for step in "$@"; do
     benchq) run bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
     rehearse2) run bench_rehearse2 900 env PG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 2 --warmup 1 ;;
     rehearse2c3) run bench_rehearse2c3 600 env PG_BENCH_REHEARSE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29612 bench.py --gpus 2 --config c3 --steps 3 --warmup 1 ;;
-    cover) run pytest_cover 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parse.py tests/test_gpu_rccl.py -k "k3 or early_split or build_host or rccl" -v --timeout 120 --timeout-method thread ;;
+    cover) run pytest_cover 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_parse.py tests/test_gpu_rccl.py -k "k3 or early_split or build_host or rccl or last_chunk" -v --timeout 120 --timeout-method thread ;;
     dbgc3) run dbg_c3 400 env PG_LIB_NAME=libpangenome_hip_dbg.so python -u tools/dbg_host_c3.py 0 2 ;;
     missing) run dbg_missing 400 env PG_LIB_NAME=libpangenome_hip_dbg.so python -u tools/dbg_missing.py gpurun_out/missing.npz ;;
     bracketrep) run bracket_rep 600 python -u tools/corruption_bracket.py repeat ;;
