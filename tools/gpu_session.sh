@@ -33,6 +33,7 @@ for step in "$@"; do
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange ;;
     pmcsq) bash tools/pmc_kernels.sh "k_emit_work|k_cover_p|k_build_range|k_emit\(|k_span_sum|k_split" sq ;;
     pmc) bash tools/pmc_kernels.sh "k_span_sum|k_emit|k_records|k_pack_fix|k_cover|k_short_emit|k_split|k_build_range|rocprim" tr traffic ;;
+    parse) run pytest_parse 600 python -u -m pytest tests/test_gpu_parse.py -x -v --timeout 120 --timeout-method thread ;;
     parity) run pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -v --timeout 120 --timeout-method thread ;;
     abcover) run ab_cover 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=2 ;;
     abhost) run ab_host 600 python -u tools/ab_k3.py --host --steps 12 --tune base --tune EARLY_SPLIT=0 ;;
