@@ -2530,8 +2530,11 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
   // a split level that overflowed: its partitions' exact counts (the cursors
   // count every record, kept or not) size it on the next attempt, so skewed
   // keys cost one re-run per level instead of a geometric capacity search
-  std::vector<uint64_t> lv_exact;
-  int lv_exact_bb = -1;
+  // (a key repeated in many records lands all of them in one partition: C4's
+  // largest level-2 partition holds ~1.9x the mean, so the plan's capacities
+  // overflowed on every build until they started from the last re-run's)
+  std::vector<uint64_t> lv_exact = c.lv_keep;
+  int lv_exact_bb = c.lv_keep_bb;
   c.t6.init();
   debug_report("stage A");
   for (int attempt = 0; attempt < 8; ++attempt) {
@@ -2674,6 +2677,8 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
         for (size_t i = 0; i < ex.size() && i < lv_exact.size(); ++i) ex[i] = std::max(ex[i], lv_exact[i]);
       lv_exact = ex;
       lv_exact_bb = bb;
+      c.lv_keep = ex;
+      c.lv_keep_bb = bb;
       if (!over) capx *= 1.5;                     // (not expected: the flag without a visible overflow)
       continue;
     }

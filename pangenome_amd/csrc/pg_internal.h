@@ -205,6 +205,10 @@ struct Ctx {
   double w_ratio = 0;                 // last host build: forward windows per input byte
   bool early_split_used = false;      // the last pg_build_host's stage C read the early split's partitions
   int bc_attempts = 0;                // stages B/C runs of the last build (1: no re-run)
+  // the largest partition of each split level that a build had to re-run
+  // for (at table bits lv_keep_bb): later builds' plans start from them
+  std::vector<uint64_t> lv_keep;
+  int lv_keep_bb = -1;
   DevBuf rseg;                        // rdBG keys: one segment of rseg_cap per stage C block
   DevBuf k5_ctr;                      // per stage C block: key / dBG / member counts
   uint64_t rseg_cap = 0, rseg_nseg = 0;

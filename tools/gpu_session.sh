@@ -28,6 +28,8 @@ for step in "$@"; do
     bracketrep) run bracket_rep 600 python -u tools/corruption_bracket.py repeat ;;
     bracketcat) run bracket_cat 900 python -u tools/corruption_bracket.py cat ;;
     bracket) run bracket_sort 500 python -u tools/corruption_bracket.py sort ;;
+    abc4dbg) run ab_c4dbg 600 env PG_DEBUG_BUILD=1 python -u tools/ab_k3.py --genomes 1000 --steps 2 --tune base ;;
+    benchc4) run bench_c4 900 python bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline --no-cli ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
     prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange ;;
