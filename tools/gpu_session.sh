@@ -38,7 +38,7 @@ for step in "$@"; do
     parse) run pytest_parse 600 python -u -m pytest tests/test_gpu_parse.py -x -v --timeout 120 --timeout-method thread ;;
     parity) run pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py -x -v --timeout 120 --timeout-method thread ;;
     abcover) run ab_cover 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=2 ;;
-    abhost) run ab_host 600 python -u tools/ab_k3.py --host --steps 12 --tune base --tune EARLY_SPLIT=0 ;;
+    abhost) run ab_host 600 python -u tools/ab_k3.py --host --alt --steps 12 --tune base --tune H2D_CHUNK=134217728,H2D_TAIL=67108864 --tune H2D_CHUNK=201326592,H2D_TAIL=67108864 --tune H2D_CHUNK=134217728,H2D_TAIL=50331648 ;;
     abchunks) run ab_chunks 900 python -u tools/ab_k3.py --steps 10 --tune base --tune K3_HEAD=8 --tune K3_HEAD=8,K3_TAIL=6 --tune K3_CHUNKS=4,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=4 --tune K3_CHUNKS=5,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=2 ;;
     npz) run pytest_npz 600 python -u -m pytest tests/test_gpu_npz.py -x -v --timeout 300 --timeout-method thread ;;
     savebd) run save_bd 300 python -u tools/save_breakdown.py ;;
