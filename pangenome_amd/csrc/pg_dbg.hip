@@ -1129,6 +1129,15 @@ __device__ __forceinline__ void drift_task_p(uint32_t A0, uint32_t A1, const uin
     }
   }
 }
+// A block barrier that orders LDS only (s_waitcnt lgkmcnt(0); s_barrier):
+// the packed coverage pass exchanges nothing through global memory inside a
+// block, so its global loads stay in flight across its barriers (a
+// __syncthreads also waits for every outstanding load, vmcnt(0)).
+__device__ __forceinline__ void cover_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2], const uint32_t (*s_ref)[RDW],
                                                const TriGeo* tri, unsigned (*best)[2][NANCH], uint32_t dm0,
                                                uint32_t dm1) {
@@ -1145,7 +1154,7 @@ __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2]
         drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo1, g.hi1, w, &best[m][ri][ai]);
     }
   }
-  __syncthreads();
+  cover_barrier();
   // pairs whose three anchors all missed: decided by every wave from the
   // state the barrier above published, and the barrier below keeps any
   // wave's search from changing best[] before every wave has decided (a
@@ -1158,7 +1167,7 @@ __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2]
       need |= 1u << p;
   }
   if (!need) return;                                          // (block-uniform)
-  __syncthreads();
+  cover_barrier();
 #pragma unroll 1
   for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
@@ -1170,7 +1179,7 @@ __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2]
         drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo, g.hi, w, &best[m][ri][ai]);
     }
   }
-  __syncthreads();
+  cover_barrier();
 }
 
 // 8 words of s_ref from word index idx (idx & 3 the same on every lane: a
@@ -1250,6 +1259,24 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
     dm0 |= (uint32_t)d0 << m;
     dm1 |= (uint32_t)(d0 && ref2 >= 0 && ref2 != td.r) << m;
   }
+  // the coverage phase's member words and exception bytes, loaded now: they
+  // depend on nothing the block computes, and the barriers up to that phase
+  // wait for LDS only (cover_barrier), so the loads land under the search
+  const int mw = __builtin_amdgcn_readfirstlane(t >> 6), lw = t & 63;
+  uint32_t M[LW], eex = 0;
+  {
+    long long rsm = mrs[0];
+#pragma unroll
+    for (int y = 1; y < QM; ++y) if (mw == y) rsm = mrs[y];
+    const long long wb = ((rsm + qt - 1) >> 4) + 4 * lw, a = wb & ~3ll;
+    const bool on = (dm0 >> mw) & 1u;
+#pragma unroll
+    for (int i = 0; i < LW; ++i) M[i] = on ? p2_word(p2, wb + i, n_p2) : 0u;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (on && a + 4 * i >= 0 && (uint64_t)(a + 4 * i + 4) <= n_p2 + 16)
+        eex |= *reinterpret_cast<const uint32_t*>(e16 + a + 4 * i);
+  }
   if (t == 0) s_rexc = 0u;
   if (t < QM * NANCH) {                            // anchors: 32 bases = 2 words each
     const int m = t / NANCH, ai = t % NANCH;
@@ -1280,7 +1307,7 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
     }
     s_tri[x] = G;
   }
-  __syncthreads();                                 // (s_rexc cleared)
+  cover_barrier();                                 // (s_rexc cleared)
   {
     static_assert(RSTAGEW <= 2 * CBLOCK, "two words per thread and reference");
     uint32_t v[2][2], ex = 0;
@@ -1304,7 +1331,7 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
           s_ref[ri][RPADW + t + h * CBLOCK] = v[ri][h];
     if (ex) atomicOr(&s_rexc, ex);
   }
-  __syncthreads();
+  cover_barrier();
   {
     // a reference whose staged span holds a base that is not ACGT covers nothing here
     const uint32_t rexc = s_rexc;
@@ -1327,7 +1354,7 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
       s_dr[m][ri] = drifts_p(s_best[m][ri], qt, pos16, R.rbase, R.rfn, R.plo, R.phi, k);
     }
   }
-  __syncthreads();
+  cover_barrier();
   // ---- coverage: wave m = member m, lane l = windows 64 l .. 64 l + 63
   const int m = __builtin_amdgcn_readfirstlane(t >> 6), l = t & 63;
   long long rs = mrs[0], rn = mrn[0];
@@ -1339,19 +1366,11 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
   if ((dm0 >> m) & 1u) {
     const long long p0 = rs + qt - 1, wb = (p0 >> 4) + 4 * l;
     const int sh2 = 2 * (int)(p0 & 15);
-    uint32_t M[LW];
-#pragma unroll
-    for (int i = 0; i < LW; ++i) M[i] = p2_word(p2, wb + i, n_p2);
-    {
-      // exception bytes of words wb .. wb + 6 (three aligned dwords around them)
-      const long long a = wb & ~3ll;
-      uint32_t e = 0;
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-        if (a + 4 * i >= 0 && (uint64_t)(a + 4 * i + 4) <= n_p2 + 16) e |= *reinterpret_cast<const uint32_t*>(e16 + a + 4 * i);
-      (void)PG_BOK(wb + LW <= (long long)n_p2 + 4 || wb > (long long)n_p2, 11, wb, n_p2);
-      mex = e != 0u;
-    }
+    // (M: the lane's words wb .. wb + 6, eex: the exception bytes of the three
+    // aligned dwords around them, both loaded at the start)
+    (void)PG_BOK(wb + LW <= (long long)n_p2 + 4 || wb > (long long)n_p2, 11, wb, n_p2);
+    (void)wb;
+    mex = eex != 0u;
     const int L = k + 2;                           // context bases of a window
     const int P = L >= 16 ? 16 : L >= 8 ? 8 : L >= 4 ? 4 : 2;
     const uint32_t rsh = 2u * (uint32_t)(L - P);
@@ -1450,7 +1469,7 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
     s_qbase = nwork ? atomicAdd(qcount + QSTRIDE * sub, (unsigned long long)nwork) : 0ull;
     (void)PG_BOK(nwork <= QM * CBLOCK && s_qbase + nwork <= qcap, 42, (long long)nwork, (long long)s_qbase);
   }
-  __syncthreads();
+  cover_barrier();
 #pragma unroll
   for (int s = 0; s < 4; ++s)
     if ((wmask >> s) & 1u) {
