@@ -42,6 +42,7 @@ for step in "$@"; do
     abchunks) run ab_chunks 900 python -u tools/ab_k3.py --steps 10 --tune base --tune K3_HEAD=8 --tune K3_HEAD=8,K3_TAIL=6 --tune K3_CHUNKS=4,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=4 --tune K3_CHUNKS=5,K3_HEAD=6,K3_TAIL=6 --tune K3_CHUNKS=2 ;;
     npz) run pytest_npz 600 python -u -m pytest tests/test_gpu_npz.py -x -v --timeout 300 --timeout-method thread ;;
     savebd) run save_bd 300 python -u tools/save_breakdown.py ;;
+    findfr) run findfr 300 python -u tools/findfr_breakdown.py ;;
     tracewin) run trace_win 300 rocprofv3 --kernel-trace --memory-copy-trace -d gpurun_out/tw -o run --output-format csv -- python tools/ab_k3.py --host --steps 3 --tune base ;;
     abfin) run ab_fin 600 python -u tools/ab_k3.py --host --alt --steps 16 --tune base --tune base --env PG_EXP_FINISH_EARLY= --env PG_EXP_FINISH_EARLY=1 ;;
     c5diag) run c5_diag 900 env C5_DIAG=1 python -u tools/c5_forms.py 0:30 0:30 0:30 ;;
