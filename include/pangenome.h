@@ -185,6 +185,13 @@ int pg_edges_export(pg_ctx* ctx, uint64_t* tuples, int64_t* counts, int64_t* fir
  * first-occurrence order (seq2graph :1893-1904), formatted on the device.
  * out == NULL: only *n_bytes (the size) is set; otherwise cap >= that size. */
 int pg_edges_format(pg_ctx* ctx, char* out, uint64_t cap, uint64_t* n_bytes);
+/* The same text written to descriptor fd at its position, which then follows
+ * it (the reference writes it to `<qry>_rdbg_weight.xyz`, :1893-1904): a
+ * regular file opened without O_APPEND takes 16 MiB pieces in parallel
+ * (pwrite from per-thread pinned buffers), anything else in order (write).
+ * *n_bytes = the bytes written.  Host-side buffered writers on fd must be
+ * flushed first. */
+int pg_edges_format_fd(pg_ctx* ctx, int fd, uint64_t* n_bytes);
 
 /* seq2graph's label dictionary (kmer_numba.py:1918-1944) built on the device:
  * the `.mcl` entries (key, value) -> line index as the host's dict holds them
@@ -215,6 +222,10 @@ int pg_rows_export(pg_ctx* ctx, int64_t* rows5, uint64_t cap);
  * offsets).  out == NULL: only *n_bytes is set. */
 int pg_rows_format(pg_ctx* ctx, const char* names, const int64_t* name_off, uint64_t n_names, char* out, uint64_t cap,
                    uint64_t* n_bytes);
+/* The same text written to descriptor fd (the reference prints it to
+ * stdout, :1946-1949), as pg_edges_format_fd writes. */
+int pg_rows_format_fd(pg_ctx* ctx, const char* names, const int64_t* name_off, uint64_t n_names, int fd,
+                      uint64_t* n_bytes);
 
 /* ---- text output (host only; no context).  The reference formats these in
  *      Python loops (kmer_numba.py:1893-1904, :1946-1949).

@@ -77,9 +77,11 @@ SIGNATURES = {
     "pg_rows": (C.c_int, [_P, _P, C.c_int, _U64P]),
     "pg_rows_export": (C.c_int, [_P, _P, C.c_uint64]),
     "pg_edges_format": (C.c_int, [_P, _P, C.c_uint64, _U64P]),
+    "pg_edges_format_fd": (C.c_int, [_P, C.c_int, _U64P]),
     "pg_labels_from_edges": (C.c_int, [_P, _P, C.c_uint64, _P, _P, _P, C.c_uint64, C.c_int64, _U64P]),
     "pg_labels_export": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_rows_format": (C.c_int, [_P, _P, _P, C.c_uint64, _P, C.c_uint64, _U64P]),
+    "pg_rows_format_fd": (C.c_int, [_P, _P, _P, C.c_uint64, C.c_int, _U64P]),
     "pg_get_stats": (C.c_int, [_P, _SP]),
     "pg_tune": (C.c_int, [_P, C.c_int, C.c_int64]),
     "pg_dbg_dump": (C.c_int, [_P, _U64P, _P, _P, _P, _U64P]),
@@ -357,6 +359,14 @@ class Context:
         check(self.lib.pg_edges_format(self.h, ptr(buf), buf.shape[0], C.byref(n)), "pg_edges_format")
         return buf[:n.value].tobytes()
 
+    def edges_write(self, fd: int) -> int:
+        """edges_text() written straight to descriptor fd at its position
+        (pg_edges_format_fd: pinned pieces, parallel pwrite into a regular
+        file); flush any buffered writer on fd first.  Returns the bytes."""
+        n = C.c_uint64()
+        check(self.lib.pg_edges_format_fd(self.h, int(fd), C.byref(n)), "pg_edges_format_fd")
+        return n.value
+
     def labels_from_edges(self, tuples=None, mcl_keys=None, mcl_vals=None, mcl_ids=None, next_label: int = 0):
         """seq2graph's label table on the device (pg_labels_from_edges): the
         .mcl entries, then the .xyz nodes in first-appearance order.  tuples
@@ -416,6 +426,19 @@ class Context:
         check(self.lib.pg_rows_format(self.h, ptr(nb), ptr(off), len(names), ptr(buf), buf.shape[0], C.byref(n)),
               "pg_rows_format")
         return buf[:n.value].tobytes()
+
+    def rows_write(self, names: list, fd: int) -> int:
+        """rows_text(names) written straight to descriptor fd at its position
+        (pg_rows_format_fd); flush any buffered writer on fd first."""
+        blob = b"".join(names)
+        off = np.zeros(len(names) + 1, np.int64)
+        if names:
+            off[1:] = np.cumsum([len(x) for x in names])
+        nb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
+        n = C.c_uint64()
+        check(self.lib.pg_rows_format_fd(self.h, ptr(nb), ptr(off), len(names), int(fd), C.byref(n)),
+              "pg_rows_format_fd")
+        return n.value
 
     def rows(self, rec_flags=None, rc1: bool = False):
         n = C.c_uint64()

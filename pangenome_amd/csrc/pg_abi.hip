@@ -482,6 +482,14 @@ int pg_edges_format(pg_ctx* x, char* out, uint64_t cap, uint64_t* n_bytes) {
   });
 }
 
+int pg_edges_format_fd(pg_ctx* x, int fd, uint64_t* n_bytes) {
+  return guard([&] {
+    if (!x || !n_bytes || fd < 0) throw pg::Error(PG_EINVAL, "pg_edges_format_fd: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    *n_bytes = pg::format_edges(x->c, nullptr, 0, fd);
+  });
+}
+
 int pg_labels_from_edges(pg_ctx* x, const uint64_t* tuples, uint64_t n_edges, const int64_t* mcl_key,
                          const int64_t* mcl_value, const int64_t* mcl_label, uint64_t n_mcl, int64_t next_label,
                          uint64_t* n_labels) {
@@ -509,6 +517,16 @@ int pg_rows_format(pg_ctx* x, const char* names, const int64_t* name_off, uint64
     PG_HIP(hipSetDevice(x->c.device));
     if (n_names < x->c.n_records) throw pg::Error(PG_EINVAL, "pg_rows_format: fewer names than records");
     *n_bytes = pg::format_rows_text(x->c, names, name_off, n_names, out, cap);
+  });
+}
+
+int pg_rows_format_fd(pg_ctx* x, const char* names, const int64_t* name_off, uint64_t n_names, int fd,
+                      uint64_t* n_bytes) {
+  return guard([&] {
+    if (!x || !n_bytes || !name_off || fd < 0) throw pg::Error(PG_EINVAL, "pg_rows_format_fd: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    if (n_names < x->c.n_records) throw pg::Error(PG_EINVAL, "pg_rows_format_fd: fewer names than records");
+    *n_bytes = pg::format_rows_text(x->c, names, name_off, n_names, nullptr, 0, fd);
   });
 }
 

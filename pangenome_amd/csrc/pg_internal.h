@@ -342,6 +342,8 @@ struct PreEnt {                   // one staged oakht slot: oriented key, 12-bit
 void dbg_load(Ctx& c, const uint64_t* keys, const uint16_t* masks, const uint8_t* counts, uint64_t n);
 uint64_t dbg_dump(Ctx& c, uint64_t& capacity, uint64_t* keys, uint16_t* values, uint8_t* counts);
 uint64_t dbg_dump_fd(Ctx& c, uint64_t& capacity, int fd, const uint64_t* off, uint32_t* crc);
+// n device bytes to descriptor fd at its position (pg_edges_format_fd, pg_rows_format_fd)
+void text_to_fd(Ctx& c, const uint8_t* src, uint64_t n, int fd, const char* what);
 uint64_t oakht_capacity(uint64_t size);
 // pg_walk.hip
 uint64_t walk_edges(Ctx& c, const uint8_t* h_rec_flag, int rc1);
@@ -349,12 +351,12 @@ void export_edges(Ctx& c, uint64_t* tuples, int64_t* counts, int64_t* first_walk
 void set_labels(Ctx& c, const int64_t* key, const int64_t* val, const int64_t* id, uint64_t n);
 uint64_t walk_rows(Ctx& c, const uint8_t* h_rec_flag, int rc1);
 void export_rows(Ctx& c, int64_t* rows5, uint64_t cap);
-uint64_t format_edges(Ctx& c, char* out, uint64_t cap);
+uint64_t format_edges(Ctx& c, char* out, uint64_t cap, int fd = -1);
 uint64_t labels_from_edges(Ctx& c, const uint64_t* h_tuples, uint64_t n_edges, const int64_t* mk, const int64_t* mv,
                            const int64_t* mi, uint64_t n_mcl, int64_t next_id);
 void export_labels(Ctx& c, int64_t* key, int64_t* val, int64_t* id, uint64_t cap);
 uint64_t format_rows_text(Ctx& c, const char* names, const int64_t* name_off, uint64_t n_names, char* out,
-                          uint64_t cap);
+                          uint64_t cap, int fd = -1);
 
 // helpers
 inline uint64_t next_pow2(uint64_t x) {

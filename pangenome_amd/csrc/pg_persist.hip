@@ -13,11 +13,14 @@
 //       mod capacity, then j, j+1, j+4, j+9, ... .  Any insertion order gives a
 //       layout lookups accept: a key's earlier probes were occupied when it
 //       was placed and nothing is ever removed.
+#include <fcntl.h>
+#include <sys/stat.h>
 #include <unistd.h>
 #include <zlib.h>
 
 #include <atomic>
 #include <cerrno>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -325,33 +328,46 @@ uint64_t dbg_dump(Ctx& c, uint64_t& capacity, uint64_t* keys, uint16_t* values, 
   return c.dump_size;
 }
 
-// dump() straight into a file: the slot arrays go from the device to `fd` at
-// off[0..2] (keys, values, counts) in DUMP_PIECE pieces, each piece through a
-// worker thread's own pinned buffer and stream (copy, CRC-32, pwrite), so the
-// copies, the CRCs and the page-cache writes of different pieces overlap and
-// no host array of the whole table is ever allocated (C3: 886 MB; C4: ~5 GB).
-constexpr uint64_t DUMP_PIECE = 16ull << 20;
-uint64_t dbg_dump_fd(Ctx& c, uint64_t& capacity, int fd, const uint64_t* off, uint32_t* crc) {
-  const uint64_t M = dump_capacity(c, capacity);
-  if (fd < 0) return c.dump_size;
-  if (!off || !crc) throw Error(-22, "pg_dbg_dump_fd: offsets and crcs are required with a descriptor");
-  DumpSlots d;
-  dump_place(c, M, d);
-  const uint8_t* src[3] = {d.ok.as<uint8_t>(), d.ov.as<uint8_t>(), d.oc.as<uint8_t>()};
-  const uint64_t len[3] = {8 * M, 2 * M, M};
+// Device bytes to a descriptor: member m (src[m], len[m] bytes) in
+// FD_PIECE pieces, each piece through a worker thread's own pinned buffer
+// and stream, so the copies, the CRCs and the page-cache writes of different
+// pieces overlap and no host array of the whole member is ever allocated.
+// pos: the file offset of each member (pwrite, pieces landing in any order),
+// or nullptr: the members in order at the descriptor's position (write, each
+// piece waiting for the one before it: pipes, terminals, O_APPEND files).
+// crc: each member's CRC-32, or nullptr.
+constexpr uint64_t FD_PIECE = 16ull << 20;
+static void stream_to_fd(Ctx& c, int nm, const uint8_t* const* src, const uint64_t* len, int fd,
+                         const uint64_t* pos, uint32_t* crc, const char* what) {
   struct Piece { int m; uint64_t at, n; };
   std::vector<Piece> jobs;
-  for (int m = 0; m < 3; ++m)
-    for (uint64_t a = 0; a < len[m]; a += DUMP_PIECE) jobs.push_back(Piece{m, a, std::min(DUMP_PIECE, len[m] - a)});
+  for (int m = 0; m < nm; ++m)
+    for (uint64_t a = 0; a < len[m]; a += FD_PIECE) jobs.push_back(Piece{m, a, std::min(FD_PIECE, len[m] - a)});
+  if (jobs.empty()) {
+    for (int m = 0; crc && m < nm; ++m) crc[m] = 0u;
+    return;
+  }
   std::vector<uint32_t> pc(jobs.size(), 0u);
   std::atomic<size_t> next{0};
   std::atomic<bool> bad{false};
-  std::mutex em;
+  std::mutex em, om;
+  std::condition_variable ocv;
+  size_t turn = 0;                                     // (ordered writes) the piece whose write is next
   std::string err;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const size_t nt = std::min<size_t>(std::min<size_t>(16, hw), jobs.size());
   if (c.dump_pin.size() < nt) c.dump_pin.resize(nt);
-  for (size_t t = 0; t < nt; ++t) c.dump_pin[t].reserve(DUMP_PIECE);
+  for (size_t t = 0; t < nt; ++t) c.dump_pin[t].reserve(FD_PIECE);
+  auto put = [&](const uint8_t* b, uint64_t n, int64_t at) {
+    for (uint64_t w = 0; w < n;) {
+      const ssize_t r = at >= 0 ? pwrite(fd, b + w, n - w, (off_t)(at + (int64_t)w)) : write(fd, b + w, n - w);
+      if (r < 0) {
+        if (errno == EINTR) continue;
+        throw Error(-5, std::string(what) + ": write failed: " + std::strerror(errno));
+      }
+      w += (uint64_t)r;
+    }
+  };
   auto worker = [&](size_t t) {
     hipStream_t st = nullptr;
     try {
@@ -362,19 +378,30 @@ uint64_t dbg_dump_fd(Ctx& c, uint64_t& capacity, int fd, const uint64_t* off, ui
         const Piece& p = jobs[j];
         PG_HIP(hipMemcpyAsync(buf, src[p.m] + p.at, p.n, hipMemcpyDeviceToHost, st));
         PG_HIP(hipStreamSynchronize(st));
-        pc[j] = (uint32_t)crc32(0ul, buf, (uInt)p.n);
-        for (uint64_t w = 0; w < p.n;) {
-          const ssize_t r = pwrite(fd, buf + w, p.n - w, (off_t)(off[p.m] + p.at + w));
-          if (r < 0) {
-            if (errno == EINTR) continue;
-            throw Error(-5, std::string("pg_dbg_dump_fd: write failed: ") + std::strerror(errno));
-          }
-          w += (uint64_t)r;
+        if (crc) pc[j] = (uint32_t)crc32(0ul, buf, (uInt)p.n);
+        if (pos) {
+          put(buf, p.n, (int64_t)(pos[p.m] + p.at));
+          continue;
         }
+        {
+          std::unique_lock<std::mutex> lk(om);      // (pieces are claimed in order, so the lowest
+          ocv.wait(lk, [&] { return turn == j || bad.load(); });   // unwritten one never waits)
+        }
+        if (bad) break;
+        put(buf, p.n, -1);
+        {
+          std::lock_guard<std::mutex> lk(om);
+          ++turn;
+        }
+        ocv.notify_all();
       }
     } catch (const std::exception& e) {
-      std::lock_guard<std::mutex> g(em);
-      if (!bad.exchange(true)) err = e.what();
+      {
+        std::lock_guard<std::mutex> g(em);
+        if (!bad.exchange(true)) err = e.what();
+      }
+      std::lock_guard<std::mutex> lk(om);
+      ocv.notify_all();
     }
     if (st) (void)hipStreamDestroy(st);
   };
@@ -383,14 +410,47 @@ uint64_t dbg_dump_fd(Ctx& c, uint64_t& capacity, int fd, const uint64_t* off, ui
   worker(0);
   for (auto& x : th) x.join();
   if (bad) throw Error(-5, err);
-  for (int m = 0; m < 3; ++m) crc[m] = 0u;
-  std::vector<bool> first(3, true);
+  if (!crc) return;
+  for (int m = 0; m < nm; ++m) crc[m] = 0u;
+  std::vector<bool> first(nm, true);
   for (size_t j = 0; j < jobs.size(); ++j) {          // pieces are in member order, ascending
     const int m = jobs[j].m;
     crc[m] = first[m] ? pc[j] : (uint32_t)crc32_combine(crc[m], pc[j], (z_off_t)jobs[j].n);
     first[m] = false;
   }
+}
+
+// dump() straight into a file: the slot arrays (keys, values, counts) at
+// off[0..2], their CRC-32s in crc[0..2] (C3: 886 MB; C4: ~5 GB, never in a
+// host array)
+uint64_t dbg_dump_fd(Ctx& c, uint64_t& capacity, int fd, const uint64_t* off, uint32_t* crc) {
+  const uint64_t M = dump_capacity(c, capacity);
+  if (fd < 0) return c.dump_size;
+  if (!off || !crc) throw Error(-22, "pg_dbg_dump_fd: offsets and crcs are required with a descriptor");
+  DumpSlots d;
+  dump_place(c, M, d);
+  const uint8_t* src[3] = {d.ok.as<uint8_t>(), d.ov.as<uint8_t>(), d.oc.as<uint8_t>()};
+  const uint64_t len[3] = {8 * M, 2 * M, M};
+  stream_to_fd(c, 3, src, len, fd, off, crc, "pg_dbg_dump_fd");
   return c.dump_size;
+}
+
+// n device bytes written to fd at its position, which then follows them: a
+// regular file opened without O_APPEND takes the pieces in parallel
+// (pwrite), anything else in order
+void text_to_fd(Ctx& c, const uint8_t* src, uint64_t n, int fd, const char* what) {
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) throw Error(-9, std::string(what) + ": bad descriptor: " + std::strerror(errno));
+  const int fl = fcntl(fd, F_GETFL);
+  const off_t cur = lseek(fd, 0, SEEK_CUR);
+  if (S_ISREG(sb.st_mode) && fl >= 0 && !(fl & O_APPEND) && cur >= 0) {
+    const uint64_t at = (uint64_t)cur;
+    stream_to_fd(c, 1, &src, &n, fd, &at, nullptr, what);
+    if (lseek(fd, cur + (off_t)n, SEEK_SET) < 0)
+      throw Error(-5, std::string(what) + ": seek failed: " + std::strerror(errno));
+  } else {
+    stream_to_fd(c, 1, &src, &n, fd, nullptr, nullptr, what);
+  }
 }
 
 }  // namespace pg

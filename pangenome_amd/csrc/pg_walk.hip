@@ -837,8 +837,9 @@ void export_edges(Ctx& c, uint64_t* tuples, int64_t* counts, int64_t* first_walk
   c.sync();
 }
 
-// the .xyz text of the last edge pass, in first-occurrence order
-uint64_t format_edges(Ctx& c, char* out, uint64_t cap) {
+// the .xyz text of the last edge pass, in first-occurrence order: its size
+// (out null, fd < 0), copied into out, or written to descriptor fd
+uint64_t format_edges(Ctx& c, char* out, uint64_t cap, int fd) {
   const uint64_t n = c.n_edges;
   if (!c.text_xyz) {
     c.text_len.reserve(8 * (n + 1));
@@ -854,8 +855,8 @@ uint64_t format_edges(Ctx& c, char* out, uint64_t cap) {
     c.text_xyz = true;
     c.text_rows = false;
   }
-  if (!out) return c.text_total;
-  if (cap < c.text_total) throw Error(-34, "pg_edges_format: buffer too small");
+  if (!out && fd < 0) return c.text_total;
+  if (out && cap < c.text_total) throw Error(-34, "pg_edges_format: buffer too small");
   if (n) {
     c.text_buf.reserve(c.text_total + 16);
     const auto* tup = c.edge_exp.as<unsigned long long>();
@@ -863,8 +864,9 @@ uint64_t format_edges(Ctx& c, char* out, uint64_t cap) {
     hipLaunchKernelGGL(k_xyz_write, dim3(grid_for(n, 256, 8192)), dim3(256), 0, c.stream, tup, ecnt, n,
                        c.text_off.as<unsigned long long>(), c.text_buf.as<char>());
     PG_HIP(hipGetLastError());
-    PG_HIP(hipMemcpyAsync(out, c.text_buf.p, c.text_total, hipMemcpyDeviceToHost, c.stream));
+    if (out) PG_HIP(hipMemcpyAsync(out, c.text_buf.p, c.text_total, hipMemcpyDeviceToHost, c.stream));
     c.sync();
+    if (!out) text_to_fd(c, c.text_buf.as<uint8_t>(), c.text_total, fd, "pg_edges_format_fd");
   }
   return c.text_total;
 }
@@ -1059,9 +1061,10 @@ void export_rows(Ctx& c, int64_t* rows5, uint64_t cap) {
 }
 
 // the region rows' text of the last row pass; names[name_off[r] ..
-// name_off[r+1]) is record r's qid (R + 1 offsets)
+// name_off[r+1]) is record r's qid (R + 1 offsets).  Its size (out null,
+// fd < 0), copied into out, or written to descriptor fd.
 uint64_t format_rows_text(Ctx& c, const char* names, const int64_t* name_off, uint64_t n_names, char* out,
-                          uint64_t cap) {
+                          uint64_t cap, int fd) {
   const uint64_t n = c.n_rows;
   if (!c.text_rows) {
     c.text_names.reserve(8 * (n_names + 1) + (uint64_t)std::max<int64_t>(name_off[n_names], 0) + 16);
@@ -1081,8 +1084,8 @@ uint64_t format_rows_text(Ctx& c, const char* names, const int64_t* name_off, ui
     c.text_rows = true;
     c.text_xyz = false;
   }
-  if (!out) return c.text_total;
-  if (cap < c.text_total) throw Error(-34, "pg_rows_format: buffer too small");
+  if (!out && fd < 0) return c.text_total;
+  if (out && cap < c.text_total) throw Error(-34, "pg_rows_format: buffer too small");
   if (n) {
     const long long* d_off = c.text_names.as<long long>();
     const char* d_names = reinterpret_cast<const char*>(d_off + n_names + 1);
@@ -1091,8 +1094,9 @@ uint64_t format_rows_text(Ctx& c, const char* names, const int64_t* name_off, ui
                        c.rows_buf.as<long long>(), n, d_names, d_off, c.text_off.as<unsigned long long>(),
                        c.text_buf.as<char>());
     PG_HIP(hipGetLastError());
-    PG_HIP(hipMemcpyAsync(out, c.text_buf.p, c.text_total, hipMemcpyDeviceToHost, c.stream));
+    if (out) PG_HIP(hipMemcpyAsync(out, c.text_buf.p, c.text_total, hipMemcpyDeviceToHost, c.stream));
     c.sync();
+    if (!out) text_to_fd(c, c.text_buf.as<uint8_t>(), c.text_total, fd, "pg_rows_format_fd");
   }
   return c.text_total;
 }

@@ -258,7 +258,11 @@ def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_
     res = rdbg_edges(g, Ns, chunk, rc, brkpt=brkpt, keep_on_device=True)
     oname = qry + "_rdbg_weight.xyz"
     with open(oname, "wb") as f:                      # "%d_%d\t%d_%d\t%d\n" (:1893-1904)
-        f.write(g.ctx.edges_text() if res is None else format_xyz(*res))
+        if res is None:
+            f.flush()
+            g.ctx.edges_write(f.fileno())             # formatted on the device, streamed into the file
+        else:
+            f.write(format_xyz(*res))
     if cluster:
         if os.path.isfile("%s.mcl" % oname):
             print("# the mcl has been ran", file=out)
@@ -272,16 +276,31 @@ def seq2graph(qry, kmer=13, bits=5, Ns=1e6, brkpt="./breakpoint_rdbg.npz", rdbg_
     flags = host.plan_rows(g.seq_len, g.shape, g.buf, int(Ns))
     g.ctx.rows_count(flags, bool(rc))
     names = [bytes(g.buf[int(hs) + 1:int(hs) + int(hl)]) for hs, hl in zip(g.hdr_start, g.hdr_len)]
-    text = g.ctx.rows_text(names)                     # print('%s\t%d\t%d\t%s\t%d') (:1946-1949)
-    if text:
-        if hasattr(out, "buffer"):
-            out.flush()
-            out.buffer.write(text)
-            out.buffer.flush()
-        else:
-            out.write(text.decode())
+    fd = _fileno(out)                                 # print('%s\t%d\t%d\t%s\t%d') (:1946-1949)
+    if fd is not None:
+        out.flush()
+        out.buffer.flush()
+        g.ctx.rows_write(names, fd)                   # formatted on the device, streamed to the descriptor
+    else:
+        text = g.ctx.rows_text(names)
+        if text:
+            if hasattr(out, "buffer"):
+                out.flush()
+                out.buffer.write(text)
+                out.buffer.flush()
+            else:
+                out.write(text.decode())
     gen = g.ctx.label_gen
     return LabelTable(loader=lambda: g.ctx.labels(gen))           # (raises once a later label pass replaced it)
+
+
+def _fileno(out):
+    """The descriptor under a text stream's binary buffer (stdout, a file),
+    or None (a stand-in with no descriptor)."""
+    try:
+        return out.buffer.fileno()
+    except (AttributeError, OSError, ValueError):   # (io.UnsupportedOperation is an OSError)
+        return None
 
 
 # ---------------------------------------------------------------------- CLI

@@ -62,6 +62,48 @@ def test_cli_entry_point(km, tmp_path):
     assert rows_of(text) == fx.rows
 
 
+@pytest.mark.parametrize("sink", ["file", "append", "pipe"])
+def test_cli_rows_to_descriptor(km, tmp_path, sink):
+    """stdout with a descriptor under it: the rows go straight from the device
+    to it (pg_rows_format_fd) - a regular file in parallel pieces at its
+    position, an O_APPEND file and a pipe in order - between the `#` lines
+    printed before and after them, as the StringIO path prints them."""
+    import threading
+    fx = Fixture("pan8_k27_c3")
+    q = tmp_path / "in.fa"
+    q.write_bytes(fx.fasta)
+    (tmp_path / "in.fa_rdbg_weight.xyz.mcl").write_text("")
+    argv = ["kmer_numba.py", "-i", str(q), "-k27", "-c", "3"]
+    ref = io.StringIO()
+    km.entry_point(argv, out=ref)
+    xyz_ref = (tmp_path / "in.fa_rdbg_weight.xyz").read_bytes()
+
+    def shape(text):                                  # the text without its timings
+        return [ln for ln in text.split("\n") if not ln.startswith("# finished in")]
+
+    if sink == "pipe":
+        r, w = os.pipe()
+        got = []
+        th = threading.Thread(target=lambda: got.append(os.fdopen(r, "rb").read()))
+        th.start()
+        with os.fdopen(w, "w") as out:
+            out.write("# before\n")
+            km.entry_point(argv, out=out)
+        th.join()
+        text = got[0].decode()
+    else:
+        fn = tmp_path / "out.txt"
+        fn.write_text("# before\n")
+        with open(fn, "a" if sink == "append" else "r+") as out:
+            out.seek(0, os.SEEK_END)
+            km.entry_point(argv, out=out)
+        text = fn.read_text()
+    assert text.startswith("# before\n")
+    assert shape(text[len("# before\n"):]) == shape(ref.getvalue())
+    assert rows_of(text) == fx.rows
+    assert (tmp_path / "in.fa_rdbg_weight.xyz").read_bytes() == xyz_ref
+
+
 def _random_fasta(rng, n_rec, k):
     """Random records exercising every length class around k and odd bytes."""
     alphabet = np.frombuffer(b"ACGTACGTACGTACGTacgtNnRY$#", dtype=np.uint8)

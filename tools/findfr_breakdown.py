@@ -60,6 +60,21 @@ def main():
         out = io.BytesIO()
         out.write(text)
         t = tick("rows_sink_ms", t)
+        with open(oname, "wb") as f:
+            g.ctx.edges_write(f.fileno())
+        t = tick("xyz_fd_ms", t)
+        with open(os.path.join(d, "rows.txt"), "wb") as f:
+            g.ctx.rows_write(names, f.fileno())
+        t = tick("rows_fd_ms", t)
+        r, w = os.pipe()
+        import threading
+        th = threading.Thread(target=lambda: [None for _ in iter(lambda: os.read(r, 1 << 20), b"")])
+        th.start()
+        g.ctx.rows_write(names, w)
+        os.close(w)
+        th.join()
+        os.close(r)
+        t = tick("rows_pipe_ms", t)
         res.update(n_rows=int(n_rows), rows_bytes=len(text), xyz_bytes=len(xyz))
         del text, out, xyz
     print(json.dumps(res), flush=True)
