@@ -1407,8 +1407,10 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
           constexpr int w = decltype(W)::value;
 #pragma unroll
           for (int i = 0; i < LW; ++i) {
-            const uint32_t x = M[i] ^ __builtin_amdgcn_alignbit(raw[w + i + 1], raw[w + i], bs);
-            Z[i] = (x | (x >> 1)) & 0x55555555u;   // even bit of each base: mismatch
+            // both bits of each base, differing where it mismatches: the smear
+            // below moves bits by even counts only, so a base's two bits stay
+            // apart until S folds them onto its even bit
+            Z[i] = M[i] ^ __builtin_amdgcn_alignbit(raw[w + i + 1], raw[w + i], bs);
           }
         };
         switch (__builtin_amdgcn_readfirstlane(iw & 3)) {
@@ -1431,7 +1433,8 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const int rel = 64 * l + 16 * s;
-          const uint32_t S = T[s] | __builtin_amdgcn_alignbit(T[s + 1], T[s], rsh);
+          const uint32_t S2 = T[s] | __builtin_amdgcn_alignbit(T[s + 1], T[s], rsh);
+          const uint32_t S = S2 | (S2 >> 1);         // even bit of each window: any mismatch in it
           covS[s] |= (rel >= lo && rel <= hi) ? ~S & 0x55555555u : 0u;
 #ifdef PG_DEBUG_BOUNDS
           {                                        // every window this drift covers, against the class bytes
