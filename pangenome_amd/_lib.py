@@ -135,6 +135,16 @@ def ptr(a: np.ndarray | None):
     return None if a is None else C.c_void_p(a.ctypes.data)
 
 
+def _names_blob(names: list):
+    """Record names as pg_rows_format takes them: one byte blob and R + 1
+    offsets."""
+    blob = b"".join(names)
+    off = np.zeros(len(names) + 1, np.int64)
+    if names:
+        off[1:] = np.cumsum([len(x) for x in names])
+    return (np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)), off
+
+
 class Context:
     """One pg_ctx: one HIP device, one stream, all device buffers."""
 
@@ -415,11 +425,7 @@ class Context:
     def rows_text(self, names: list) -> bytes:
         """The region rows' text of the last pg_rows, formatted on the device
         (pg_rows_format); names[r] = record r's qid."""
-        blob = b"".join(names)
-        off = np.zeros(len(names) + 1, np.int64)
-        if names:
-            off[1:] = np.cumsum([len(x) for x in names])
-        nb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
+        nb, off = _names_blob(names)
         n = C.c_uint64()
         check(self.lib.pg_rows_format(self.h, ptr(nb), ptr(off), len(names), None, 0, C.byref(n)), "pg_rows_format")
         buf = np.empty(max(n.value, 1), np.uint8)
@@ -430,11 +436,7 @@ class Context:
     def rows_write(self, names: list, fd: int) -> int:
         """rows_text(names) written straight to descriptor fd at its position
         (pg_rows_format_fd); flush any buffered writer on fd first."""
-        blob = b"".join(names)
-        off = np.zeros(len(names) + 1, np.int64)
-        if names:
-            off[1:] = np.cumsum([len(x) for x in names])
-        nb = np.frombuffer(blob, np.uint8) if blob else np.zeros(1, np.uint8)
+        nb, off = _names_blob(names)
         n = C.c_uint64()
         check(self.lib.pg_rows_format_fd(self.h, ptr(nb), ptr(off), len(names), int(fd), C.byref(n)),
               "pg_rows_format_fd")
