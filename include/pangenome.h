@@ -161,15 +161,29 @@ int pg_dbg_load(pg_ctx* ctx, const uint64_t* keys, const uint16_t* masks, const 
 uint64_t pg_oakht_capacity(uint64_t size);
 
 /* ---- multi-GPU exchange (one process per GPU; the caller moves the bytes
- *      with RCCL).  Replaces nothing in the reference, which is single-core. */
+ *      with RCCL).  Replaces nothing in the reference, which is single-core.
+ *      Device pointers the caller passes (d_out, d_records, d_rows) must be
+ *      ready when the call is made: the library's streams do not wait on the
+ *      caller's (synchronise the caller's streams first). */
 /* Owner-partition this rank's local dBG into `nparts` contiguous runs of
  * 16-byte records (d_out device buffer, capacity out_cap records).
  * counts[nparts] receives run lengths; d_out == NULL only counts. */
 int pg_dbg_partition(pg_ctx* ctx, int nparts, void* d_out, uint64_t out_cap, uint64_t* counts);
+/* Integrity sums of the last pg_dbg_partition scatter: sums[i] = the sum
+ * mod 2^64 of a 64-bit hash of each 16-byte record of run i (the hash is
+ * row_check in pangenome_amd/csrc/pg_common.h; order-free, so the
+ * receiver's pg_rows_checksum of the same records must equal it). */
+int pg_dbg_partition_sums(pg_ctx* ctx, int nparts, uint64_t* sums);
+/* The same sums over nseg segments of 16-byte records at device address
+ * d_rows: segment s = records [seg_off[s], seg_off[s+1]). */
+int pg_rows_checksum(pg_ctx* ctx, const void* d_rows, const uint64_t* seg_off, uint64_t nseg, uint64_t* sums);
 /* OR-merge received 16-byte records (device pointer) into a fresh owner
  * table (the rdBG of the owner's keys is built with it); sentinel != 0 adds
  * the n<k key.  capacity_hint is ignored (the table is sized exactly). */
 int pg_dbg_merge(pg_ctx* ctx, const void* d_records, uint64_t n, uint64_t capacity_hint, int sentinel);
+/* What the last pg_dbg_merge read: non-empty records and the sum of their
+ * hashes (pg_dbg_partition_sums' hash over all n records). */
+int pg_dbg_merge_check(const pg_ctx* ctx, uint64_t* rows, uint64_t* sum);
 
 /* ---- edge pass: rdbg_edge_weight_jit_ (kmer_numba.py:1808-1827) ->
  *      rdbg_edge_weight (:1446-1518).  rec_flags as above (walked records);
@@ -302,6 +316,11 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * and the peak it restarts are shared by every context of the process (and
  * every device).  For tests of a path's memory budget at a scaled-down size. */
 #define PG_TUNE_DEVICE_CAP 9
+/* PG_TUNE_POISON (debug, PROCESS-WIDE like PG_TUNE_DEVICE_CAP): every device
+ * buffer the library allocates from now on is filled with this byte value
+ * (0..255; -1, the default, = off), so that a kernel reading memory nothing
+ * wrote gives a different result instead of inheriting an earlier run's. */
+#define PG_TUNE_POISON 17
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Device bytes the library's buffers hold in this process now (peak == 0)

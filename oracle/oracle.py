@@ -52,6 +52,10 @@ def lib():
         L.pgo_get_rows.argtypes = [P, P]
         L.pgo_set_rdbg.argtypes = [P, P, i64]
         L.pgo_free.argtypes = [P]
+        L.pgo_dbg_range.argtypes = [u8p, i64, i32, i32, i64, i32, i64, C.c_uint64, C.c_uint64,
+                                    C.POINTER(P), C.POINTER(P)]
+        L.pgo_dbg_range.restype = i64
+        L.pgo_free_buf.argtypes = [P]
         _lib = L
     return _lib
 
@@ -159,6 +163,43 @@ class OracleRun:
             qid = self.fasta[hst:hst + hlen].decode()[1:]
             lines.append("%s\t%d\t%d\t%s\t%d" % (qid, s, e, "+" if strand == 1 else "-", lab))
         return lines
+
+
+def dbg_range(fasta, k: int, c: int, lo: int, hi: int, ns=None, dbg_chunk: int = CHUNK):
+    """The dBG entries with keys in [lo, hi) (hi = 2**64 - 1 includes the n<k
+    sentinel), sorted by key: pgo_dbg_range, the same pass as OracleRun with
+    a sort instead of the oakht (inputs too large for one in-memory table are
+    digested range by range).  `fasta`: bytes or a uint8 array (np.memmap)."""
+    arr = np.frombuffer(fasta, dtype=np.uint8) if not isinstance(fasta, np.ndarray) else fasta
+    kp, mp = C.c_void_p(), C.c_void_p()
+    ns_v, never = _ns(ns)
+    n = lib().pgo_dbg_range(arr.ctypes.data_as(C.POINTER(C.c_uint8)), arr.shape[0], min(max(1, k), 27),
+                            int((c >> 1) == 1), ns_v, never, dbg_chunk, lo, hi, C.byref(kp), C.byref(mp))
+    if n < 0:
+        raise MemoryError("pgo_dbg_range: out of host memory for the range [%d, %d)" % (lo, hi))
+    try:
+        keys = np.ctypeslib.as_array((C.c_uint64 * n).from_address(kp.value)).copy() if n else np.zeros(0, np.uint64)
+        masks = np.ctypeslib.as_array((C.c_uint16 * n).from_address(mp.value)).copy() if n else np.zeros(0, np.uint16)
+    finally:
+        lib().pgo_free_buf(kp)
+        lib().pgo_free_buf(mp)
+    return keys, masks
+
+
+def key_ranges(k: int, parts: int):
+    """`parts` consecutive key ranges covering every key of k digits and the
+    sentinel: [lo_i, lo_{i+1}), the last one ending at 2**64 - 1."""
+    top = 5 ** min(max(1, k), 27)
+    b = [top * i // parts for i in range(parts)] + [2 ** 64 - 1]
+    return list(zip(b[:-1], b[1:]))
+
+
+def rdbg_member(masks: np.ndarray) -> np.ndarray:
+    """build_rdbg_jit_ :1300-1305: kept unless exactly one predecessor bit and
+    one successor bit."""
+    pc = np.array([bin(i).count("1") for i in range(64)], np.int8)
+    m = masks.astype(np.int64)
+    return ~((pc[(m >> 6) & 63] == 1) & (pc[m & 63] == 1))
 
 
 def label_table(xyz_text: str, mcl_text: str):

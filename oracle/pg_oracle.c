@@ -334,26 +334,23 @@ struct pgo_result {
 
 static int ns_hit(int64_t N, int64_t ns, int ns_never) { return !ns_never && N > ns; }
 
-int pgo_build_graph(const uint8_t* buf, int64_t n, int k, int rc0,
-                    int64_t ns, int ns_never, int64_t chunk, pgo_result** out) {
-    init_tables();
-    if (k < 1) k = 1;
-    if (k > 27) k = 27;                               /* :1236 */
-    pgo_result* r = (pgo_result*)calloc(1, sizeof(pgo_result));
-    r->k = k;
-    double t0 = now_s();
-    oak_init(&r->dbg, 1 << 20); r->has_dbg = 1;       /* init_dict :1097-1122 */
+/* seq2rdbg :1251-1266 -> seq2dbg_jit_ :1208-1228: every window of the pass
+ * (both strands when rc0) to fn, with the chunk checkpoints (:1224-1225) and
+ * their resume (offset = the seqio ptr of the record that crossed, :1255-1259)
+ * and the -n limit (:1227). */
+static void dbg_pass(const uint8_t* buf, int64_t n, int k, int rc0, int64_t ns, int ns_never, int64_t chunk,
+                     window_fn fn, void* ctx, int64_t* n_bases, int64_t* n_records) {
     uint8_t* rv = NULL; int64_t rvcap = 0;
     int64_t N = 0, offset = 0;
-    for (;;) {                                       /* seq2rdbg :1251-1266 */
+    for (;;) {
         int64_t Nl = 0, chk = 0, ptr = 0; int done = 1;
         rec_iter it; it_init(&it, buf, n, offset);
-        while (next_record(&it)) {                   /* seq2dbg_jit_ :1208-1228 */
+        while (next_record(&it)) {
             const uint8_t* s = it.seq; int64_t ln = it.seq_len;
-            walk_windows(s, ln, k, dbg_window, &r->dbg);
-            Nl += ln; chk += ln; r->n_bases += ln; r->n_records++;
+            walk_windows(s, ln, k, fn, ctx);
+            Nl += ln; chk += ln; *n_bases += ln; (*n_records)++;
             if (rc0) {
-                walk_windows(reverse_seq(s, ln, &rv, &rvcap), ln, k, dbg_window, &r->dbg);
+                walk_windows(reverse_seq(s, ln, &rv, &rvcap), ln, k, fn, ctx);
                 Nl += ln; chk += ln;
             }
             if (chk > chunk) { done = -1; ptr = it.r_ptr; break; }
@@ -366,6 +363,18 @@ int pgo_build_graph(const uint8_t* buf, int64_t n, int k, int rc0,
         if (ns_hit(N, ns, ns_never)) break;
     }
     free(rv);
+}
+
+int pgo_build_graph(const uint8_t* buf, int64_t n, int k, int rc0,
+                    int64_t ns, int ns_never, int64_t chunk, pgo_result** out) {
+    init_tables();
+    if (k < 1) k = 1;
+    if (k > 27) k = 27;                               /* :1236 */
+    pgo_result* r = (pgo_result*)calloc(1, sizeof(pgo_result));
+    r->k = k;
+    double t0 = now_s();
+    oak_init(&r->dbg, 1 << 20); r->has_dbg = 1;       /* init_dict :1097-1122 */
+    dbg_pass(buf, n, k, rc0, ns, ns_never, chunk, dbg_window, &r->dbg, &r->n_bases, &r->n_records);
     double t1 = now_s();
     /* dbg2rdbg :1313-1321 -> build_rdbg_jit_ :1293-1309 (slot order) */
     oak_init(&r->rdbg, 1 << 20); r->has_rdbg = 1;
@@ -382,6 +391,79 @@ int pgo_build_graph(const uint8_t* buf, int64_t n, int k, int rc0,
     *out = r;
     return 0;
 }
+
+/* ------------------------------------------------- dBG of one key range */
+/* The same dBG (key -> OR of add_kmer's masks, :1036-1047) for the keys in
+ * [lo, hi) only (hi = 2^64-1 includes the n<k sentinel), by sorting the
+ * range's occurrences instead of inserting them into an oakht: what the
+ * benchmark-scale digests of inputs too large for one in-memory oakht use
+ * (tests/golden/make_scale_digests.py).  The result is a set, so it does not
+ * depend on the table (tests/test_oracle_golden.py checks it against
+ * pgo_build_graph on every golden input). */
+typedef struct { uint64_t key; uint16_t mask; uint16_t pad[3]; } kocc;
+typedef struct { uint64_t lo, hi; kocc* v; int64_t n, cap; } range_ctx;
+
+/* pass 1 (v == NULL) counts the range's occurrences, pass 2 stores them */
+static void range_window(void* ctx, uint64_t idx, uint64_t key, uint8_t hd, uint8_t nt) {
+    (void)idx;
+    range_ctx* c = (range_ctx*)ctx;
+    if (!(key >= c->lo && (key < c->hi || (c->hi == SENTINEL && key == SENTINEL)))) return;
+    if (c->v && c->n < c->cap) {
+        c->v[c->n].key = key;
+        c->v[c->n].mask = (uint16_t)((LASTC[hd] << OFFBIT) | LASTC[nt]);
+    }
+    c->n++;
+}
+
+static int radix_sort_kocc(kocc* a, int64_t n) {      /* LSD, 8-bit digits, stable */
+    kocc* b = (kocc*)malloc(sizeof(kocc) * (size_t)(n ? n : 1));
+    if (!b) return -1;
+    int64_t cnt[256];
+    uint64_t all_or = 0, all_and = ~0ull;
+    for (int64_t i = 0; i < n; i++) { all_or |= a[i].key; all_and &= a[i].key; }
+    kocc *src = a, *dst = b;
+    for (int sh = 0; sh < 64; sh += 8) {
+        if ((((all_or ^ all_and) >> sh) & 0xFF) == 0) continue;       /* digit equal everywhere */
+        memset(cnt, 0, sizeof(cnt));
+        for (int64_t i = 0; i < n; i++) cnt[(src[i].key >> sh) & 0xFF]++;
+        int64_t o = 0;
+        for (int d = 0; d < 256; d++) { int64_t t = cnt[d]; cnt[d] = o; o += t; }
+        for (int64_t i = 0; i < n; i++) dst[cnt[(src[i].key >> sh) & 0xFF]++] = src[i];
+        kocc* t = src; src = dst; dst = t;
+    }
+    if (src != a) memcpy(a, src, sizeof(kocc) * (size_t)n);
+    free(b);
+    return 0;
+}
+
+int64_t pgo_dbg_range(const uint8_t* buf, int64_t n, int k, int rc0, int64_t ns, int ns_never, int64_t chunk,
+                      uint64_t lo, uint64_t hi, uint64_t** keys_out, uint16_t** masks_out) {
+    init_tables();
+    if (k < 1) k = 1;
+    if (k > 27) k = 27;
+    range_ctx c = {lo, hi, NULL, 0, 0};
+    int64_t nb = 0, nr = 0;
+    dbg_pass(buf, n, k, rc0, ns, ns_never, chunk, range_window, &c, &nb, &nr);
+    c.cap = c.n;
+    c.v = (kocc*)malloc(sizeof(kocc) * (size_t)(c.cap ? c.cap : 1));
+    if (!c.v) return -1;
+    c.n = 0;
+    dbg_pass(buf, n, k, rc0, ns, ns_never, chunk, range_window, &c, &nb, &nr);
+    if (c.n != c.cap || radix_sort_kocc(c.v, c.n) != 0) { free(c.v); return -1; }
+    int64_t m = 0;
+    for (int64_t i = 0; i < c.n; i++) {               /* OR per key, in key order */
+        if (m && c.v[m - 1].key == c.v[i].key) c.v[m - 1].mask |= c.v[i].mask;
+        else c.v[m++] = c.v[i];
+    }
+    uint64_t* K = (uint64_t*)malloc(8 * (size_t)(m ? m : 1));
+    uint16_t* M = (uint16_t*)malloc(2 * (size_t)(m ? m : 1));
+    if (!K || !M) { free(K); free(M); free(c.v); return -1; }
+    for (int64_t i = 0; i < m; i++) { K[i] = c.v[i].key; M[i] = c.v[i].mask; }
+    free(c.v);
+    *keys_out = K; *masks_out = M;
+    return m;
+}
+void pgo_free_buf(void* p) { free(p); }
 
 /* rdbg_edge_weight :1446-1518 for one walk */
 typedef struct {

@@ -76,6 +76,16 @@ void pgo_set_rdbg(pgo_result* r, const uint64_t* keys, int64_t n);
 
 void pgo_free(pgo_result* r);
 
+/* The dBG entries whose key lies in [lo, hi) (hi = 2^64-1: the n<k sentinel
+ * included), sorted by key, of the same dBG pass as pgo_build_graph, by
+ * sorting the range's occurrences instead of an oakht (inputs too big for
+ * one in-memory table are digested range by range).  Returns the entry
+ * count, or -1 when out of memory; *keys / *masks are freed with
+ * pgo_free_buf. */
+int64_t pgo_dbg_range(const uint8_t* buf, int64_t n, int k, int rc0, int64_t ns, int ns_never, int64_t chunk,
+                      uint64_t lo, uint64_t hi, uint64_t** keys, uint16_t** masks);
+void pgo_free_buf(void* p);
+
 #ifdef __cplusplus
 }
 #endif

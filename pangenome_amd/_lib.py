@@ -31,6 +31,7 @@ PG_TUNE_K3_TAIL = 13
 PG_TUNE_EARLY_SPLIT = 14
 PG_TUNE_K3_HEAD = 15
 PG_TUNE_H2D_TAIL = 16
+PG_TUNE_POISON = 17             # process-wide debug: new device buffers filled with this byte
 
 
 class PgStats(C.Structure):
@@ -71,6 +72,9 @@ SIGNATURES = {
     "pg_rdbg_export": (C.c_int, [_P, _P, C.c_uint64, _U64P]),
     "pg_dbg_partition": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
     "pg_dbg_merge": (C.c_int, [_P, _P, C.c_uint64, C.c_uint64, C.c_int]),
+    "pg_dbg_partition_sums": (C.c_int, [_P, C.c_int, _P]),
+    "pg_rows_checksum": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
+    "pg_dbg_merge_check": (C.c_int, [_P, _U64P, _U64P]),
     "pg_edges": (C.c_int, [_P, _P, C.c_int, _U64P]),
     "pg_edges_export": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_set_labels": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
@@ -328,6 +332,27 @@ class Context:
     def merge(self, d_records: int, n: int, capacity_hint: int = 0, sentinel: bool = False):
         check(self.lib.pg_dbg_merge(self.h, C.c_void_p(d_records) if n else None, n, capacity_hint,
                                     int(bool(sentinel))), "pg_dbg_merge")
+
+    def partition_sums(self, nparts: int):
+        """row_check sums of the last partition scatter's runs (uint64[nparts])."""
+        sums = np.zeros(nparts, np.uint64)
+        check(self.lib.pg_dbg_partition_sums(self.h, nparts, ptr(sums)), "pg_dbg_partition_sums")
+        return sums
+
+    def rows_checksum(self, d_rows: int, seg_off):
+        """row_check sums of segments [seg_off[s], seg_off[s+1]) of the 16-byte
+        records at device address d_rows (uint64[len(seg_off) - 1])."""
+        off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+        sums = np.zeros(max(off.shape[0] - 1, 1), np.uint64)
+        check(self.lib.pg_rows_checksum(self.h, C.c_void_p(d_rows) if d_rows else None, ptr(off),
+                                        max(off.shape[0] - 1, 0), ptr(sums)), "pg_rows_checksum")
+        return sums[:max(off.shape[0] - 1, 0)]
+
+    def merge_check(self):
+        """(non-empty records, row_check sum) the last merge read."""
+        rows, s = C.c_uint64(), C.c_uint64()
+        check(self.lib.pg_dbg_merge_check(self.h, C.byref(rows), C.byref(s)), "pg_dbg_merge_check")
+        return rows.value, s.value
 
     # -------------------------------------------------------------- walks
     def edges_count(self, rec_flags=None, rc1: bool = False) -> int:

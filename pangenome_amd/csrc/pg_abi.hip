@@ -330,6 +330,10 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         pg::DevBytes::cap().store((uint64_t)value);
         pg::DevBytes::peak().store(pg::DevBytes::cur().load());
         break;
+      case PG_TUNE_POISON:
+        if (value < -1 || value > 255) throw pg::Error(PG_EINVAL, "pg_tune: poison byte must be in [-1, 255]");
+        pg::DevBytes::poison().store((int)value);
+        break;
       case PG_TUNE_STAGE_SLOTS:
         if (value < 0 || value == 1 || value > 8) throw pg::Error(PG_EINVAL, "pg_tune: staging slots must be 0 or 2..8");
         x->c.stage_slots = value ? (uint64_t)value : 4;
@@ -426,7 +430,33 @@ int pg_dbg_merge(pg_ctx* x, const void* d_records, uint64_t n, uint64_t cap_hint
   return guard([&] {
     if (!x || (!d_records && n)) throw pg::Error(PG_EINVAL, "pg_dbg_merge: bad arguments");
     PG_HIP(hipSetDevice(x->c.device));
+    x->c.merge_sum = x->c.merge_rows = 0;
     pg::merge_dbg(x->c, d_records, n, cap_hint, sentinel);
+  });
+}
+
+int pg_dbg_partition_sums(pg_ctx* x, int nparts, uint64_t* sums) {
+  return guard([&] {
+    if (!x || !sums || nparts < 1 || nparts > 64) throw pg::Error(PG_EINVAL, "pg_dbg_partition_sums: bad arguments");
+    if (x->c.part_nparts != nparts) throw pg::Error(PG_EINVAL, "pg_dbg_partition_sums: no scatter into that many parts");
+    for (int i = 0; i < nparts; ++i) sums[i] = x->c.part_sums[i];
+  });
+}
+
+int pg_rows_checksum(pg_ctx* x, const void* d_rows, const uint64_t* seg_off, uint64_t nseg, uint64_t* sums) {
+  return guard([&] {
+    if (!x || !seg_off || (nseg && !sums) || (!d_rows && nseg && seg_off[nseg] > seg_off[0]))
+      throw pg::Error(PG_EINVAL, "pg_rows_checksum: bad arguments");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::rows_checksum(x->c, d_rows, seg_off, nseg, sums);
+  });
+}
+
+int pg_dbg_merge_check(const pg_ctx* x, uint64_t* rows, uint64_t* sum) {
+  return guard([&] {
+    if (!x || !rows || !sum) throw pg::Error(PG_EINVAL, "pg_dbg_merge_check: bad arguments");
+    *rows = x->c.merge_rows;
+    *sum = x->c.merge_sum;
   });
 }
 

@@ -79,6 +79,15 @@ struct alignas(16) Slot {
   unsigned int aux;
 };
 
+// Integrity check of one 16-byte exchange record (words w0 = key1, w1 = mask |
+// aux << 32).  Sums of it (mod 2^64) over a run of records are order-free, so
+// the sender's per-owner sums, the receiver's per-source sums and what the
+// owner's merge reads can be compared (pg_dbg_partition_sums,
+// pg_rows_checksum, pg_dbg_merge_check; dist.py raises on a mismatch).
+__host__ __device__ __forceinline__ uint64_t row_check(uint64_t w0, uint64_t w1) {
+  return fmix64(w0 ^ fmix64(w1 ^ 0x9E3779B97F4A7C15ull));
+}
+
 // The primary table is quotiented: a bijective hash h = perm(c) of the kb-bit
 // key splits into a bucket index (high bits) and a quotient (low qbits <= 38
 // bits), so [quotient | 26-bit mask word] is one 64-bit word and a new key is

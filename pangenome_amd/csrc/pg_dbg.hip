@@ -1767,7 +1767,11 @@ k_preload_emit(const PreEnt* __restrict__ e, uint64_t n, TableView T, BinOut O) 
 }
 
 // Exchange records a multi-GPU owner received (pg_dbg_merge): canonical key
-// + 1 and the 26-bit mask word of both orientations.
+// + 1 and the 26-bit mask word of both orientations.  The sum of the
+// records' row_check and the count of non-empty records go to flags[8..9]
+// and flags[10..11] (pg_dbg_merge_check: what the merge read, against what
+// the senders' partition sums say was sent).
+constexpr int F_MERGE_SUM = 8, F_MERGE_ROWS = 10;       // 64-bit words at these flag indices
 __global__ void __launch_bounds__(IBLOCK)
 k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
   __shared__ EmitLds<1> s_emit;
@@ -1775,6 +1779,7 @@ k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
   __shared__ uint32_t st_mw[EST];
   if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
   __syncthreads();
+  unsigned long long acc = 0ull, live = 0ull;
   for (uint64_t b = blockIdx.x * (uint64_t)(4 * IBLOCK); b < n; b += (uint64_t)gridDim.x * 4 * IBLOCK) {
     uint64_t hh[4];
     uint32_t mm[4];
@@ -1785,10 +1790,19 @@ k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
       mm[t] = 0;
       if (i < n) {
         const Slot s = e[i];
-        if (s.key1) { hh[t] = T.perm(s.key1 - 1ull); mm[t] = s.mask & (uint32_t)MW_MASK; }
+        acc += row_check(s.key1, (uint64_t)s.mask | ((uint64_t)s.aux << 32));
+        if (s.key1) { hh[t] = T.perm(s.key1 - 1ull); mm[t] = s.mask & (uint32_t)MW_MASK; ++live; }
       }
     }
     block_emit<4>(O, hh, mm, s_emit, st_key, st_mw);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    acc += __shfl_down(acc, o, 64);
+    live += __shfl_down(live, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0 && (acc || live)) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(O.flags + F_MERGE_SUM), acc);
+    atomicAdd(reinterpret_cast<unsigned long long*>(O.flags + F_MERGE_ROWS), live);
   }
 }
 
@@ -2270,12 +2284,16 @@ __global__ void k_part_count(TableView T, uint64_t nw, uint64_t ntot, int nparts
 // shared owner cursors serialised ~8 M same-address atomics at the memory
 // side for a C3 table, tens of ms; see NQ above.)  Record order inside an
 // owner's run is arbitrary: the owner OR-merges them.
+// Each owner's run also gets the sum of its records' row_check (sums[owner]:
+// one LDS sum per block, one global atomic per block and owner at the end).
 constexpr int PT = 256, PE = 8, PCH = PT * PE;
 __global__ void __launch_bounds__(PT)
 k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts, unsigned long long* __restrict__ cursor,
-               Slot* __restrict__ out) {
+               Slot* __restrict__ out, unsigned long long* __restrict__ sums) {
   __shared__ unsigned s_cnt[64];
   __shared__ unsigned long long s_base[64];
+  __shared__ unsigned long long s_sum[64];
+  if (threadIdx.x < 64) s_sum[threadIdx.x] = 0ull;
   for (uint64_t c0 = blockIdx.x * (uint64_t)PCH; c0 < ntot; c0 += (uint64_t)gridDim.x * PCH) {
     if (threadIdx.x < 64) s_cnt[threadIdx.x] = 0u;
     __syncthreads();
@@ -2296,8 +2314,36 @@ k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts, unsigned lon
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < PE; ++j)
-      if (m[j]) out[s_base[own[j]] + rank[j]] = Slot{key[j] + 1ull, m[j], 0u};
+      if (m[j]) {
+        out[s_base[own[j]] + rank[j]] = Slot{key[j] + 1ull, m[j], 0u};
+        atomicAdd(&s_sum[own[j]], (unsigned long long)row_check(key[j] + 1ull, m[j]));
+      }
     __syncthreads();
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nparts && s_sum[threadIdx.x]) atomicAdd(&sums[threadIdx.x], s_sum[threadIdx.x]);
+}
+
+// Sums of row_check over segments of 16-byte records: segment s = records
+// [off[s], off[s+1]) (grid row s), one atomic per block.
+constexpr int RS_SEG = 32;
+struct SegOff { unsigned long long o[RS_SEG + 1]; };
+__global__ void __launch_bounds__(256) k_rows_sum(const Slot* __restrict__ rows, SegOff so,
+                                                  unsigned long long* __restrict__ sums) {
+  __shared__ unsigned long long s_red[4];
+  const uint32_t s = blockIdx.y;
+  const uint64_t lo = so.o[s], hi = so.o[s + 1];
+  unsigned long long acc = 0ull;
+  for (uint64_t i = lo + blockIdx.x * 256ull + threadIdx.x; i < hi; i += (uint64_t)gridDim.x * 256ull) {
+    const Slot r = rows[i];
+    acc += row_check(r.key1, (uint64_t)r.mask | ((uint64_t)r.aux << 32));
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    if (t) atomicAdd(&sums[s], t);
   }
 }
 
@@ -2679,6 +2725,8 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
       if (a.bits & F_A_OVER) return false;
     }
     const unsigned bits = hf[4];
+    c.merge_sum = (uint64_t)hf[F_MERGE_SUM] | ((uint64_t)hf[F_MERGE_SUM + 1] << 32);
+    c.merge_rows = (uint64_t)hf[F_MERGE_ROWS] | ((uint64_t)hf[F_MERGE_ROWS + 1] << 32);
     static const bool dbg_build = std::getenv("PG_DEBUG_BUILD") != nullptr;
     if (dbg_build)
       std::fprintf(stderr, "finish_build attempt %d: total %llu maxreg %llu maxbin %llu bb %d levels %zu rec_max %llu "
@@ -3037,10 +3085,10 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
   if (!c.built) throw Error(-22, "partition_dbg: no dBG");
   if (nparts < 1 || nparts > 64) throw Error(-22, "partition_dbg: nparts must be in [1, 64]");
   const uint64_t ntot = 2 * c.cap + c.ovf_cap;
-  DevBuf& cnt = c.part_cnt;                             // [0, 64) counts, [64, 128) cursors
-  cnt.reserve(16 * 64);
+  DevBuf& cnt = c.part_cnt;                             // [0, 64) counts, [64, 128) cursors, [128, 192) sums
+  cnt.reserve(24 * 64);
   auto* counts = cnt.as<unsigned long long>();
-  c.h_pin.reserve(16 * 64);
+  c.h_pin.reserve(24 * 64);
   auto* h = c.h_pin.as<unsigned long long>();
   if (!d_out) {                                         // count pass
     PG_HIP(hipMemsetAsync(cnt.p, 0, 8 * 64, c.stream));
@@ -3063,14 +3111,47 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
   uint64_t total = 0;
   for (int i = 0; i < nparts; ++i) { h[64 + i] = total; total += c.part_counts[i]; h_counts[i] = c.part_counts[i]; }
   if (out_cap < total) throw Error(-22, "partition_dbg: output buffer too small");
+  for (int i = 0; i < 64; ++i) c.part_sums[i] = 0;
   if (total) {
-    PG_HIP(hipMemcpyAsync(counts + 64, h + 64, 8 * nparts, hipMemcpyHostToDevice, c.stream));
+    for (int i = 0; i < nparts; ++i) h[128 + i] = 0;
+    PG_HIP(hipMemcpyAsync(counts + 64, h + 64, 8 * 128, hipMemcpyHostToDevice, c.stream));   // cursors, zeroed sums
     hipLaunchKernelGGL(k_part_scatter, dim3(grid_for(ntot, PCH, 4096)), dim3(PT), 0, c.stream, c.tv, 2 * c.cap, ntot,
-                       nparts, counts + 64, reinterpret_cast<Slot*>(d_out));
+                       nparts, counts + 64, reinterpret_cast<Slot*>(d_out), counts + 128);
     PG_HIP(hipGetLastError());
+    PG_HIP(hipMemcpyAsync(h + 128, counts + 128, 8 * nparts, hipMemcpyDeviceToHost, c.stream));
     c.sync();
+    for (int i = 0; i < nparts; ++i) c.part_sums[i] = h[128 + i];
   }
   return total;
+}
+
+// Sums of row_check over nseg segments of 16-byte records at d_rows
+// (segment s = records [off[s], off[s+1])), on the context's stream.
+void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums) {
+  DevBuf& out = c.part_cnt;                             // (after the partition words: [192, 192 + RS_SEG))
+  out.reserve(8 * (192 + RS_SEG));
+  auto* d = out.as<unsigned long long>() + 192;
+  c.h_pin.reserve(8 * RS_SEG);
+  auto* h = c.h_pin.as<unsigned long long>();
+  for (uint64_t s0 = 0; s0 < nseg; s0 += RS_SEG) {
+    const uint32_t ns = (uint32_t)std::min<uint64_t>(RS_SEG, nseg - s0);
+    SegOff so{};
+    uint64_t mx = 0;
+    for (uint32_t s = 0; s <= ns; ++s) so.o[s] = off[s0 + s];
+    for (uint32_t s = 0; s < ns; ++s) {
+      if (so.o[s + 1] < so.o[s]) throw Error(-22, "rows_checksum: segment offsets decrease");
+      mx = std::max<uint64_t>(mx, so.o[s + 1] - so.o[s]);
+    }
+    PG_HIP(hipMemsetAsync(d, 0, 8 * RS_SEG, c.stream));
+    if (mx) {
+      hipLaunchKernelGGL(k_rows_sum, dim3(grid_for(mx, 256, 2048), ns), dim3(256), 0, c.stream,
+                         reinterpret_cast<const Slot*>(d_rows), so, d);
+      PG_HIP(hipGetLastError());
+    }
+    PG_HIP(hipMemcpyAsync(h, d, 8 * ns, hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    for (uint32_t s = 0; s < ns; ++s) sums[s0 + s] = h[s];
+  }
 }
 
 // OR-merge received exchange records into a fresh owner table (stage A from

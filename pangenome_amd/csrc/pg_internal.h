@@ -42,6 +42,10 @@ struct DevBytes {
     uint64_t pk = peak().load();
     while (now > pk && !peak().compare_exchange_weak(pk, now)) {}
   }
+  // pg_tune PG_TUNE_POISON (debug): every new allocation is filled with this
+  // byte (-1 = off), so a read of memory no kernel wrote shows up as a
+  // different result instead of inheriting an earlier run's bytes
+  static std::atomic<int>& poison() { static std::atomic<int> v{-1}; return v; }
 };
 
 // A growable device buffer (never shrinks; reused across calls so the steady
@@ -71,6 +75,11 @@ struct DevBuf {
     }
     cap = nb;
     DevBytes::add(nb);
+    const int pv = DevBytes::poison().load();
+    if (pv >= 0) {
+      PG_HIP(hipMemset(p, pv, nb));
+      PG_HIP(hipDeviceSynchronize());
+    }
   }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
   void release() {
@@ -225,6 +234,8 @@ struct Ctx {
   int k3_ref2 = -1;               // k_cover's second reference record, -1: none
   DevBuf part_cnt;                // multi-GPU partition: owner counts and cursors
   uint64_t part_counts[64] = {};  // counts of the last count pass
+  uint64_t part_sums[64] = {};    // row_check sums of the last scatter's runs
+  uint64_t merge_sum = 0, merge_rows = 0;   // the last merge: row_check sum / non-empty records it read
   uint64_t part_total = 0;
   int part_nparts = 0;
   uint64_t part_gen = ~0ull;      // build_gen of the table the counts are for
@@ -334,6 +345,7 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap);
 uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap);
 uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts);
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel);
+void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums);
 // pg_persist.hip
 struct PreEnt {                   // one staged oakht slot: oriented key, 12-bit mask, count
   unsigned long long key;

@@ -464,17 +464,20 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
 // (s >= 1).  Under the chunked upload, the boundary at s1 is packed again by
 // the next chunk's call once the span after it is emitted; until then only
 // its bytes below own_s1 are final, and nothing reads the others.
+// (grid-stride: the launch's grid is capped)
 __global__ void k_pack_fix(const Fn* __restrict__ incl, uint64_t s0, uint64_t s1, const uint8_t* __restrict__ cls,
                            uint32_t* __restrict__ p2, uint8_t* __restrict__ e16) {
-  const uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s > s1 || s == 0) return;
-  const unsigned long long own = incl[s - 1].c0;
-  if (!(own & 15ull)) return;                                 // (no shared chunk)
-  const unsigned long long g = own & ~15ull;
-  const uint4 cv = *reinterpret_cast<const uint4*>(cls + g);
-  uint32_t exc;
-  p2[g >> 4] = pack_word(cv, exc);
-  e16[g >> 4] = exc ? 1 : 0;
+  for (uint64_t s = s0 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s <= s1;
+       s += (uint64_t)gridDim.x * blockDim.x) {
+    if (s == 0) continue;
+    const unsigned long long own = incl[s - 1].c0;
+    if (!(own & 15ull)) continue;                             // (no shared chunk)
+    const unsigned long long g = own & ~15ull;
+    const uint4 cv = *reinterpret_cast<const uint4*>(cls + g);
+    uint32_t exc;
+    p2[g >> 4] = pack_word(cv, exc);
+    e16[g >> 4] = exc ? 1 : 0;
+  }
 }
 
 // The record table from the scan's total (read on the device: no host round

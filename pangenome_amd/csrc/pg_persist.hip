@@ -337,6 +337,7 @@ uint64_t dbg_dump(Ctx& c, uint64_t& capacity, uint64_t* keys, uint16_t* values, 
 // piece waiting for the one before it: pipes, terminals, O_APPEND files).
 // crc: each member's CRC-32, or nullptr.
 constexpr uint64_t FD_PIECE = 16ull << 20;
+constexpr size_t FD_KEEP = 4;
 static void stream_to_fd(Ctx& c, int nm, const uint8_t* const* src, const uint64_t* len, int fd,
                          const uint64_t* pos, uint32_t* crc, const char* what) {
   struct Piece { int m; uint64_t at, n; };
@@ -409,6 +410,11 @@ static void stream_to_fd(Ctx& c, int nm, const uint8_t* const* src, const uint64
   for (size_t t = 1; t < nt; ++t) th.emplace_back(worker, t);
   worker(0);
   for (auto& x : th) x.join();
+  // the context keeps FD_KEEP piece buffers for its next dump / text write
+  // (pinning them costs ~1 ms each); the rest go back now, so a context holds
+  // at most FD_KEEP x 18 MiB of pinned host memory between calls
+  for (size_t t = FD_KEEP; t < c.dump_pin.size(); ++t) c.dump_pin[t].release();
+  if (c.dump_pin.size() > FD_KEEP) c.dump_pin.resize(FD_KEEP);
   if (bad) throw Error(-5, err);
   if (!crc) return;
   for (int m = 0; m < nm; ++m) crc[m] = 0u;

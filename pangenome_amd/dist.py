@@ -88,20 +88,94 @@ def _comm_device(device, group):
     return stage, (torch.device("cpu") if stage else device)
 
 
-def _route(table, world: int, device, group=None, sentinel_local: bool = False, subparts: int = 1, tm=None):
+M64 = (1 << 64) - 1
+# env PG_EXCHANGE_SELF_RCCL=1: a rank's own run goes through the collective
+# like every other (at world 1: through RCCL) instead of a device copy
+SELF_COPY = os.environ.get("PG_EXCHANGE_SELF_RCCL") != "1"
+# env PG_DEBUG_POISON=<byte>: the exchange's torch buffers are filled with it
+# before use (pg_tune PG_TUNE_POISON does the same for the library's own)
+_POISON = os.environ.get("PG_DEBUG_POISON")
+
+
+class ExchangeIntegrityError(RuntimeError):
+    """Records of the owner exchange changed between the sender's partition
+    and the owner's merge (the message names the round, the peer, the piece
+    and the stage where the sums first disagree)."""
+
+
+def _fence(device):
+    """The library runs on its own non-blocking streams, which do not wait on
+    torch's: before native code reads or writes memory the torch allocator
+    handed out, everything torch's streams (the current one, RCCL's) queued
+    must be done — a block freed behind queued work (a clone, a collective)
+    is handed out again at once to the next torch.empty on the same stream."""
+    if _is_cuda(device):
+        import torch
+        torch.cuda.synchronize(device)
+
+
+def _fmix64(k):
+    k = k ^ (k >> np.uint64(33))
+    k = k * np.uint64(0xFF51AFD7ED558CCD)
+    k = k ^ (k >> np.uint64(33))
+    k = k * np.uint64(0xC4CEB9FE1A85EC53)
+    return k ^ (k >> np.uint64(33))
+
+
+def row_check_sum(rows) -> int:
+    """Sum mod 2^64 of row_check (pg_common.h) over (n, 2) int64 records on
+    the host: the CPU form of pg_rows_checksum."""
+    w = np.ascontiguousarray(np.asarray(rows)).reshape(-1, 2).view(np.uint64)
+    if w.shape[0] == 0:
+        return 0
+    with np.errstate(over="ignore"):
+        h = _fmix64(w[:, 0] ^ _fmix64(w[:, 1] ^ np.uint64(0x9E3779B97F4A7C15)))
+        return int(h.sum(dtype=np.uint64))
+
+
+def _seg_sums(shard, buf, offsets, device) -> list:
+    """row_check sums of segments [offsets[i], offsets[i+1]) of the (n, 2)
+    int64 tensor buf: on the device through the library, on the host with
+    numpy."""
+    if len(offsets) < 2:
+        return []
+    if getattr(buf, "is_cuda", False):
+        _fence(device)
+        return [int(x) for x in shard.rows_checksum(buf.data_ptr(), np.asarray(offsets, np.uint64))]
+    a = buf.numpy() if hasattr(buf, "numpy") else np.asarray(buf)
+    return [row_check_sum(a[offsets[i]:offsets[i + 1]]) for i in range(len(offsets) - 1)]
+
+
+def _poisoned(t):
+    if _POISON is not None:
+        t.view(-1).view(__import__("torch").uint8).fill_(int(_POISON, 0) & 255)
+    return t
+
+
+def _route(table, world: int, device, group=None, sentinel_local: bool = False, subparts: int = 1, tm=None,
+           where: str = "", fail=None):
     """This rank's table -> owner runs of 16-byte records (pg_dbg_partition)
-    -> one all-to-all.  Every rank's run lengths, with its n<k sentinel flag,
-    go to every rank in one small all-gather: the whole (source, owner) count
-    matrix gives this rank's receive sizes, the largest peer message (the
-    piece count of _all_to_all_rows) and the global sentinel, and is the only
-    host read.  With `subparts` = P > 1 the table is cut into world x P parts
-    (part q: owner q // P, the owner's sub-log q % P; world x P <= 64), so an
-    owner's run from each rank arrives already split into its P sub-logs.
+    -> one all-to-all.  Every rank's run lengths and their integrity sums,
+    with its n<k sentinel flag, go to every rank in one small all-gather: the
+    whole (source, owner) matrix gives this rank's receive sizes, the largest
+    peer message (the piece count of _all_to_all_rows), the global sentinel
+    and the sums each received run must have; it is the only host read.  With
+    `subparts` = P > 1 the table is cut into world x P parts (part q: owner
+    q // P, the owner's sub-log q % P; world x P <= 64), so an owner's run
+    from each rank arrives already split into its P sub-logs.
+    Integrity (always on): the partition must hold every entry of the table
+    (record conservation), and every received (source, sub-log) run must
+    carry the sum its sender computed while scattering it; a mismatch on any
+    rank raises ExchangeIntegrityError on every rank (one MAX all-reduce of a
+    flag), naming `where`, the peer, the sub-log and the 512 MiB piece.
+    `fail`: a failed check of this rank since the last collective (a
+    message): it travels in the count matrix and every rank raises.
     Returns (the records this rank owns as an (n, 2) int64 tensor on
     `device`, the received counts per (source rank, sub-log) as a (world, P)
-    array, bytes sent to other ranks, whether any rank saw the sentinel).
-    `tm` (a dict) accumulates the seconds of the partition and of the
-    all-to-all (the collectives are synchronised for it)."""
+    array, their expected sums as a (world, P) array of Python ints, bytes
+    sent to other ranks, whether any rank saw the sentinel).  `tm` (a dict)
+    accumulates the seconds of the partition and of the all-to-all (the
+    collectives are synchronised for it)."""
     import torch
     import torch.distributed as dist
     P = subparts
@@ -110,28 +184,48 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     t0 = perf_counter()
     counts = table.partition(world * P).astype(np.int64).reshape(world, P)
     total = int(counts.sum())
-    send = torch.empty((max(total, 1), 2), dtype=torch.int64, device=device)
+    n_ent = table.entries() if hasattr(table, "entries") else None
+    if n_ent is not None and total != n_ent and not fail:
+        fail = ("%s: rank %d's partition holds %d records for a table of %d entries (stage: partition)"
+                % (where or "exchange", rank, total, n_ent))
+    send = _poisoned(torch.empty((max(total, 1), 2), dtype=torch.int64, device=device))
+    sums = np.zeros(world * P, np.uint64)
     if total:
+        _fence(device)
         table.partition(world * P, send.data_ptr(), total)   # (returns after the scatter)
+        sums = np.asarray(table.partition_sums(world * P), np.uint64)
     t1 = perf_counter()
-    head = np.zeros((world, P + 1), np.int64)
+    head = np.zeros((world, 2 * P + 2), np.int64)
     head[:, :P] = counts
     head[:, P] = 1 if sentinel_local else 0
+    head[:, P + 1:2 * P + 1] = sums.reshape(world, P).view(np.int64)
+    head[:, 2 * P + 1] = 1 if fail else 0
     send_head = torch.from_numpy(head.reshape(-1)).to(comm)
     heads = [torch.empty_like(send_head) for _ in range(world)]
     dist.all_gather(heads, send_head, group=group)
-    H = torch.stack(heads).cpu().numpy().reshape(world, world, P + 1)     # [source, owner, sub-log | flag]
-    rh = H[:, rank, :]
-    rsplit = rh[:, :P].sum(axis=1).tolist()
+    H = torch.stack(heads).cpu().numpy().reshape(world, world, 2 * P + 2)  # [source, owner, counts|flag|sums|fail]
+    _raise_if_any(fail, H[:, 0, 2 * P + 1].tolist(), rank)
+    rh = H[:, rank, :P]
+    want = H[:, rank, P + 1:2 * P + 1].copy().view(np.uint64)
+    rsplit = rh.sum(axis=1).tolist()
     nrecv = int(sum(rsplit))
-    recv = torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm)
+    recv = _poisoned(torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm))
     ssplit = counts.sum(axis=1).tolist()
     if stage:
         dist.all_to_all_single(recv[:nrecv], send.cpu()[:total], output_split_sizes=rsplit,
                                input_split_sizes=ssplit, group=group)
         recv = recv.to(device)
     else:
-        _all_to_all_rows(recv, send, rsplit, ssplit, comm, group, big=int(H[:, :, :P].sum(axis=2).max()))
+        _all_to_all_rows(recv, send, rsplit, ssplit, comm, group, big=int(H[:, :, :P].sum(axis=2).max()),
+                         self_copy=SELF_COPY)
+    # every received (source, sub-log) run against its sender's sum
+    off = np.concatenate([[0], np.cumsum(rh.reshape(-1))]).astype(np.int64).tolist()
+    got = _seg_sums(table, recv, off, device)
+    bad = [(s, p) for s in range(world) for p in range(P) if got[s * P + p] != int(want[s, p])]
+    flag = torch.tensor([1 if bad else 0], dtype=torch.int64, device=comm)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm, group, where)
     if tm is not None:
         if _is_cuda(device):
             torch.cuda.synchronize(device)
@@ -139,7 +233,49 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
         tm["partition"] = tm.get("partition", 0.0) + (t1 - t0)
         tm["all_to_all"] = tm.get("all_to_all", 0.0) + (t2 - t1)
         tm["rows"] = tm.get("rows", 0) + total
-    return recv[:nrecv], rh[:, :P], 16 * (total - int(counts[rank].sum())), bool(H[:, :, P].any())
+    want_l = [[int(want[s, p]) for p in range(P)] for s in range(world)]
+    return recv[:nrecv], rh, want_l, 16 * (total - int(counts[rank].sum())), bool(H[:, :, P].any())
+
+
+def _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm, group, where):
+    """A received run's sum disagreed somewhere: every rank sums its send and
+    receive messages per A2A_ROWS piece, the senders' piece sums go to every
+    rank, and every rank raises, the receivers naming the pieces that
+    differ."""
+    import torch
+    import torch.distributed as dist
+    ssplit, rsplit = counts.sum(axis=1), rh.sum(axis=1)
+    npc = max(1, int(-(-max(int(ssplit.max()), int(rsplit.max()), 1) // A2A_ROWS)))
+
+    def piece_offsets(split):
+        base = np.concatenate([[0], np.cumsum(split)]).astype(np.int64)
+        return [[int(min(base[o] + j * A2A_ROWS, base[o + 1])) for j in range(npc + 1)] for o in range(world)]
+    so, ro = piece_offsets(ssplit), piece_offsets(rsplit)
+    mine = np.array([_seg_sums(table, send, so[o], device) for o in range(world)], np.uint64).reshape(world, npc)
+    psum = sums.reshape(world, P)
+    with np.errstate(over="ignore"):
+        changed = [o for o in range(world) if int(mine[o].sum(dtype=np.uint64)) != int(psum[o].sum(dtype=np.uint64))]
+    npc_t = torch.tensor([npc], dtype=torch.int64, device=comm)
+    dist.all_reduce(npc_t, op=dist.ReduceOp.MAX, group=group)
+    if int(npc_t.item()) != npc:
+        raise ExchangeIntegrityError("%s: received run sums differ (rank %d: %s); piece counts differ across ranks"
+                                     % (where or "exchange", rank, bad))
+    t = torch.from_numpy(mine.view(np.int64).reshape(-1)).to(comm)
+    allp = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(allp, t, group=group)
+    sent = torch.stack(allp).cpu().numpy().view(np.uint64).reshape(world, world, npc)   # [source, owner, piece]
+    msgs = ["this rank's send buffer for owners %s no longer matches its partition sums (stage: send buffer, between "
+            "the scatter and the all_to_all)" % changed] if changed else []
+    for s in sorted({b[0] for b in bad}):
+        got = _seg_sums(table, recv, ro[s], device)
+        pcs = [j for j in range(npc) if got[j] != int(sent[s, rank, j])]
+        msgs.append("from rank %d: sub-logs %s, %s (stage: all_to_all, %s)"
+                    % (s, [p for (s2, p) in bad if s2 == s],
+                       "pieces %s of %d rows each differ on the wire" % (pcs, A2A_ROWS) if pcs else
+                       "no piece differs on the wire: the sender's buffer changed after its partition sums",
+                       "self copy" if s == rank and SELF_COPY else "collective"))
+    raise ExchangeIntegrityError("%s: rank %d: exchanged records changed between the partition and the receive: %s"
+                                 % (where or "exchange", rank, "; ".join(msgs) or "(another rank's records)"))
 
 
 # Records per peer and collective on device backends: RCCL 2.26 (ROCm 7)
@@ -155,17 +291,13 @@ def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None, big=None, sel
     any rank decides; `big`, when the caller knows it, else one MAX
     all-reduce finds it).  Views of contiguous runs; the rank's own run is a
     device copy and never goes through the collective (`self_copy=False`:
-    it does, tests/test_gpu_rccl.py's way to drive RCCL at world 1)."""
+    it does, as every other run; at world 1 that drives RCCL)."""
     import torch
     import torch.distributed as dist
     world = len(ssplit)
     me = dist.get_rank(group) if world > 1 else 0
     if not self_copy:
         me = -1
-    # the rank's own run: a device copy (at world 1 nothing else moves).  C5's
-    # streamed exchange at world 1 came back wrong in some runs when its
-    # ~16 GB per round went to self through RCCL in 512 MiB pieces
-    # (nondeterministic, box-dependent) and never with the copy.
     if me >= 0 and ssplit[me]:
         so_me = int(np.sum(ssplit[:me])) if me else 0
         ro_me = int(np.sum(rsplit[:me])) if me else 0
@@ -202,13 +334,39 @@ def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None, big=None, sel
                 at += x.shape[0]
 
 
-def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None, sentinel_global=None, tm=None):
+def _merge_checked(table, buf, n: int, sentinel: bool, want_sum: int, device, what: str):
+    """table.merge of the first n records of buf, then what the merge read
+    against (n, want_sum): record conservation and integrity of the log
+    between the all-to-all and the merge.  Returns None, or the mismatch as a
+    message for the caller to raise on every rank at its next collective
+    (raising here alone would leave the other ranks waiting in it)."""
+    _fence(device)
+    table.merge(buf.data_ptr() if n else 0, n, sentinel=sentinel)
+    if hasattr(table, "merge_check"):
+        rows, s = table.merge_check()
+        if rows != n or (s & M64) != (want_sum & M64):
+            return ("%s: the merge read %d records with sum %#x, the log holds %d with sum %#x (stage: merge)"
+                    % (what, rows, s, n, want_sum & M64))
+    return None
+
+
+def _raise_if_any(fail, flags, rank: int):
+    """every rank raises when any rank's check failed (flags: one per rank)"""
+    bad = [r for r, f in enumerate(flags) if f]
+    if bad:
+        raise ExchangeIntegrityError(fail if fail else "exchange: rank(s) %s failed an integrity check (rank %d's "
+                                     "records are fine)" % (bad, rank))
+
+
+def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None, sentinel_global=None, tm=None,
+                  want_sum=None):
     """OR-merge the owned records into a fresh owner table, rdBG rule on it;
     global (n_dbg, n_rdbg) by one sum all-reduce.  `sentinel_global`: whether
     any rank saw the n<k sentinel, when the caller already knows (else one MAX
-    all-reduce of `sentinel_local` finds out).  Returns (n_dbg_total,
-    n_rdbg_total, n_rdbg_local); `tm["merge"]` accumulates the seconds of the
-    merge, the rdBG rule and the count all-reduce."""
+    all-reduce of `sentinel_local` finds out); `want_sum`: the integrity sum
+    the received records must have.  Returns (n_dbg_total, n_rdbg_total,
+    n_rdbg_local); `tm["merge"]` accumulates the seconds of the merge, the
+    rdBG rule and the count all-reduce."""
     import torch
     import torch.distributed as dist
     _, comm = _comm_device(device, group)
@@ -217,15 +375,21 @@ def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=No
         flag = torch.tensor([1 if sentinel_local else 0], dtype=torch.int64, device=comm)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
         sentinel_global = bool(flag.item())
-    if _is_cuda(device):
-        torch.cuda.synchronize(device)
     # the n<k sentinel key belongs to one owner: rank 0
     n = int(recv.shape[0])
-    table.merge(recv.data_ptr(), n, sentinel=sentinel_global and rank == 0)
+    fail = None
+    if want_sum is None:
+        _fence(device)
+        table.merge(recv.data_ptr(), n, sentinel=sentinel_global and rank == 0)
+    else:
+        fail = _merge_checked(table, recv, n, sentinel_global and rank == 0, want_sum, device,
+                              "exchange: rank %d's owner merge" % rank)
     st = table.build_rdbg()
-    sums = torch.tensor([st.n_dbg, st.n_rdbg], dtype=torch.int64, device=comm)
+    sums = torch.tensor([st.n_dbg, st.n_rdbg, 1 if fail else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
-    n_dbg, n_rdbg = sums.tolist()
+    n_dbg, n_rdbg, nfail = sums.tolist()
+    if nfail:
+        _raise_if_any(fail, [1], rank)
     if tm is not None:
         tm["merge"] = tm.get("merge", 0.0) + (perf_counter() - t0)
     return int(n_dbg), int(n_rdbg), int(st.n_rdbg)
@@ -236,8 +400,10 @@ def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bo
     host reads (the count matrix, the global counts) besides the partition's
     own count read.  Returns (n_dbg_total, n_rdbg_total, n_rdbg_local,
     bytes_sent); `tm` accumulates partition / all_to_all / merge seconds."""
-    recv, _, sent, sentinel = _route(table, world, device, group, sentinel_local, tm=tm)
-    return _owner_reduce(table, recv, rank, device, sentinel_local, group, sentinel_global=sentinel, tm=tm) + (sent,)
+    recv, _, want, sent, sentinel = _route(table, world, device, group, sentinel_local, tm=tm, where="exchange")
+    want_sum = sum(x for row in want for x in row) & M64
+    return _owner_reduce(table, recv, rank, device, sentinel_local, group, sentinel_global=sentinel, tm=tm,
+                         want_sum=want_sum) + (sent,)
 
 
 def stream_chunks(flags, seq_len, limit: int) -> list:
@@ -317,21 +483,26 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         compact_at = max(1 << 20, _free_device_bytes(device) // 4 // 16)
     logs = [[] for _ in range(P)]
     logn, base = [0] * P, [0] * P
+    logsum = [0] * P                                   # integrity sum of each sub-log's records (mod 2^64)
     sentinel, sent = False, 0
+    fail = []                                          # failed checks, raised on every rank at the next collective
 
-    def compact(p):
+    def compact(p, i):
         cat = torch.cat(logs[p]) if len(logs[p]) > 1 else logs[p][0]
         logs[p] = []                                   # (the pieces go as soon as they are merged)
-        if _is_cuda(device):
-            torch.cuda.synchronize(device)
-        shard.merge(cat.data_ptr(), int(cat.shape[0]), False)
+        f = _merge_checked(shard, cat, int(cat.shape[0]), False, logsum[p], device,
+                           "exchange round %d: rank %d's compaction of sub-log %d" % (i, rank, p))
+        if f:
+            fail.append(f)
         del cat
         m = int(shard.partition(1)[0])
-        out = torch.empty((max(m, 1), 2), dtype=torch.int64, device=device)
+        out = _poisoned(torch.empty((max(m, 1), 2), dtype=torch.int64, device=device))
         if m:
+            _fence(device)
             shard.partition(1, out.data_ptr(), m)
         logs[p] = [out[:m]] if m else []
         logn[p] = base[p] = m
+        logsum[p] = int(shard.partition_sums(1)[0]) if m else 0
 
     for i in range(rounds):
         if staged is not None and i < 2:
@@ -343,7 +514,8 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         sentinel |= bool(shard.build(f, extra if i == 0 else 0, rc0))
         if on_chunk is not None:
             on_chunk()
-        recv, sub, s, _ = _route(shard, world, device, group, subparts=P)
+        recv, sub, want, s, _ = _route(shard, world, device, group, subparts=P, where="exchange round %d" % i,
+                                       fail=fail[0] if fail else None)
         sent += s
         # each source's run arrives as its P sub-log runs; with P > 1 each run
         # is copied out, so that compacting one sub-log frees its memory (a
@@ -355,34 +527,43 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
                 if m:
                     logs[p].append(recv[off:off + m].clone() if P > 1 else recv[off:off + m])
                     logn[p] += m
+                    logsum[p] = (logsum[p] + want[src][p]) & M64
                 off += m
         del recv
         total = sum(logn)
         if total >= compact_at:
             for p in sorted(range(P), key=lambda q: -logn[q]):
                 if logn[p] >= 2 * base[p] and len(logs[p]) > 1:
-                    compact(p)
+                    compact(p, i)
     # the n<k sentinel key belongs to one owner: rank 0 (sub-log 0)
-    flag = torch.tensor([1 if sentinel else 0], dtype=torch.int64, device=comm)
+    flag = torch.tensor([1 if sentinel else 0, 1 if fail else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    sent_global = bool(flag.item())
+    sent_global = bool(flag[0].item())
+    if int(flag[1].item()):
+        _raise_if_any(fail[0] if fail else None, [1], rank)
     n_dbg_loc = n_rdbg_loc = 0
     keys = []
     for p in range(P):
         cat = (torch.cat(logs[p]) if len(logs[p]) > 1 else logs[p][0]) if logs[p] else None
         logs[p] = []
-        if _is_cuda(device):
-            torch.cuda.synchronize(device)
         n = 0 if cat is None else int(cat.shape[0])
-        shard.merge(cat.data_ptr() if n else 0, n, sentinel=sent_global and rank == 0 and p == 0)
+        if n != logn[p]:
+            fail.append("exchange: rank %d's sub-log %d holds %d records, %d were received (stage: log)"
+                        % (rank, p, n, logn[p]))
+        f = _merge_checked(shard, cat, n, sent_global and rank == 0 and p == 0, logsum[p], device,
+                           "exchange: rank %d's final merge of sub-log %d" % (rank, p))
+        if f:
+            fail.append(f)
         del cat
         st = shard.build_rdbg()
         n_dbg_loc += int(st.n_dbg)
         n_rdbg_loc += int(st.n_rdbg)
         keys.append(np.ascontiguousarray(shard.owner_rdbg(), dtype=np.uint64))
-    sums = torch.tensor([n_dbg_loc, n_rdbg_loc], dtype=torch.int64, device=comm)
+    sums = torch.tensor([n_dbg_loc, n_rdbg_loc, 1 if fail else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
-    n_dbg, n_rdbg = sums.tolist()
+    n_dbg, n_rdbg, nfail = sums.tolist()
+    if nfail:
+        _raise_if_any(fail[0] if fail else None, [1], rank)
     own = np.sort(np.concatenate(keys)) if keys else np.zeros(0, np.uint64)
     return int(n_dbg), int(n_rdbg), n_rdbg_loc, sent, rounds, own
 
@@ -553,7 +734,13 @@ class GpuShard:
         self.ctx.dbg_load(keys, masks, counts)
 
     def build(self, flags, extra, rc0):
-        return bool(self.ctx.build_dbg(flags, int(extra), bool(rc0)).sentinel)
+        st = self.ctx.build_dbg(flags, int(extra), bool(rc0))
+        self.n_entries = int(st.n_slots)
+        return bool(st.sentinel)
+
+    def entries(self):
+        """canonical entries of the last build or merge (what a partition must hold)"""
+        return self.n_entries
 
     def counts(self):
         _, _, keys, values, counts = self.ctx.dbg_dump()
@@ -566,6 +753,16 @@ class GpuShard:
 
     def merge(self, ptr, n, sentinel=False):
         self.ctx.merge(ptr, n, 0, sentinel)
+        self.n_entries = int(self.ctx.stats().n_slots)
+
+    def merge_check(self):
+        return self.ctx.merge_check()
+
+    def partition_sums(self, nparts):
+        return self.ctx.partition_sums(nparts)
+
+    def rows_checksum(self, d_rows, seg_off):
+        return self.ctx.rows_checksum(d_rows, seg_off)
 
     def build_rdbg(self):
         return self.ctx.build_rdbg()

@@ -153,6 +153,7 @@ class NumpyTable:
         return ((z >> np.uint64(40)) % np.uint64(nparts)).astype(np.int64)
 
     def partition(self, nparts, ptr=None, cap=0):
+        from pangenome_amd.dist import row_check_sum
         own = self._owner(nparts)
         counts = np.bincount(own, minlength=nparts).astype(np.uint64)
         if ptr is not None:
@@ -160,15 +161,29 @@ class NumpyTable:
             order = np.argsort(own, kind="stable")
             buf[:, 0] = (self.c[order] + np.uint64(1)).view(np.int64)
             buf[:, 1] = self.mw[order].view(np.int64)
+            off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+            self.psums = np.array([row_check_sum(buf[off[i]:off[i + 1]]) for i in range(nparts)], np.uint64)
         return counts
 
+    def partition_sums(self, nparts):
+        return self.psums[:nparts]
+
+    def entries(self):
+        return int(self.c.shape[0])
+
     def merge(self, ptr, n, sentinel=False):
+        from pangenome_amd.dist import row_check_sum
         if n:
             buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * n)).from_address(ptr)).reshape(n, 2)
+            self.mcheck = (int(np.count_nonzero(buf[:, 0])), row_check_sum(buf))
             self._set(buf[:, 0].view(np.uint64) - np.uint64(1), buf[:, 1].view(np.uint64))
         else:
+            self.mcheck = (0, 0)
             self.c, self.mw = np.zeros(0, np.uint64), np.zeros(0, np.uint64)
         self.sentinel = sentinel
+
+    def merge_check(self):
+        return self.mcheck
 
     def _members(self):
         a = (self.mw & np.uint64(0xFFF)).astype(np.int64)
@@ -249,8 +264,17 @@ class OracleShard:
     def partition(self, nparts, ptr=None, cap=0):
         return self.table.partition(nparts, ptr, cap)
 
+    def partition_sums(self, nparts):
+        return self.table.partition_sums(nparts)
+
+    def entries(self):
+        return self.table.entries()
+
     def merge(self, ptr, n, sentinel=False):
         self.table.merge(ptr, n, sentinel)
+
+    def merge_check(self):
+        return self.table.merge_check()
 
     def build_rdbg(self):
         return self.table.build_rdbg()

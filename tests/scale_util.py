@@ -43,6 +43,16 @@ INPUTS = {
     # the file's genome-major order (0.5 Gbp; two segments, each twice)
     "c5s": dict(kind="c5", genomes=[0, 1], records=[0, 1], k=27, c=2,
                 desc="C5 form: synth.c5_record(g, r) for g in 0-1, r in 0-1 (4 x 125 Mbp, 1 % SNP, 0.1 % indel)"),
+    # C5 at the streamed exchange's production chunk (2^30 forward bases): the
+    # first 8 records of genome 0 fill one chunk (1.0 Gbp), genome 1's first
+    # two (their 1 %-SNP variants) the next; 1.25 Gbp, ~2.3 G dBG keys, too
+    # many for one in-memory oakht, so digested by key range (pgo_dbg_range)
+    "c5m": dict(kind="c5pairs", pairs=[(0, r) for r in range(8)] + [(1, 0), (1, 1)], k=27, c=2, ranges=32,
+                desc="C5 at 2^30-base chunks: synth.c5_record(0, 0..7), then (1, 0..1) (10 x 125 Mbp)"),
+    # the C5 shard one rank holds at N = 8 (tests/test_gpu_c5.py): genome 0's
+    # 24 records and genome 1's first 6 (3.75 Gbp), digested by key range
+    "c5shard": dict(kind="c5pairs", pairs=[(0, r) for r in range(24)] + [(1, r) for r in range(6)], k=27, c=2,
+                    ranges=96, desc="C5 shard of rank 0 at N = 8: synth.c5_record(0, 0..23), then (1, 0..5)"),
 }
 
 
@@ -53,6 +63,8 @@ def make_input(name: str) -> bytes:
         return synth.ecoli_like()
     if s["kind"] == "c5":
         return b"".join(synth.c5_record(g, r) for g in s["genomes"] for r in s["records"])
+    if s["kind"] == "c5pairs":
+        return b"".join(synth.c5_record(g, r) for g, r in s["pairs"])
     return synth.pangenome(s["n"], s["length"], snp=s["snp"], indel=s["indel"], first_index=s["first"])
 
 

@@ -122,3 +122,79 @@ def test_sublog_count(world, rounds, subparts, want):
     from pangenome_amd.dist import sublog_count
     P = sublog_count(world, rounds, subparts)
     assert P == want and world * P <= 64 and P & (P - 1) == 0
+
+
+def _corrupt_worker(rank, world, port, q, fasta, k, mode):
+    """exchange_and_reduce with one record changed after the sender summed it
+    (mode "send": in rank 1's send buffer, between partition and all-to-all)
+    or in the owner's receive buffer before its merge (mode "merge")."""
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes
+    import torch.distributed as dist
+    from oracle import oracle
+    from pangenome_amd import dist as pdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pdist.A2A_ROWS = 500                          # several pieces per message
+
+    class Bad(NumpyTable):
+        def partition(self, nparts, ptr=None, cap=0):
+            c = super().partition(nparts, ptr, cap)
+            if ptr is not None and mode == "send" and rank == 1 and cap > 1200:
+                buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * cap)).from_address(ptr)).reshape(cap, 2)
+                buf[1200, 1] ^= 1 << 3              # one mask bit of one record
+            return c
+
+        def merge(self, ptr, n, sentinel=False):
+            if mode == "merge" and rank == 0 and n > 10:
+                buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * n)).from_address(ptr)).reshape(n, 2)
+                buf[10, 0] += 1                     # one key
+            super().merge(ptr, n, sentinel)
+
+    if mode == "wire":                            # a piece damaged in flight (the collective's output)
+        real = pdist._all_to_all_rows
+
+        def lossy(recv, send, rsplit, ssplit, *a, **kw):
+            real(recv, send, rsplit, ssplit, *a, **kw)
+            if rank == 0 and rsplit[1] > 1200:
+                recv[int(rsplit[0]) + 1200, 0] += 2
+        pdist._all_to_all_rows = lossy
+
+    recs = _records(fasta)
+    mine = b"".join(r if r.endswith(b"\n") else r + b"\n" for r in recs[rank::world])
+    keys, masks = oracle.OracleRun(mine, k, 2).dbg()
+    t = Bad(k)
+    t.load_dbg(keys, masks)
+    try:
+        pdist.exchange_and_reduce(t, world, rank, "cpu", t.sentinel)
+        q.put((rank, None))
+    except pdist.ExchangeIntegrityError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["send", "wire", "merge"])
+def test_exchange_integrity_check_raises(oracle_mod, mode):
+    """A record changed anywhere between the sender's partition and the
+    owner's merge fails the exchange loudly on every rank, never as a silently
+    wrong count: a change in the sender's buffer after its partition sums
+    (named by the sender), a piece damaged on the wire (the receiver names
+    the source rank and the piece), a change in the owner's log (at the
+    owner's merge)."""
+    from dist_util import spawn_ranks
+    from pangenome_amd import synth
+    fasta = synth.pangenome(6, 30_000, snp=0.01, indel=1e-3, seed=41)
+    out = spawn_ranks(2, _corrupt_worker, (fasta, 27, mode))
+    if mode in ("send", "wire"):
+        for r in range(2):
+            assert out[r] is not None, out
+        owner = [r for r in range(2) if "from rank 1" in out[r]]
+        assert len(owner) == 1 and "stage: all_to_all" in out[owner[0]], out
+        if mode == "send":
+            assert "stage: send buffer" in out[1], out
+        else:
+            assert "pieces [2] of 500 rows each differ on the wire" in out[owner[0]], out
+    else:
+        assert out[0] is not None and "stage: merge" in out[0], out

@@ -68,3 +68,21 @@ def test_sentinel_and_empty(oracle_mod):
     keys, masks = run.dbg()
     assert keys.tolist() == [2 ** 64 - 1] and masks.tolist() == [32]
     assert run.rdbg().tolist() == [2 ** 64 - 1]
+
+
+@pytest.mark.parametrize("name", fixture_names())
+def test_oracle_key_ranges_match_reference(oracle_mod, name):
+    """pgo_dbg_range (the sorted form the benchmark-scale digests use for
+    inputs too big for one oakht) gives the reference's dBG and rdBG range by
+    range, at the fixture's -c, -n and checkpoint settings."""
+    fx = Fixture(name)
+    ks, ms = [], []
+    for lo, hi in oracle_mod.key_ranges(fx.k, 7):
+        k_, m_ = oracle_mod.dbg_range(fx.fasta, fx.k, fx.c, lo, hi, ns=fx.ns)
+        assert np.all(np.diff(k_.astype(np.float64)) >= 0) and np.all((k_ >= lo) & ((k_ < hi) | (k_ == hi)))
+        ks.append(k_)
+        ms.append(m_)
+    keys, masks = np.concatenate(ks), np.concatenate(ms)
+    assert np.array_equal(keys, fx.dbg_keys)
+    assert np.array_equal(masks, fx.dbg_masks)
+    assert np.array_equal(keys[oracle_mod.rdbg_member(masks)], fx.rdbg_keys)
