@@ -61,6 +61,8 @@ typedef struct pg_stats {
                               (PG_TUNE_EARLY_SPLIT) and stage C read them; bits
                               8..15: stages B/C re-runs of the last build (a plan
                               or a capacity that did not hold)                     */
+  uint64_t n_work_items;   /* K3 stage A work-pass items: 16-window segments the
+                              coverage pass left, 64 class bytes read each        */
 } pg_stats;
 
 /* Context on HIP device `device` for k-mer length k (clamped to [1, 27] as

@@ -42,7 +42,7 @@ class PgStats(C.Structure):
         ("ms_parse", C.c_double), ("ms_clear", C.c_double), ("ms_insert", C.c_double),
         ("ms_scan", C.c_double), ("sentinel", C.c_uint64),
         ("n_records_a", C.c_uint64), ("ms_split", C.c_double), ("ms_range", C.c_double),
-        ("build_flags", C.c_uint64),
+        ("build_flags", C.c_uint64), ("n_work_items", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -80,6 +80,9 @@ constexpr int CSTRIDE = 8;                    // counter spacing: one 64-byte li
 // [4] stage B/C bits (a separate 16-byte unit: stage C re-runs clear it alone)
 enum : unsigned { F_OVF_FULL = 1u, F_A_OVER = 2u, F_LDS_SPILL = 4u, F_SPLIT_OVER = 8u, F_RSEG_OVER = 16u };
 constexpr int N_FLAGS = 16;
+// 64-bit counters at these flag indices (cleared with the flags when stage A
+// starts): what a merge read (k_slots_emit) and the work pass's items
+constexpr int F_MERGE_SUM = 8, F_MERGE_ROWS = 10, F_WORK_ITEMS = 12;
 
 // overflow table: linear probing on 16-byte slots (CAS on key1, then OR);
 // a full table sets F_OVF_FULL in *fl (C3: ~2 % of the keys land here, in
@@ -1641,6 +1644,8 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
   __syncthreads();
   uint8_t* slot = scratch[threadIdx.x];
   const unsigned long long n = s_pre[NQ];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && n)                 // the build's work items (pg_stats)
+    atomicAdd(reinterpret_cast<unsigned long long*>(O.flags + F_WORK_ITEMS), n);
   for (unsigned long long i0 = (unsigned long long)blockIdx.x * IBLOCK; i0 < n;
        i0 += (unsigned long long)gridDim.x * IBLOCK) {          // block-uniform trip count
     const unsigned long long i = i0 + threadIdx.x;
@@ -1771,7 +1776,6 @@ k_preload_emit(const PreEnt* __restrict__ e, uint64_t n, TableView T, BinOut O) 
 // records' row_check and the count of non-empty records go to flags[8..9]
 // and flags[10..11] (pg_dbg_merge_check: what the merge read, against what
 // the senders' partition sums say was sent).
-constexpr int F_MERGE_SUM = 8, F_MERGE_ROWS = 10;       // 64-bit words at these flag indices
 __global__ void __launch_bounds__(IBLOCK)
 k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
   __shared__ EmitLds<1> s_emit;
@@ -2727,6 +2731,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
     const unsigned bits = hf[4];
     c.merge_sum = (uint64_t)hf[F_MERGE_SUM] | ((uint64_t)hf[F_MERGE_SUM + 1] << 32);
     c.merge_rows = (uint64_t)hf[F_MERGE_ROWS] | ((uint64_t)hf[F_MERGE_ROWS + 1] << 32);
+    c.work_items = (uint64_t)hf[F_WORK_ITEMS] | ((uint64_t)hf[F_WORK_ITEMS + 1] << 32);
     static const bool dbg_build = std::getenv("PG_DEBUG_BUILD") != nullptr;
     if (dbg_build)
       std::fprintf(stderr, "finish_build attempt %d: total %llu maxreg %llu maxbin %llu bb %d levels %zu rec_max %llu "

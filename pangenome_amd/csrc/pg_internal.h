@@ -146,6 +146,7 @@ struct Ctx {
   hipStream_t stream2 = nullptr;  // side stream: K3 work passes overlap the next coverage pass
   hipStream_t stream3 = nullptr;  // copy stream: chunked host uploads (pg_parse_host, pg_build_host)
   hipEvent_t ev[16] = {};         // ordering events between the two streams
+  hipEvent_t rec_ev = nullptr;    // the record table's copy to the host (K1)
   hipEvent_t cev[16] = {};        // chunk-landed events of the copy stream
   int n_cu = 256;                 // compute units (persistent-kernel grids)
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
@@ -236,6 +237,7 @@ struct Ctx {
   uint64_t part_counts[64] = {};  // counts of the last count pass
   uint64_t part_sums[64] = {};    // row_check sums of the last scatter's runs
   uint64_t merge_sum = 0, merge_rows = 0;   // the last merge: row_check sum / non-empty records it read
+  uint64_t work_items = 0;        // the last build's work-pass items (segments the coverage pass left)
   uint64_t part_total = 0;
   int part_nparts = 0;
   uint64_t part_gen = ~0ull;      // build_gen of the table the counts are for

@@ -32,6 +32,7 @@
 // whose line does not start with '>' (:155).  Lines before the first header
 // land in front of record 0 in the compacted stream and belong to no record
 // (:156-161, qid[0] != 62).  A file without any '\n' has no lines at all.
+#include <chrono>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -306,11 +307,9 @@ __device__ __forceinline__ uint32_t pack_word(const uint4& v, uint32_t& exc) {
 }
 
 __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
-                                                 uint64_t nspan,
-                                                 const Fn* __restrict__ incl, uint64_t rcap,
+                                                 uint64_t nspan, const Fn* __restrict__ incl,
                                                  uint8_t* __restrict__ out, uint32_t* __restrict__ p2,
-                                                 uint8_t* __restrict__ e16, long long* __restrict__ rec_start,
-                                                 long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
+                                                 uint8_t* __restrict__ e16) {
   // pending bytes (< 32) + one step's (<= WSTEP) + the fast step's fifth dword
   constexpr int STAGE = WSTEP + 48;
   __shared__ uint8_t lut[256];
@@ -333,7 +332,7 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
   const uint64_t p0 = span * WSPAN;
   // the prefix function evaluated at the file's in-state (0; byte 0 starts a line)
   const Fn pre = span ? incl[span - 1] : fn_identity();
-  unsigned long long off = pre.c0, rec = pre.hdr;
+  unsigned long long off = pre.c0;
   // stage[0] holds output position cb (16-aligned); bytes below `own` belong
   // to the previous span
   unsigned long long cb = off & ~15ull;
@@ -347,7 +346,7 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
     if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
     const uint64_t pn = p + WSTEP;
     const uint4 vn = (s + 1 < WSTEPS && pn < n) ? load16(buf, pn, n) : make_uint4(0, 0, 0, 0);
-    uint32_t ctot, hcnt = 0;
+    uint32_t ctot;
     // Fast step (wave-uniform): in-state 0, every byte below n - 1, no '>',
     // at most one '\n' per lane and every other byte one of ACGTacgt - the
     // lane's bases are its 16 bytes minus the '\n', classed in registers and
@@ -385,36 +384,18 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
       const LaneStep ls = lane_step(v, p, n, lane, carry);
       const uint32_t region = lane_region(ls, lane_in(ls, state));
       const uint32_t cm = lane_content(ls, region);
-      const uint32_t mine = (uint32_t)__builtin_popcount(cm) | (uint32_t)__builtin_popcount(ls.hs) << 16;
+      const uint32_t mine = (uint32_t)__builtin_popcount(cm);
       const uint32_t incl = wave_incl_sum(mine);
       const uint32_t excl = incl - mine;
       const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
-      const unsigned long long lane_off = off + (excl & 0xFFFFu);
-      const unsigned long long lane_rec = rec + (excl >> 16);
-      // header lines: start (record begins at the next base) and terminator
-      const uint32_t term = region & (ls.nlm | (~ls.vn1 & below_mask(p, n) & (ls.vn1 + 1u)));
-      if (ls.hs | term) {
-        for (uint32_t m = ls.hs; m; m &= m - 1) {
-          const int jj = __builtin_ctz(m);
-          const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((1u << jj) - 1u));
-          if (r >= rcap) continue;                            // the host re-runs with the exact count
-          hdr_start[r] = (long long)(p + jj);
-          rec_start[r] = (long long)(lane_off + __builtin_popcount(cm & ((1u << jj) - 1u)));
-        }
-        for (uint32_t m = term; m; m &= m - 1) {
-          const int jj = __builtin_ctz(m);
-          const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((2u << jj) - 1u)) - 1;
-          if (r < rcap) hdr_end[r] = (long long)(p + jj);
-        }
-      }
+      // (header entries of the record table: k_headers)
       // stage this step's bases after the pending bytes of chunk `cb`
-      uint32_t w = (uint32_t)(off - cb) + (excl & 0xFFFFu);
+      uint32_t w = (uint32_t)(off - cb) + excl;
       const uint32_t words[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int jj = 0; jj < 16; ++jj)
         if ((cm >> jj) & 1u) stage[w++] = lut[(words[jj >> 2] >> (8 * (jj & 3))) & 0xFFu];
-      ctot = tot & 0xFFFFu;
-      hcnt = tot >> 16;
+      ctot = tot;
       state = step_out(ls, state);
     }
     wave_sync();
@@ -446,7 +427,6 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
       wave_sync();
     }
     off += ctot;
-    rec += hcnt;
     v = vn;
     p = pn;
   }
@@ -454,6 +434,58 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
   if (lane < 16) {
     const unsigned long long q = cb + lane;
     if (q >= own && q < off) out[q] = stage[lane];
+  }
+}
+
+// The record table's header entries, before (and beside) the emission: each
+// header's byte span and its record's start in the compacted stream.  Only
+// the spans a header starts in, or whose first line continues one, do any
+// work (C3: ~100 of 31 K spans); they step through their 16 KiB with the
+// general step's line logic and content counts.  With the record table out
+// of k_emit, its round trip to the host runs while the emission does.
+__global__ void __launch_bounds__(PBLOCK) k_headers(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
+                                                    uint64_t nspan, const Fn* __restrict__ incl, uint64_t rcap,
+                                                    long long* __restrict__ rec_start,
+                                                    long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t span = span0 + (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (span >= nspan) return;                                  // wave-uniform
+  const Fn pre = span ? incl[span - 1] : fn_identity();
+  uint32_t state = pre.o & 1u;
+  if (incl[span].hdr == pre.hdr && !state) return;            // no header starts or ends here
+  const uint64_t p0 = span * WSPAN;
+  unsigned long long off = pre.c0, rec = pre.hdr;
+  uint32_t carry = p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u);
+  for (int s = 0; s < WSTEPS; ++s) {
+    if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
+    const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
+    const uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+    const LaneStep ls = lane_step(v, p, n, lane, carry);
+    const uint32_t region = lane_region(ls, lane_in(ls, state));
+    const uint32_t cm = lane_content(ls, region);
+    const uint32_t mine = (uint32_t)__builtin_popcount(cm) | (uint32_t)__builtin_popcount(ls.hs) << 16;
+    const uint32_t incl_l = wave_incl_sum(mine);
+    const uint32_t excl = incl_l - mine;
+    const uint32_t tot = __builtin_amdgcn_readlane(incl_l, 63);
+    const unsigned long long lane_off = off + (excl & 0xFFFFu);
+    const unsigned long long lane_rec = rec + (excl >> 16);
+    // header lines: start (record begins at the next base) and terminator
+    const uint32_t term = region & (ls.nlm | (~ls.vn1 & below_mask(p, n) & (ls.vn1 + 1u)));
+    for (uint32_t m = ls.hs; m; m &= m - 1) {
+      const int jj = __builtin_ctz(m);
+      const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((1u << jj) - 1u));
+      if (r >= rcap) continue;                                // the host re-runs with the exact count
+      hdr_start[r] = (long long)(p + jj);
+      rec_start[r] = (long long)(lane_off + __builtin_popcount(cm & ((1u << jj) - 1u)));
+    }
+    for (uint32_t m = term; m; m &= m - 1) {
+      const int jj = __builtin_ctz(m);
+      const unsigned long long r = lane_rec + __builtin_popcount(ls.hs & ((2u << jj) - 1u)) - 1;
+      if (r < rcap) hdr_end[r] = (long long)(p + jj);
+    }
+    off += tot & 0xFFFFu;
+    rec += tot >> 16;
+    state = step_out(ls, state);
   }
 }
 
@@ -536,7 +568,7 @@ static void upload_byte_class(int device) {
 // spans - so only the last chunk's K1 follows the copy.
 void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t)>* on_chunk) {
   upload_byte_class(c.device);
-  hipStream_t st = c.stream;
+  const hipStream_t st = c.stream;
   const uint64_t n = c.n_bytes;
   c.parsed = false;
   c.n_lines = c.n_records = c.n_bases = c.n_nl = 0;
@@ -548,6 +580,8 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     return;
   }
 
+  c.t0.init();
+  c.t0.start(st);
   const uint64_t nspan = (n + WSPAN - 1) / WSPAN;
   const unsigned nblk = (unsigned)((nspan + WAVES - 1) / WAVES);
   c.span_sum.reserve(sizeof(Fn) * nspan);
@@ -576,19 +610,47 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     c.rec_pack.reserve(64 + 40 * rcap);
     c.h_pin.reserve(64 + 40 * rcap);
   };
-  auto emit = [&](uint64_t s0, uint64_t s1, uint64_t rcap) {
-    auto* hdr = c.rec_hdr.as<long long>();
+  auto emit = [&](uint64_t s0, uint64_t s1) {
     hipLaunchKernelGGL(k_emit, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta, n, s0,
-                       s1, incl, rcap, c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>(),
-                       c.rec_start.as<long long>(), hdr, hdr + rcap);
+                       s1, incl, c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>());
     PG_HIP(hipGetLastError());
     // boundaries s0 .. s1 (s1 = nspan: the stream's end, incl[nspan - 1])
     hipLaunchKernelGGL(k_pack_fix, dim3(grid_for(s1 - s0 + 1, 256, 65535)), dim3(256), 0, st, incl, s0, s1,
                        c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>());
     PG_HIP(hipGetLastError());
   };
+  // the header entries of spans s0 .. s1 (k_headers), then the record table
+  // of the spans so far (k_records, total = incl[s1 - 1]) and its copy to the
+  // host, marked by rec_ev: queued before the spans' emission, so the host
+  // reads the table while the emission runs
+  auto records = [&](uint64_t s0, uint64_t s1, uint64_t rcap) {
+    auto* hdr = c.rec_hdr.as<long long>();
+    hipLaunchKernelGGL(k_headers, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta, n,
+                       s0, s1, incl, rcap, c.rec_start.as<long long>(), hdr, hdr + rcap);
+    PG_HIP(hipGetLastError());
+  };
+  auto table_copy = [&](uint64_t s1, uint64_t rcap) {
+    hipLaunchKernelGGL(k_records, dim3(grid_for(rcap, 256, 1024)), dim3(256), 0, st, incl + s1 - 1, n, rcap,
+                       c.rec_start.as<long long>(), c.rec_hdr.as<long long>(), c.rec_len.as<long long>(),
+                       c.rec_pack.as<long long>());
+    PG_HIP(hipGetLastError());
+    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 64 + 40 * rcap, hipMemcpyDeviceToHost, st));
+    PG_HIP(hipEventRecord(c.rec_ev, st));
+  };
+  // (a polling wait, as Ctx::sync: a blocking wait's wake-up is on the path)
+  auto table_wait = [&]() {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t e = hipEventQuery(c.rec_ev);
+      if (e == hipSuccess) return;
+      if (e != hipErrorNotReady) break;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50)) break;
+    }
+    PG_HIP(hipEventSynchronize(c.rec_ev));
+  };
   reserve_records(rcap0);
   bool streaming = on_chunk != nullptr;
+  std::pair<uint64_t, uint64_t> pending{0, 0};               // spans whose emission follows the table's copy
   // (the stager's last work - waiting for the DMAs and unregistering the
   // chunks' pages - is waited for right after the last chunk's K1 is queued:
   // left to run beside the last record round trip and stage A share, its
@@ -622,16 +684,20 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
                          n, s0, s1, fns);
       PG_HIP(hipGetLastError());
       scan(s1);
-      emit(s0, s1, rcap0);
-      if (!streaming || i + 1 == nch) continue;
+      records(s0, s1, rcap0);
+      if (i + 1 == nch) {                                     // (after the final table's copy, below)
+        pending = {s0, s1};
+        continue;
+      }
+      if (!streaming) {
+        emit(s0, s1);
+        continue;
+      }
       // the records complete so far (every header seen but the last one):
-      // the host waits for this chunk's K1 while the copies go on
-      auto* hdr = c.rec_hdr.as<long long>();
-      hipLaunchKernelGGL(k_records, dim3(grid_for(rcap0, 256, 1024)), dim3(256), 0, st, incl + s1 - 1, n, rcap0,
-                         c.rec_start.as<long long>(), hdr, c.rec_len.as<long long>(), c.rec_pack.as<long long>());
-      PG_HIP(hipGetLastError());
-      PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 64 + 40 * rcap0, hipMemcpyDeviceToHost, st));
-      c.sync();
+      // the host reads them while this chunk's emission and the copies go on
+      table_copy(s1, rcap0);
+      emit(s0, s1);
+      table_wait();
       const Fn t = *c.h_pin.as<Fn>();
       const uint64_t Rs = t.nl ? t.hdr : 0;
       if (Rs > rcap0) { streaming = false; continue; }        // more records than the arrays hold
@@ -647,26 +713,29 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
     PG_HIP(hipGetLastError());
     scan(nspan);
-    emit(0, nspan, rcap0);
+    records(0, nspan, rcap0);
+    pending = {0, nspan};
   }
-  // Emission and the record table are queued behind the scan with no host
-  // round trip: the class stream is sized by the file (bases < n), the
-  // record arrays by the last parse's record count (re-run if exceeded).
+  // The record table's copy is queued behind the header pass and ahead of the
+  // (last) emission, with no host round trip before it: the class stream is
+  // sized by the file (bases < n), the record arrays by the last parse's
+  // record count (the header pass re-run with the exact count if exceeded).
   static_assert(sizeof(Fn) <= 64, "the total in front of the packed record table");
   uint64_t R = 0;
   Fn tot{};
   for (int attempt = 0; attempt < 2; ++attempt) {
     const uint64_t rcap = attempt ? std::max<uint64_t>(c.rec_cap, 64) : rcap0;
-    if (attempt) {                                            // the exact record count: emission again
+    if (attempt) {                                            // the exact record count: the header pass again
       reserve_records(rcap);
-      emit(0, nspan, rcap);
+      records(0, nspan, rcap);
     }
-    auto* hdr = c.rec_hdr.as<long long>();
-    hipLaunchKernelGGL(k_records, dim3(grid_for(rcap, 256, 1024)), dim3(256), 0, st, incl + nspan - 1, n, rcap,
-                       c.rec_start.as<long long>(), hdr, c.rec_len.as<long long>(), c.rec_pack.as<long long>());
-    PG_HIP(hipGetLastError());
-    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 64 + 40 * rcap, hipMemcpyDeviceToHost, st));
-    c.sync();
+    table_copy(nspan, rcap);
+    if (pending.second > pending.first) {
+      emit(pending.first, pending.second);
+      pending = {0, 0};
+      c.t0.stop(st);                                          // K1's end on the stream
+    }
+    table_wait();
     tot = *c.h_pin.as<Fn>();
     R = tot.nl ? tot.hdr : 0;
     if (R <= rcap) {

@@ -8,11 +8,13 @@
 //       `counts` are occurrences per oriented key (__setitem__ :556),
 //       something the OR-table does not keep;
 //   k_count_staged   staged npz slots add their own counts (-r resume);
-//   k_dump_place     each present oriented key claims the first free slot of
-//       oakht.pointer's probe sequence (:521-538): j = FNV-1a(low 4 key bytes)
-//       mod capacity, then j, j+1, j+4, j+9, ... .  Any insertion order gives a
-//       layout lookups accept: a key's earlier probes were occupied when it
-//       was placed and nothing is ever removed.
+//   k_dump_list / k_dump_propose / k_dump_claim   each present oriented key
+//       takes a free slot of oakht.pointer's probe sequence (:521-538): j =
+//       FNV-1a(low 4 key bytes) mod capacity, then j, j+1, j+4, j+9, ... .
+//       Any insertion order gives a layout lookups accept (a key's earlier
+//       probes were occupied when it was placed and nothing is ever removed);
+//       rounds in which the smallest proposing key takes each slot make it
+//       the same layout on every run.
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -129,32 +131,63 @@ __host__ __device__ __forceinline__ uint64_t oak_fnv(uint64_t x) {
   return a;
 }
 
-__global__ void k_dump_place(TableView T, uint64_t nw, uint64_t ntot, const unsigned* __restrict__ cnt, uint64_t M,
-                             unsigned* __restrict__ occ, unsigned long long* __restrict__ okeys,
-                             unsigned short* __restrict__ ovals, unsigned char* __restrict__ ocnts,
-                             unsigned* __restrict__ fail) {
+// The slot placement, deterministic: in rounds, every oriented key not yet
+// placed proposes the first slot of its probe sequence that no earlier round
+// filled (atomicMin of key + 1 on the slot's proposal word), and the
+// smallest proposer takes each proposed slot; the others go on from there
+// next round.  Which slot a key ends in depends only on the set of keys, not
+// on the order threads run (one racing pass gave a different, equally valid
+// layout per run), so two dumps of one build are byte-equal.
+struct PendEnt {                                   // an oriented key waiting for its slot
+  unsigned long long x;
+  uint32_t vc;                                     // value | count << 16
+  uint32_t probe;                                  // probe index kk of its next try
+};
+__global__ void k_dump_list(TableView T, uint64_t nw, uint64_t ntot, const unsigned* __restrict__ cnt,
+                            PendEnt* __restrict__ out, unsigned long long* __restrict__ nout) {
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < ntot;
        i += (uint64_t)gridDim.x * blockDim.x) {
     const uint32_t m = entry_mask(T, nw, i);
-    if (!(m & (PRES_A | PRES_B))) continue;
+    const uint32_t np = ((m & PRES_A) ? 1u : 0u) + ((m & PRES_B) ? 1u : 0u);
+    if (!np) continue;
     const uint64_t c = entry_key(T, nw, i);
+    unsigned long long at = atomicAdd(nout, (unsigned long long)np);
     for (int o = 0; o < 2; ++o) {
       if (!(m & (o ? PRES_B : PRES_A))) continue;
-      const uint64_t x = o ? T.rc(c) : c;
-      const unsigned short v = (unsigned short)((o ? (m >> B_SHIFT) : m) & MASK12);
       const unsigned n = cnt[2 * i + o];
-      const uint64_t j0 = oak_fnv(x) % M;
-      bool placed = false;
-      for (uint64_t kk = 0; kk < M && !placed; ++kk) {
-        const uint64_t s = (j0 + kk * kk) % M;
-        if (atomicCAS(occ + s, 0u, 1u) == 0u) {
-          okeys[s] = x;
-          ovals[s] = v;
-          ocnts[s] = (unsigned char)(n > 255u ? 255u : (n ? n : 1u));
-          placed = true;
-        }
-      }
-      if (!placed) atomicOr(fail, 1u);
+      const uint32_t v = (o ? (m >> B_SHIFT) : m) & MASK12;
+      const uint32_t cn = n > 255u ? 255u : (n ? n : 1u);
+      out[at++] = PendEnt{o ? T.rc(c) : c, v | (cn << 16), 0u};
+    }
+  }
+}
+__device__ __forceinline__ uint64_t oak_probe(uint64_t j0, uint64_t kk, uint64_t M) { return (j0 + kk * kk) % M; }
+
+__global__ void k_dump_propose(PendEnt* __restrict__ e, uint64_t n, uint64_t M, const unsigned char* __restrict__ ocnts,
+                               unsigned long long* __restrict__ prop, unsigned* __restrict__ fail) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    PendEnt p = e[i];
+    const uint64_t j0 = oak_fnv(p.x) % M;
+    uint64_t kk = p.probe;
+    while (kk < M && ocnts[oak_probe(j0, kk, M)]) ++kk;     // (filled slots are final)
+    if (kk >= M) { atomicOr(fail, 1u); continue; }
+    e[i].probe = (uint32_t)kk;
+    atomicMin(prop + oak_probe(j0, kk, M), p.x + 1ull);
+  }
+}
+__global__ void k_dump_claim(const PendEnt* __restrict__ e, uint64_t n, uint64_t M,
+                             const unsigned long long* __restrict__ prop, unsigned long long* __restrict__ okeys,
+                             unsigned short* __restrict__ ovals, unsigned char* __restrict__ ocnts,
+                             PendEnt* __restrict__ left, unsigned long long* __restrict__ nleft) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const PendEnt p = e[i];
+    const uint64_t s = oak_probe(oak_fnv(p.x) % M, p.probe, M);
+    if (prop[s] == p.x + 1ull) {                  // the smallest key that proposed s
+      okeys[s] = p.x;
+      ovals[s] = (unsigned short)(p.vc & 0xFFFFu);
+      ocnts[s] = (unsigned char)(p.vc >> 16);
+    } else {
+      left[atomicAdd(nleft, 1ull)] = PendEnt{p.x, p.vc, p.probe + 1u};
     }
   }
 }
@@ -270,23 +303,47 @@ struct DumpSlots {
 };
 static void dump_place(Ctx& c, uint64_t M, DumpSlots& d) {
   const uint64_t nw = 2 * c.cap, ntot = nw + c.ovf_cap;
-  DevBuf occ, fail;
-  occ.reserve(4 * M); d.ok.reserve(8 * M); d.ov.reserve(2 * M); d.oc.reserve(M); fail.reserve(4);
-  PG_HIP(hipMemsetAsync(occ.p, 0, 4 * M, c.stream));
+  const uint64_t npend = c.dump_size - (c.sentinel ? 1 : 0);
+  DevBuf prop, fail, lst[2], cnt;
+  prop.reserve(8 * M); d.ok.reserve(8 * M); d.ov.reserve(2 * M); d.oc.reserve(M); fail.reserve(4);
+  cnt.reserve(16);
+  for (auto& b : lst) b.reserve(sizeof(PendEnt) * std::max<uint64_t>(npend, 1));
+  PG_HIP(hipMemsetAsync(prop.p, 0xFF, 8 * M, c.stream));
   PG_HIP(hipMemsetAsync(d.ok.p, 0, 8 * M, c.stream));
   PG_HIP(hipMemsetAsync(d.ov.p, 0, 2 * M, c.stream));
   PG_HIP(hipMemsetAsync(d.oc.p, 0, M, c.stream));
   PG_HIP(hipMemsetAsync(fail.p, 0, 4, c.stream));
-  hipLaunchKernelGGL(k_dump_place, dim3(grid_for(ntot, 256, 8192)), dim3(256), 0, c.stream, c.tv, nw, ntot,
-                     c.dump_cnt.as<unsigned>(), M, occ.as<unsigned>(), d.ok.as<unsigned long long>(),
-                     d.ov.as<unsigned short>(), d.oc.as<unsigned char>(), fail.as<unsigned>());
+  PG_HIP(hipMemsetAsync(cnt.p, 0, 16, c.stream));
+  auto* nc = cnt.as<unsigned long long>();
+  hipLaunchKernelGGL(k_dump_list, dim3(grid_for(ntot, 256, 8192)), dim3(256), 0, c.stream, c.tv, nw, ntot,
+                     c.dump_cnt.as<unsigned>(), lst[0].as<PendEnt>(), nc);
   PG_HIP(hipGetLastError());
-  unsigned failed = 0;
-  PG_HIP(hipMemcpyAsync(&failed, fail.p, 4, hipMemcpyDeviceToHost, c.stream));
+  unsigned long long n = 0;
+  PG_HIP(hipMemcpyAsync(&n, nc, 8, hipMemcpyDeviceToHost, c.stream));
   c.sync();
-  occ.release();
+  if (n != npend) throw Error(-5, "pg_dbg_dump: " + std::to_string(n) + " present keys, counted " + std::to_string(npend));
+  for (int round = 0, a = 0; n; ++round, a ^= 1) {
+    if (round > 100000) throw Error(-5, "pg_dbg_dump: slot placement does not converge");
+    const unsigned g = grid_for(n, 256, 8192);
+    hipLaunchKernelGGL(k_dump_propose, dim3(g), dim3(256), 0, c.stream, lst[a].as<PendEnt>(), n, M,
+                       d.oc.as<unsigned char>(), prop.as<unsigned long long>(), fail.as<unsigned>());
+    PG_HIP(hipGetLastError());
+    PG_HIP(hipMemsetAsync(nc + 1, 0, 8, c.stream));
+    hipLaunchKernelGGL(k_dump_claim, dim3(g), dim3(256), 0, c.stream, lst[a].as<PendEnt>(), n, M,
+                       prop.as<unsigned long long>(), d.ok.as<unsigned long long>(), d.ov.as<unsigned short>(),
+                       d.oc.as<unsigned char>(), lst[a ^ 1].as<PendEnt>(), nc + 1);
+    PG_HIP(hipGetLastError());
+    unsigned h[2] = {0u, 0u};
+    unsigned long long left = 0;
+    PG_HIP(hipMemcpyAsync(&left, nc + 1, 8, hipMemcpyDeviceToHost, c.stream));
+    PG_HIP(hipMemcpyAsync(h, fail.p, 4, hipMemcpyDeviceToHost, c.stream));
+    c.sync();
+    if (h[0]) throw Error(-34, "pg_dbg_dump: a key found no free slot on its probe sequence");
+    n = left;
+  }
+  prop.release();
   fail.release();
-  if (failed) throw Error(-34, "pg_dbg_dump: a key found no free slot on its probe sequence");
+  for (auto& b : lst) b.release();
   if (c.sentinel) {                                  // key 2^64-1, mask '$' (:1087-1088)
     const uint64_t j0 = oak_fnv(SENTINEL) % M;
     uint64_t kk = 0, s = j0;

@@ -95,6 +95,7 @@ SELF_COPY = os.environ.get("PG_EXCHANGE_SELF_RCCL") != "1"
 # env PG_DEBUG_POISON=<byte>: the exchange's torch buffers are filled with it
 # before use (pg_tune PG_TUNE_POISON does the same for the library's own)
 _POISON = os.environ.get("PG_DEBUG_POISON")
+_NO_FENCE = os.environ.get("PG_DEBUG_NO_FENCE") == "1"
 
 
 class ExchangeIntegrityError(RuntimeError):
@@ -108,8 +109,9 @@ def _fence(device):
     torch's: before native code reads or writes memory the torch allocator
     handed out, everything torch's streams (the current one, RCCL's) queued
     must be done — a block freed behind queued work (a clone, a collective)
-    is handed out again at once to the next torch.empty on the same stream."""
-    if _is_cuda(device):
+    is handed out again at once to the next torch.empty on the same stream.
+    (PG_DEBUG_NO_FENCE=1, diagnostics only: round 4's unfenced behaviour.)"""
+    if _is_cuda(device) and not _NO_FENCE:
         import torch
         torch.cuda.synchronize(device)
 

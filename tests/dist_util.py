@@ -84,6 +84,40 @@ def oak_place(keys_in, vals_in, cnts_in, M):
     return keys, vals, cnts
 
 
+def oak_place_rounds(keys_in, vals_in, cnts_in, M):
+    """pg_dbg_dump's deterministic placement restated (test helper): in
+    rounds, every unplaced key proposes the first still-empty slot of its
+    oakht.pointer probe sequence from where it stands, and the smallest key
+    proposing a slot takes it; then the n<k sentinel at the first empty slot
+    of its sequence."""
+    keys = np.zeros(M, np.uint64)
+    vals = np.zeros(M, np.uint16)
+    cnts = np.zeros(M, np.uint8)
+    trip = list(zip(keys_in.tolist(), vals_in.tolist(), cnts_in.tolist()))
+    sent = [t for t in trip if t[0] == SENTINEL]
+    pend = [(int(x), int(v), int(c), 0) for x, v, c in trip if x != SENTINEL]
+    while pend:
+        prop, nxt = {}, []
+        for i, (x, v, c, kk) in enumerate(pend):
+            j0 = oak_fnv(x) % M
+            while cnts[(j0 + kk * kk) % M]:
+                kk += 1
+            pend[i] = (x, v, c, kk)
+            s = (j0 + kk * kk) % M
+            prop[s] = min(prop.get(s, x), x)
+        for x, v, c, kk in pend:
+            s = (oak_fnv(x) % M + kk * kk) % M
+            if prop[s] == x:
+                keys[s], vals[s], cnts[s] = x, v, c
+            else:
+                nxt.append((x, v, c, kk + 1))
+        pend = nxt
+    for x, v, c in sent:
+        j = oak_slot(keys, cnts, x)
+        keys[j], vals[j], cnts[j] = x, v, c
+    return keys, vals, cnts
+
+
 def _isprime(n):
     if n <= 1 or n % 2 == 0 or n % 3 == 0:
         return False

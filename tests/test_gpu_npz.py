@@ -62,11 +62,13 @@ def test_dump_matches_reference_dump(name, tmp_path):
 @pytest.mark.parametrize("name", _graph_fixtures())
 def test_native_dump_file_equals_host_write(name, tmp_path):
     """pg_dbg_dump_fd (slot arrays streamed from the device into the file,
-    kmer.dump) writes what pg_dbg_dump + host.write_db_npz write: a valid zip
-    (every CRC), the same parameters and the same (key, value, count) slots,
-    the n<k sentinel's included, each where oakht.pointer looks for it.  (The
-    slot a key takes among colliding probe sequences depends on which thread
-    claims first, so two dumps need not be byte-equal.)"""
+    kmer.dump) writes what pg_dbg_dump + host.write_db_npz write, byte for
+    byte: a valid zip (every CRC), the same parameters and (key, value,
+    count) slots, the n<k sentinel's included, each where oakht.pointer looks
+    for it.  The slot placement is deterministic (the smallest proposing key
+    takes a contested slot), so a dump of the same input from a fresh build
+    in a fresh context is byte-equal too, and equals the host restatement of
+    the placement rule (dist_util.oak_place_rounds)."""
     import zipfile
     from pangenome_amd import host, kmer
     fx = Fixture(name)
@@ -91,6 +93,15 @@ def test_native_dump_file_equals_host_write(name, tmp_path):
     sample = idx if idx.shape[0] <= 5000 else idx[np.random.default_rng(1).choice(idx.shape[0], 5000, False)]
     for j in sample.tolist():
         assert oak_slot(ka, ca, int(ka[j])) == j
+    a_bytes = (tmp_path / "a_db.npz").read_bytes()
+    assert a_bytes == (tmp_path / "b_db.npz").read_bytes()
+    g2 = kmer.seq2rdbg(str(q), fx.k, 5, Ns, brkpt="", chunk=2 ** 33, rc=(fx.c >> 1) == 1)
+    kmer.dump(g2, str(tmp_path / "c_db"))
+    assert (tmp_path / "c_db.npz").read_bytes() == a_bytes
+    if sa.sum() <= 20000:
+        from dist_util import oak_place_rounds
+        K, V, C = oak_place_rounds(ka[sa], va[sa], ca[sa], cap)
+        assert np.array_equal(K, ka) and np.array_equal(V, va) and np.array_equal(C, ca)
 
 
 def _run_cli(argv):

@@ -336,6 +336,7 @@ def test_build_device_one_call(oracle_mod):
         refs.append((_rec_table(b), dk, dm, o.rdbg()))
     ctx = Context(27)
     dev = [torch.frombuffer(bytearray(b), dtype=torch.uint8).to("cuda") for b in bufs]
+    torch.cuda.synchronize()
     for i in (0, 1, 2, 3, 0, 0, 3, 1):
         st = ctx.build_device(dev[i].data_ptr(), dev[i].numel(), True, keepalive=dev[i])
         rec, dk, dm, rk = refs[i]
