@@ -80,9 +80,9 @@ constexpr int CSTRIDE = 8;                    // counter spacing: one 64-byte li
 // [4] stage B/C bits (a separate 16-byte unit: stage C re-runs clear it alone)
 enum : unsigned { F_OVF_FULL = 1u, F_A_OVER = 2u, F_LDS_SPILL = 4u, F_SPLIT_OVER = 8u, F_RSEG_OVER = 16u };
 constexpr int N_FLAGS = 16;
-// 64-bit counters at these flag indices (cleared with the flags when stage A
-// starts): what a merge read (k_slots_emit) and the work pass's items
-constexpr int F_MERGE_SUM = 8, F_MERGE_ROWS = 10, F_WORK_ITEMS = 12;
+// a 64-bit counter at this flag index (cleared with the flags when stage A
+// starts): the work pass's items (one atomic per launch)
+constexpr int F_WORK_ITEMS = 12;
 
 // overflow table: linear probing on 16-byte slots (CAS on key1, then OR);
 // a full table sets F_OVF_FULL in *fl (C3: ~2 % of the keys land here, in
@@ -1773,14 +1773,19 @@ k_preload_emit(const PreEnt* __restrict__ e, uint64_t n, TableView T, BinOut O) 
 
 // Exchange records a multi-GPU owner received (pg_dbg_merge): canonical key
 // + 1 and the 26-bit mask word of both orientations.  The sum of the
-// records' row_check and the count of non-empty records go to flags[8..9]
-// and flags[10..11] (pg_dbg_merge_check: what the merge read, against what
-// the senders' partition sums say was sent).
+// records' row_check and the count of non-empty records go to `chk`
+// (pg_dbg_merge_check: what the merge read, against what the senders'
+// partition sums say was sent).
+// (the sums: one per block, spread over MCHK slot pairs of `chk` so that no
+// address takes more than a few hundred atomics - thousands on one line
+// serialise at the memory side: 0.65 ms on C3's world-1 merge)
+constexpr int MCHK = 64;
 __global__ void __launch_bounds__(IBLOCK)
-k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
+k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsigned long long* __restrict__ chk) {
   __shared__ EmitLds<1> s_emit;
   __shared__ unsigned long long st_key[EST];
   __shared__ uint32_t st_mw[EST];
+  __shared__ unsigned long long s_chk[2][IBLOCK / 64];
   if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
   __syncthreads();
   unsigned long long acc = 0ull, live = 0ull;
@@ -1804,9 +1809,19 @@ k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O) {
     acc += __shfl_down(acc, o, 64);
     live += __shfl_down(live, o, 64);
   }
-  if ((threadIdx.x & 63) == 0 && (acc || live)) {
-    atomicAdd(reinterpret_cast<unsigned long long*>(O.flags + F_MERGE_SUM), acc);
-    atomicAdd(reinterpret_cast<unsigned long long*>(O.flags + F_MERGE_ROWS), live);
+  if ((threadIdx.x & 63) == 0) {
+    s_chk[0][threadIdx.x >> 6] = acc;
+    s_chk[1][threadIdx.x >> 6] = live;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long a = 0ull, l = 0ull;
+    for (int w = 0; w < IBLOCK / 64; ++w) { a += s_chk[0][w]; l += s_chk[1][w]; }
+    if (a || l) {
+      unsigned long long* slot = chk + 2 * (blockIdx.x % MCHK);
+      atomicAdd(slot, a);
+      atomicAdd(slot + 1, l);
+    }
   }
 }
 
@@ -2288,9 +2303,11 @@ __global__ void k_part_count(TableView T, uint64_t nw, uint64_t ntot, int nparts
 // shared owner cursors serialised ~8 M same-address atomics at the memory
 // side for a C3 table, tens of ms; see NQ above.)  Record order inside an
 // owner's run is arbitrary: the owner OR-merges them.
-// Each owner's run also gets the sum of its records' row_check (sums[owner]:
-// one LDS sum per block, one global atomic per block and owner at the end).
+// Each owner's run also gets the sum of its records' row_check (one LDS sum
+// per block; at the end one global atomic per block and owner, into one of
+// CSPR words per owner, sums[owner * CSPR + block % CSPR], which the host adds).
 constexpr int PT = 256, PE = 8, PCH = PT * PE;
+constexpr int CSPR = 16;
 __global__ void __launch_bounds__(PT)
 k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts, unsigned long long* __restrict__ cursor,
                Slot* __restrict__ out, unsigned long long* __restrict__ sums) {
@@ -2325,11 +2342,13 @@ k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts, unsigned lon
     __syncthreads();
   }
   __syncthreads();
-  if ((int)threadIdx.x < nparts && s_sum[threadIdx.x]) atomicAdd(&sums[threadIdx.x], s_sum[threadIdx.x]);
+  if ((int)threadIdx.x < nparts && s_sum[threadIdx.x])
+    atomicAdd(&sums[threadIdx.x * CSPR + (blockIdx.x % CSPR)], s_sum[threadIdx.x]);
 }
 
 // Sums of row_check over segments of 16-byte records: segment s = records
-// [off[s], off[s+1]) (grid row s), one atomic per block.
+// [off[s], off[s+1]) (grid row s), one atomic per block into
+// sums[s * CSPR + block % CSPR].
 constexpr int RS_SEG = 32;
 struct SegOff { unsigned long long o[RS_SEG + 1]; };
 __global__ void __launch_bounds__(256) k_rows_sum(const Slot* __restrict__ rows, SegOff so,
@@ -2347,7 +2366,7 @@ __global__ void __launch_bounds__(256) k_rows_sum(const Slot* __restrict__ rows,
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long t = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-    if (t) atomicAdd(&sums[s], t);
+    if (t) atomicAdd(&sums[s * CSPR + (blockIdx.x % CSPR)], t);
   }
 }
 
@@ -2366,11 +2385,11 @@ __global__ void k_gather_segs(const unsigned long long* __restrict__ seg, uint64
 // the flags and (spec) stage A's region cursors, copied into pinned host
 // memory by plain vector stores (three DMA copies cost ~20 us of copy-engine
 // starts on the critical path).
-struct Gather { const unsigned long long* src[3]; uint32_t n[3], stride[3]; };
+struct Gather { const unsigned long long* src[4]; uint32_t n[4], stride[4]; };
 __global__ void __launch_bounds__(256) k_gather_out(Gather g, unsigned long long* __restrict__ dst) {
   uint32_t o = 0;
 #pragma unroll
-  for (int j = 0; j < 3; ++j) {
+  for (int j = 0; j < 4; ++j) {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < g.n[j]; i += gridDim.x * 256u)
       dst[o + i] = g.src[j][(uint64_t)i * g.stride[j]];
     o += g.n[j];
@@ -2494,9 +2513,9 @@ static BinOut stageA_begin(Ctx& c, uint64_t cap, FillList& fl, bool reset = true
     c.recA_key.reserve(8 * NREG * cap);
     c.recA_mw.reserve(4 * NREG * cap);
     c.ctrA.reserve(8 * CSTRIDE * NREG);
-    c.flags.reserve(4 * N_FLAGS);
+    c.flags.reserve(4 * N_FLAGS + 16 * MCHK);      // the flags, then the merge's checksum slots
     fl.add(c.ctrA.p, 8 * CSTRIDE * NREG);
-    fl.add(c.flags.p, 4 * N_FLAGS);
+    fl.add(c.flags.p, 4 * N_FLAGS + 16 * MCHK);
   }
   cap = c.capA;
   return BinOut{c.recA_key.as<unsigned long long>(), c.recA_mw.as<uint32_t>(), c.ctrA.as<unsigned long long>(),
@@ -2706,10 +2725,11 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
     // one readback: stage C's counters, the flags, (spec) stage A's cursors
     // (one word per region: stride CSTRIDE on the device, 1 in the copy)
     const size_t kbytes = 8 * RB_CTR * grid, abytes = spec ? 8 * NREG : 0;
-    c.h_out.reserve(kbytes + 4 * N_FLAGS + abytes);
-    Gather gth{{c.k5_ctr.as<unsigned long long>(), c.flags.as<unsigned long long>(), c.ctrA.as<unsigned long long>()},
-               {(uint32_t)(RB_CTR * grid), (uint32_t)(N_FLAGS / 2), spec ? (uint32_t)NREG : 0u},
-               {1u, 1u, (uint32_t)CSTRIDE}};
+    c.h_out.reserve(kbytes + 4 * N_FLAGS + abytes + 16 * MCHK);
+    Gather gth{{c.k5_ctr.as<unsigned long long>(), c.flags.as<unsigned long long>(), c.ctrA.as<unsigned long long>(),
+                c.flags.as<unsigned long long>() + N_FLAGS / 2},
+               {(uint32_t)(RB_CTR * grid), (uint32_t)(N_FLAGS / 2), spec ? (uint32_t)NREG : 0u, 2u * MCHK},
+               {1u, 1u, (uint32_t)CSTRIDE, 1u}};
     hipLaunchKernelGGL(k_gather_out, dim3(4), dim3(256), 0, c.stream, gth,
                        reinterpret_cast<unsigned long long*>(c.h_out.dp));
     PG_HIP(hipGetLastError());
@@ -2729,8 +2749,14 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
       if (a.bits & F_A_OVER) return false;
     }
     const unsigned bits = hf[4];
-    c.merge_sum = (uint64_t)hf[F_MERGE_SUM] | ((uint64_t)hf[F_MERGE_SUM + 1] << 32);
-    c.merge_rows = (uint64_t)hf[F_MERGE_ROWS] | ((uint64_t)hf[F_MERGE_ROWS + 1] << 32);
+    {                                          // the merge's checksum slots (zero for a build)
+      const unsigned long long* mk =
+          reinterpret_cast<const unsigned long long*>(c.h_out.as<uint8_t>() + kbytes + 4 * N_FLAGS + abytes);
+      uint64_t s = 0, r = 0;
+      for (int j = 0; j < MCHK; ++j) s += mk[2 * j], r += mk[2 * j + 1];
+      c.merge_sum = s;
+      c.merge_rows = r;
+    }
     c.work_items = (uint64_t)hf[F_WORK_ITEMS] | ((uint64_t)hf[F_WORK_ITEMS + 1] << 32);
     static const bool dbg_build = std::getenv("PG_DEBUG_BUILD") != nullptr;
     if (dbg_build)
@@ -3086,14 +3112,17 @@ uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap) {
   return c.n_rdbg;
 }
 
+// part_cnt words: [0, 64) counts, [64, 128) cursors, [PCW_SUMS, +64 * CSPR)
+// the partition sums, [PCW_ROWS, +RS_SEG * CSPR) rows_checksum's sums
+constexpr size_t PCW_SUMS = 128, PCW_ROWS = PCW_SUMS + 64 * CSPR;
 uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts) {
   if (!c.built) throw Error(-22, "partition_dbg: no dBG");
   if (nparts < 1 || nparts > 64) throw Error(-22, "partition_dbg: nparts must be in [1, 64]");
   const uint64_t ntot = 2 * c.cap + c.ovf_cap;
-  DevBuf& cnt = c.part_cnt;                             // [0, 64) counts, [64, 128) cursors, [128, 192) sums
-  cnt.reserve(24 * 64);
+  DevBuf& cnt = c.part_cnt;                             // [0, 64) counts, [64, 128) cursors, then the sums
+  cnt.reserve(8 * PCW_ROWS);
   auto* counts = cnt.as<unsigned long long>();
-  c.h_pin.reserve(24 * 64);
+  c.h_pin.reserve(8 * PCW_ROWS);
   auto* h = c.h_pin.as<unsigned long long>();
   if (!d_out) {                                         // count pass
     PG_HIP(hipMemsetAsync(cnt.p, 0, 8 * 64, c.stream));
@@ -3118,14 +3147,16 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
   if (out_cap < total) throw Error(-22, "partition_dbg: output buffer too small");
   for (int i = 0; i < 64; ++i) c.part_sums[i] = 0;
   if (total) {
-    for (int i = 0; i < nparts; ++i) h[128 + i] = 0;
-    PG_HIP(hipMemcpyAsync(counts + 64, h + 64, 8 * 128, hipMemcpyHostToDevice, c.stream));   // cursors, zeroed sums
+    const size_t sw = (size_t)nparts * CSPR;
+    for (size_t i = 0; i < sw; ++i) h[PCW_SUMS + i] = 0;
+    PG_HIP(hipMemcpyAsync(counts + 64, h + 64, 8 * (64 + sw), hipMemcpyHostToDevice, c.stream));  // cursors, zeroed sums
     hipLaunchKernelGGL(k_part_scatter, dim3(grid_for(ntot, PCH, 4096)), dim3(PT), 0, c.stream, c.tv, 2 * c.cap, ntot,
-                       nparts, counts + 64, reinterpret_cast<Slot*>(d_out), counts + 128);
+                       nparts, counts + 64, reinterpret_cast<Slot*>(d_out), counts + PCW_SUMS);
     PG_HIP(hipGetLastError());
-    PG_HIP(hipMemcpyAsync(h + 128, counts + 128, 8 * nparts, hipMemcpyDeviceToHost, c.stream));
+    PG_HIP(hipMemcpyAsync(h + PCW_SUMS, counts + PCW_SUMS, 8 * sw, hipMemcpyDeviceToHost, c.stream));
     c.sync();
-    for (int i = 0; i < nparts; ++i) c.part_sums[i] = h[128 + i];
+    for (int i = 0; i < nparts; ++i)
+      for (int j = 0; j < CSPR; ++j) c.part_sums[i] += h[PCW_SUMS + (size_t)i * CSPR + j];
   }
   return total;
 }
@@ -3133,10 +3164,10 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
 // Sums of row_check over nseg segments of 16-byte records at d_rows
 // (segment s = records [off[s], off[s+1])), on the context's stream.
 void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums) {
-  DevBuf& out = c.part_cnt;                             // (after the partition words: [192, 192 + RS_SEG))
-  out.reserve(8 * (192 + RS_SEG));
-  auto* d = out.as<unsigned long long>() + 192;
-  c.h_pin.reserve(8 * RS_SEG);
+  DevBuf& out = c.part_cnt;                             // (after the partition words)
+  out.reserve(8 * (PCW_ROWS + RS_SEG * CSPR));
+  auto* d = out.as<unsigned long long>() + PCW_ROWS;
+  c.h_pin.reserve(8 * RS_SEG * CSPR);
   auto* h = c.h_pin.as<unsigned long long>();
   for (uint64_t s0 = 0; s0 < nseg; s0 += RS_SEG) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(RS_SEG, nseg - s0);
@@ -3147,15 +3178,19 @@ void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nse
       if (so.o[s + 1] < so.o[s]) throw Error(-22, "rows_checksum: segment offsets decrease");
       mx = std::max<uint64_t>(mx, so.o[s + 1] - so.o[s]);
     }
-    PG_HIP(hipMemsetAsync(d, 0, 8 * RS_SEG, c.stream));
+    PG_HIP(hipMemsetAsync(d, 0, 8 * RS_SEG * CSPR, c.stream));
     if (mx) {
       hipLaunchKernelGGL(k_rows_sum, dim3(grid_for(mx, 256, 2048), ns), dim3(256), 0, c.stream,
                          reinterpret_cast<const Slot*>(d_rows), so, d);
       PG_HIP(hipGetLastError());
     }
-    PG_HIP(hipMemcpyAsync(h, d, 8 * ns, hipMemcpyDeviceToHost, c.stream));
+    PG_HIP(hipMemcpyAsync(h, d, 8 * (size_t)ns * CSPR, hipMemcpyDeviceToHost, c.stream));
     c.sync();
-    for (uint32_t s = 0; s < ns; ++s) sums[s0 + s] = h[s];
+    for (uint32_t s = 0; s < ns; ++s) {
+      uint64_t t = 0;
+      for (int j = 0; j < CSPR; ++j) t += h[(size_t)s * CSPR + j];
+      sums[s0 + s] = t;
+    }
   }
 }
 
@@ -3179,7 +3214,8 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
     if (n) {
       hipLaunchKernelGGL(k_slots_emit, dim3(grid_for(n, 4 * IBLOCK, 4096)), dim3(IBLOCK), 0, c.stream,
-                         reinterpret_cast<const Slot*>(d_pairs), n, c.tv, O);
+                         reinterpret_cast<const Slot*>(d_pairs), n, c.tv, O,
+                         c.flags.as<unsigned long long>() + N_FLAGS / 2);
       PG_HIP(hipGetLastError());
     }
     c.t1.stop(c.stream);

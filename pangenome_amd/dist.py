@@ -155,7 +155,7 @@ def _poisoned(t):
 
 
 def _route(table, world: int, device, group=None, sentinel_local: bool = False, subparts: int = 1, tm=None,
-           where: str = "", fail=None):
+           where: str = "", fail=None, defer=None):
     """This rank's table -> owner runs of 16-byte records (pg_dbg_partition)
     -> one all-to-all.  Every rank's run lengths and their integrity sums,
     with its n<k sentinel flag, go to every rank in one small all-gather: the
@@ -172,6 +172,9 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     flag), naming `where`, the peer, the sub-log and the 512 MiB piece.
     `fail`: a failed check of this rank since the last collective (a
     message): it travels in the count matrix and every rank raises.
+    `defer` (a dict): the received-run check skips its own all-reduce and
+    leaves `bad` (this rank's mismatching runs) and `diagnose` (the
+    collective that raises) for the caller's next all-reduce to carry.
     Returns (the records this rank owns as an (n, 2) int64 tensor on
     `device`, the received counts per (source rank, sub-log) as a (world, P)
     array, their expected sums as a (world, P) array of Python ints, bytes
@@ -224,10 +227,15 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     off = np.concatenate([[0], np.cumsum(rh.reshape(-1))]).astype(np.int64).tolist()
     got = _seg_sums(table, recv, off, device)
     bad = [(s, p) for s in range(world) for p in range(P) if got[s * P + p] != int(want[s, p])]
-    flag = torch.tensor([1 if bad else 0], dtype=torch.int64, device=comm)
-    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-    if int(flag.item()):
-        _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm, group, where)
+    if defer is not None:
+        defer["bad"] = bad
+        defer["diagnose"] = lambda: _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm,
+                                              group, where)
+    else:
+        flag = torch.tensor([1 if bad else 0], dtype=torch.int64, device=comm)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()):
+            _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm, group, where)
     if tm is not None:
         if _is_cuda(device):
             torch.cuda.synchronize(device)
@@ -361,12 +369,13 @@ def _raise_if_any(fail, flags, rank: int):
 
 
 def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=None, sentinel_global=None, tm=None,
-                  want_sum=None):
+                  want_sum=None, route=None):
     """OR-merge the owned records into a fresh owner table, rdBG rule on it;
     global (n_dbg, n_rdbg) by one sum all-reduce.  `sentinel_global`: whether
     any rank saw the n<k sentinel, when the caller already knows (else one MAX
     all-reduce of `sentinel_local` finds out); `want_sum`: the integrity sum
-    the received records must have.  Returns (n_dbg_total, n_rdbg_total,
+    the received records must have; `route`: _route's deferred receive
+    check, carried by the count all-reduce.  Returns (n_dbg_total, n_rdbg_total,
     n_rdbg_local); `tm["merge"]` accumulates the seconds of the merge, the
     rdBG rule and the count all-reduce."""
     import torch
@@ -387,9 +396,12 @@ def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=No
         fail = _merge_checked(table, recv, n, sentinel_global and rank == 0, want_sum, device,
                               "exchange: rank %d's owner merge" % rank)
     st = table.build_rdbg()
-    sums = torch.tensor([st.n_dbg, st.n_rdbg, 1 if fail else 0], dtype=torch.int64, device=comm)
+    rbad = 1 if route and route.get("bad") else 0
+    sums = torch.tensor([st.n_dbg, st.n_rdbg, 1 if fail else 0, rbad], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
-    n_dbg, n_rdbg, nfail = sums.tolist()
+    n_dbg, n_rdbg, nfail, nrbad = sums.tolist()
+    if nrbad:
+        route["diagnose"]()                          # (collective; raises on every rank)
     if nfail:
         _raise_if_any(fail, [1], rank)
     if tm is not None:
@@ -402,10 +414,12 @@ def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bo
     host reads (the count matrix, the global counts) besides the partition's
     own count read.  Returns (n_dbg_total, n_rdbg_total, n_rdbg_local,
     bytes_sent); `tm` accumulates partition / all_to_all / merge seconds."""
-    recv, _, want, sent, sentinel = _route(table, world, device, group, sentinel_local, tm=tm, where="exchange")
+    chk = {}
+    recv, _, want, sent, sentinel = _route(table, world, device, group, sentinel_local, tm=tm, where="exchange",
+                                           defer=chk)
     want_sum = sum(x for row in want for x in row) & M64
     return _owner_reduce(table, recv, rank, device, sentinel_local, group, sentinel_global=sentinel, tm=tm,
-                         want_sum=want_sum) + (sent,)
+                         want_sum=want_sum, route=chk) + (sent,)
 
 
 def stream_chunks(flags, seq_len, limit: int) -> list:
