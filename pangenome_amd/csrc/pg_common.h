@@ -240,11 +240,29 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* lds, u
   return pre + x - v;
 }
 
+// The class stream as K1 leaves it: the packed words (16 bases x 2 bits per
+// 32-bit word) and one exception byte per 16 bases, and the class bytes only
+// of the 16-base chunks with an exception (N, '$', other) or shared by two
+// parse spans.  ensure_cls fills in the rest for the passes that read bytes.
+struct PackedCls {
+  const uint8_t* cls;
+  const uint32_t* p2;
+  const uint8_t* e16;
+  __device__ __forceinline__ uint32_t operator[](long long i) const {
+    return e16[i >> 4] ? (uint32_t)cls[i] : (p2[i >> 4] >> (2 * (i & 15))) & 3u;
+  }
+};
+// the 4 class bytes of bases 4d .. 4d+3 of a packed word
+__device__ __forceinline__ uint32_t unpack4(uint32_t w, int d) {
+  const uint32_t b = (w >> (8 * d)) & 0xFFu;
+  return (b | (b << 6) | (b << 12) | (b << 18)) & 0x03030303u;
+}
+
 // build_dbg for one strand of length n in {k, k+1}: emit(key, 12-bit mask)
 // per window.  strand 0: s[i] = cls[rs+i]; strand 1: s[i] =
 // comp_class(cls[rs+n-1-i]) (tab_rev(reversed(s)), :1217).
-template <class Emit>
-__device__ void short_strand(const uint8_t* cls, long long rs, long long n, int strand, int k, uint64_t shift,
+template <class Src, class Emit>
+__device__ void short_strand(const Src& cls, long long rs, long long n, int strand, int k, uint64_t shift,
                              Emit&& emit) {
   auto S = [&](long long i) -> uint32_t {
     return strand == 0 ? (uint32_t)cls[rs + i] : comp_class(cls[rs + n - 1 - i]);

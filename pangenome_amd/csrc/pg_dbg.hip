@@ -1609,7 +1609,7 @@ __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[
 // the rows.
 template <bool RC, int NP>
 __global__ void __launch_bounds__(IBLOCK)
-k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
+k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
             const unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, uint64_t shift,
             TableView T, BinOut O) {
   static_assert(NQ == 64, "one wave scans the sub-queue counts");
@@ -1664,9 +1664,17 @@ k_emit_work(const uint8_t* __restrict__ cls, const WorkItem* __restrict__ queue,
       const long long from = w.rs + w.q0 - 2;
       aligned = from > 0 ? from & ~15ll : 0;
       uint32_t* s32 = reinterpret_cast<uint32_t*>(slot);          // (4-byte aligned rows)
+      // the 4 chunks' packed words, unpacked; a chunk with an exception
+      // (not all ACGT) from its class bytes
+      const uint64_t c0 = (uint64_t)aligned >> 4;
+      uint32_t pw[4], ex[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { pw[j] = pc.p2[c0 + j]; ex[j] = pc.e16[c0 + j]; }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint4 v = *reinterpret_cast<const uint4*>(cls + aligned + 16 * j);
+        uint4 v;
+        if (ex[j]) v = *reinterpret_cast<const uint4*>(pc.cls + aligned + 16 * j);
+        else v = make_uint4(unpack4(pw[j], 0), unpack4(pw[j], 1), unpack4(pw[j], 2), unpack4(pw[j], 3));
         s32[4 * j] = v.x; s32[4 * j + 1] = v.y; s32[4 * j + 2] = v.z; s32[4 * j + 3] = v.w;
       }
     }
@@ -1705,7 +1713,7 @@ __device__ __forceinline__ void canon_record(const TableView& T, uint64_t x, uin
 // Records with n <= k+1 (build_dbg's short paths, :1061-1088): the windows of
 // both strands as canonical records; n < k sets the n<k sentinel (:1087-1088).
 __global__ void __launch_bounds__(IBLOCK)
-k_short_emit(const uint8_t* __restrict__ cls, const long long* __restrict__ rec_start,
+k_short_emit(PackedCls cls, const long long* __restrict__ rec_start,
              const long long* __restrict__ rec_len, const uint8_t* __restrict__ rec_flag, uint64_t R, int k,
              uint64_t shift, int rc, TableView T, BinOut O) {
   __shared__ EmitLds<1> s_emit;
@@ -2816,7 +2824,7 @@ constexpr uint64_t K3_CHUNK_MIN = 1024;       // coverage groups per chunk below
 
 static void launch_short(Ctx& c, hipStream_t s, int rc0, uint64_t shift, const BinOut& O) {
   if (!c.n_records) return;
-  hipLaunchKernelGGL(k_short_emit, dim3(grid_for(c.n_records, IBLOCK, 1024)), dim3(IBLOCK), 0, s, c.cls.as<uint8_t>(),
+  hipLaunchKernelGGL(k_short_emit, dim3(grid_for(c.n_records, IBLOCK, 1024)), dim3(IBLOCK), 0, s, packed_cls(c),
                      c.rec_start.as<long long>(), c.rec_len.as<long long>(), c.rec_flag.as<uint8_t>(), c.n_records,
                      c.k, shift, rc0, c.tv, O);
   PG_HIP(hipGetLastError());
@@ -2844,7 +2852,12 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   const bool tail = part == SA_WHOLE || part == SA_TAIL || part == SA_FIRST_TAIL || part == SA_MORE_TAIL;
   const BinOut O = stageA_begin(c, cap, fl, begin);
   if (part == SA_TAIL) ntiles = 0;
+  if (c.k3_cover == 1 || c.k3_cover == 2) ensure_cls(c);   // (the class-byte coverage forms)
+#ifdef PG_DEBUG_BOUNDS
+  ensure_cls(c);                                            // (k_cover_p's debug check reads class bytes)
+#endif
   const uint8_t* cls = c.cls.as<uint8_t>();
+  const PackedCls pc = packed_cls(c);
   const dim3 b(IBLOCK);
   int nch = ntiles >= (uint64_t)K3_CHUNKS * K3_CHUNK_MIN ? K3_CHUNKS : 1;
   if (c.k3_chunks > 0) nch = std::min(6, c.k3_chunks);
@@ -2933,7 +2946,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     const bool halves = c.k3_emit != 1;
     auto* kw = rc0 ? (halves ? k_emit_work<true, 2> : k_emit_work<true, 1>)
                    : (halves ? k_emit_work<false, 2> : k_emit_work<false, 1>);
-    hipLaunchKernelGGL(kw, dim3(gw), b, 0, ws, cls, qi, qni, (unsigned long long)qcapc[i], c.k, shift, c.tv, O);
+    hipLaunchKernelGGL(kw, dim3(gw), b, 0, ws, pc, qi, qni, (unsigned long long)qcapc[i], c.k, shift, c.tv, O);
     PG_HIP(hipGetLastError());
   }
   if (!short_done && tail) launch_short(c, s0, rc0, shift, O);

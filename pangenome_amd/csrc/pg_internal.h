@@ -178,9 +178,12 @@ struct Ctx {
   DevBuf rec_start, rec_len;      // int64 per record: compacted offset / length
   DevBuf rec_hdr, rec_ptr;        // int64 per record: header byte span packed, `ptr` emulation
   DevBuf rec_flag;                // uint8 per record: take part in the current pass
-  DevBuf cls;                     // uint8 per base: class code (records concatenated)
+  DevBuf cls;                     // uint8 per base: class code (records concatenated); K1 writes only
+                                  // the 16-base chunks with an exception or shared by two spans
   DevBuf p2;                      // uint32 per 16 bases: 2-bit codes (class & 3), the packed base stream
   DevBuf e16;                     // uint8 per 16 bases: nonzero if any is not ACGT
+  bool cls_full = false;          // every chunk of `cls` written (ensure_cls)
+  uint64_t n_cls = 0;             // length of the compacted stream (bases before the first header too)
   DevBuf scratch;                 // rocPRIM temp storage
   DevBuf rec_pack;                // the scan total + int64 [5][rec_cap]: the record table for one copy
   uint64_t rec_cap = 0;           // record arrays sized for the last parse's record count
@@ -337,6 +340,10 @@ void pool_destroy(Ctx& c);
 // so far (their lengths in c.h_rec_len, c.n_records = that count), and once
 // at the end with all of them; it may enqueue work on c.stream.
 void parse_fasta(Ctx& c, const uint8_t* h_src = nullptr, const std::function<void(uint64_t)>* on_chunk = nullptr);
+// the class bytes of every chunk K1 left packed (e16 == 0), once per parse,
+// on c.stream: for the passes that read `cls` directly (walks, checkpoints)
+void ensure_cls(Ctx& c);
+inline PackedCls packed_cls(Ctx& c) { return PackedCls{c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>()}; }
 // pg_build_host: parse of host bytes with stage A of the build streamed under
 // the upload (every record, no -n / checkpoint plan), then stages B and C
 void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0);

@@ -407,10 +407,10 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
         const uint8_t* src = stage + (g - cb);
         if (g >= own) {
           const uint4 cv = *reinterpret_cast<const uint4*>(src);
-          *reinterpret_cast<uint4*>(out + g) = cv;
           uint32_t exc;
           p2[g >> 4] = pack_word(cv, exc);              // (a shared chunk: k_pack_fix)
           e16[g >> 4] = exc ? 1 : 0;
+          if (exc) *reinterpret_cast<uint4*>(out + g) = cv;   // (the class bytes: exception chunks only)
         } else {
           for (int jj = 0; jj < 16; ++jj)
             if (g + jj >= own) out[g + jj] = src[jj];
@@ -455,12 +455,14 @@ __global__ void __launch_bounds__(PBLOCK) k_headers(const uint8_t* __restrict__ 
   if (incl[span].hdr == pre.hdr && !state) return;            // no header starts or ends here
   const uint64_t p0 = span * WSPAN;
   unsigned long long off = pre.c0, rec = pre.hdr;
+  uint4 v[WSTEPS];                                            // (every load in flight at once)
+  load_span(buf, p0, n, lane, v);
   uint32_t carry = p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u);
+#pragma unroll
   for (int s = 0; s < WSTEPS; ++s) {
     if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
     const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
-    const uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
-    const LaneStep ls = lane_step(v, p, n, lane, carry);
+    const LaneStep ls = lane_step(v[s], p, n, lane, carry);
     const uint32_t region = lane_region(ls, lane_in(ls, state));
     const uint32_t cm = lane_content(ls, region);
     const uint32_t mine = (uint32_t)__builtin_popcount(cm) | (uint32_t)__builtin_popcount(ls.hs) << 16;
@@ -510,6 +512,28 @@ __global__ void k_pack_fix(const Fn* __restrict__ incl, uint64_t s0, uint64_t s1
     p2[g >> 4] = pack_word(cv, exc);
     e16[g >> 4] = exc ? 1 : 0;
   }
+}
+
+// The class bytes of the chunks K1 left packed (e16 == 0: all ACGT, class =
+// the 2-bit code), 16 bases per thread, grid-stride.
+__global__ void k_unpack_cls(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint64_t nchunk,
+                             uint8_t* __restrict__ cls) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nchunk; i += (uint64_t)gridDim.x * blockDim.x) {
+    if (e16[i]) continue;
+    const uint32_t w = p2[i];
+    *reinterpret_cast<uint4*>(cls + 16 * i) = make_uint4(unpack4(w, 0), unpack4(w, 1), unpack4(w, 2), unpack4(w, 3));
+  }
+}
+
+void ensure_cls(Ctx& c) {
+  if (c.cls_full || !c.parsed) return;
+  const uint64_t nchunk = (c.n_cls + 15) / 16;
+  if (nchunk) {
+    hipLaunchKernelGGL(k_unpack_cls, dim3(grid_for(nchunk, 256, 8192)), dim3(256), 0, c.stream, c.p2.as<uint32_t>(),
+                       c.e16.as<uint8_t>(), nchunk, c.cls.as<uint8_t>());
+    PG_HIP(hipGetLastError());
+  }
+  c.cls_full = true;
 }
 
 // The record table from the scan's total (read on the device: no host round
@@ -571,7 +595,8 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   const hipStream_t st = c.stream;
   const uint64_t n = c.n_bytes;
   c.parsed = false;
-  c.n_lines = c.n_records = c.n_bases = c.n_nl = 0;
+  c.cls_full = false;
+  c.n_lines = c.n_records = c.n_bases = c.n_nl = c.n_cls = 0;
   c.h_rec_start.clear(); c.h_rec_len.clear(); c.h_rec_hdr_start.clear();
   c.h_rec_hdr_len.clear(); c.h_rec_ptr.clear();
   if (n == 0) {
@@ -623,19 +648,22 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   // of the spans so far (k_records, total = incl[s1 - 1]) and its copy to the
   // host, marked by rec_ev: queued before the spans' emission, so the host
   // reads the table while the emission runs
+  // (on `rs`: the context's stream, or for a whole-file parse the second
+  // stream, beside the emission)
+  hipStream_t rs = st;
   auto records = [&](uint64_t s0, uint64_t s1, uint64_t rcap) {
     auto* hdr = c.rec_hdr.as<long long>();
-    hipLaunchKernelGGL(k_headers, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta, n,
+    hipLaunchKernelGGL(k_headers, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, rs, c.d_fasta, n,
                        s0, s1, incl, rcap, c.rec_start.as<long long>(), hdr, hdr + rcap);
     PG_HIP(hipGetLastError());
   };
   auto table_copy = [&](uint64_t s1, uint64_t rcap) {
-    hipLaunchKernelGGL(k_records, dim3(grid_for(rcap, 256, 1024)), dim3(256), 0, st, incl + s1 - 1, n, rcap,
+    hipLaunchKernelGGL(k_records, dim3(grid_for(rcap, 256, 1024)), dim3(256), 0, rs, incl + s1 - 1, n, rcap,
                        c.rec_start.as<long long>(), c.rec_hdr.as<long long>(), c.rec_len.as<long long>(),
                        c.rec_pack.as<long long>());
     PG_HIP(hipGetLastError());
-    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 64 + 40 * rcap, hipMemcpyDeviceToHost, st));
-    PG_HIP(hipEventRecord(c.rec_ev, st));
+    PG_HIP(hipMemcpyAsync(c.h_pin.p, c.rec_pack.p, 64 + 40 * rcap, hipMemcpyDeviceToHost, rs));
+    PG_HIP(hipEventRecord(c.rec_ev, rs));
   };
   // (a polling wait, as Ctx::sync: a blocking wait's wake-up is on the path)
   auto table_wait = [&]() {
@@ -713,6 +741,12 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
     PG_HIP(hipGetLastError());
     scan(nspan);
+    // the header pass, the record table and its copy to the host on the
+    // second stream, beside the emission (they read the FASTA's header
+    // spans and the scan, nothing the emission writes)
+    PG_HIP(hipEventRecord(c.ev[14], st));
+    PG_HIP(hipStreamWaitEvent(c.stream2, c.ev[14], 0));
+    rs = c.stream2;
     records(0, nspan, rcap0);
     pending = {0, nspan};
   }
@@ -750,6 +784,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     c.rec_cap = R;
   }
   c.n_nl = tot.nl;
+  c.n_cls = tot.c0;
   if (tot.nl == 0) {                                        // no line at all (:126-132)
     c.parsed = true;
     if (on_chunk) (*on_chunk)(streaming ? 0 : ~0ull);

@@ -249,6 +249,7 @@ static void dump_counts(Ctx& c) {
     for (uint64_t j = 0; j < nch; ++j) chunks.push_back(((unsigned long long)r << 32) | j);
   }
   DevBuf dch;
+  ensure_cls(c);                              // (the window counts read class bytes)
   if (!chunks.empty()) {
     dch.reserve(8 * chunks.size());
     PG_HIP(hipMemcpyAsync(dch.p, chunks.data(), 8 * chunks.size(), hipMemcpyHostToDevice, c.stream));

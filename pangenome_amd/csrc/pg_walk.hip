@@ -621,6 +621,7 @@ static void plan_walk(Ctx& c, const uint8_t* h_rec_flag, WalkPlan& P) {
 
 static WalkArgs make_args(Ctx& c, WalkPlan& P, int rc) {
   WalkArgs a;
+  ensure_cls(c);                              // (the walks read class bytes)
   a.cls = c.cls.as<uint8_t>();
   a.rec_start = c.rec_start.as<long long>();
   a.rec_len = c.rec_len.as<long long>();
