@@ -186,6 +186,31 @@ int pg_dbg_merge(pg_ctx* ctx, const void* d_records, uint64_t n, uint64_t capaci
 /* What the last pg_dbg_merge read: non-empty records and the sum of their
  * hashes (pg_dbg_partition_sums' hash over all n records). */
 int pg_dbg_merge_check(const pg_ctx* ctx, uint64_t* rows, uint64_t* sum);
+/* Routed exchange: the owners build once.  Instead of a local dBG that is
+ * partitioned and merged again, a rank's stage A records (h = the table
+ * hash of the canonical key, the 26-bit mask word) go to their owners, and
+ * only the owners run stages B and C.  The owner of a record is the top
+ * log2(nparts) bits of h (nparts a power of two, at most 64), so a rank's
+ * records for one owner are whole stage A regions.
+ * pg_route_stage_a: after pg_parse / pg_set_fasta(_device) + pg_parse, stage
+ * A of the build pg_build_dbg would run (same arguments), held for routing;
+ * counts[nparts] = records per owner, *sentinel = the n<k sentinel seen. */
+int pg_route_stage_a(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0, int nparts, uint64_t* counts,
+                     int* sentinel);
+/* The held records as 16-byte rows {h, mask word, 0} grouped by owner into
+ * d_out (device, capacity out_cap rows; owner o's run after owner o-1's);
+ * sums[nparts] = each run's integrity sum (as pg_dbg_partition_sums). */
+int pg_route_scatter(pg_ctx* ctx, int nparts, void* d_out, uint64_t out_cap, uint64_t* sums);
+/* World 1: stages B and C on the held records where they lie (this rank
+ * owns them all) - the dBG and rdBG of pg_build_dbg, no copy. */
+int pg_route_finish(pg_ctx* ctx, uint64_t* n_rdbg, pg_stats* stats);
+/* Owner `part` of `nparts`: a fresh table from the n received rows (every
+ * rank's run for this owner, device pointer), stages A (re-binning), B and
+ * C; sentinel != 0 adds the n<k key.  pg_dbg_merge_check reports what it
+ * read.  The table's hash domain is h rotated left by log2(nparts) bits:
+ * pg_dbg_export / pg_rdbg_export return plain keys. */
+int pg_route_merge(pg_ctx* ctx, const void* d_rows, uint64_t n, int nparts, int sentinel, uint64_t* n_rdbg,
+                   pg_stats* stats);
 
 /* ---- edge pass: rdbg_edge_weight_jit_ (kmer_numba.py:1808-1827) ->
  *      rdbg_edge_weight (:1446-1518).  rec_flags as above (walked records);
@@ -323,6 +348,17 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * (0..255; -1, the default, = off), so that a kernel reading memory nothing
  * wrote gives a different result instead of inheriting an earlier run's. */
 #define PG_TUNE_POISON 17
+/* PG_TUNE_K1: K1 form bits.  Bit 0: the span pass, 0 = per-step form (fast
+ * or general 1 KiB step), 1 = whole-span form (a 16 KiB span without '>' and
+ * below the last byte counted in one pass of SWAR sums, its newline positions
+ * found afterwards; the spans left over by a step-parallel per-step pass).
+ * Bit 1: the emission keeps two wave steps of loads in flight (else one). */
+#define PG_TUNE_K1 18
+/* PG_TUNE_TIMERS: which stage spans of pg_stats are timed with HIP events on
+ * the stream (each timing event costs the stream a few us): bit 0 K1
+ * (ms_parse), bit 1 stage A (ms_insert), bit 2 stages B/C (ms_split,
+ * ms_range); 7 (default) = all, 0 = none (the spans read 0). */
+#define PG_TUNE_TIMERS 19
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Device bytes the library's buffers hold in this process now (peak == 0)

@@ -32,6 +32,8 @@ PG_TUNE_EARLY_SPLIT = 14
 PG_TUNE_K3_HEAD = 15
 PG_TUNE_H2D_TAIL = 16
 PG_TUNE_POISON = 17             # process-wide debug: new device buffers filled with this byte
+PG_TUNE_K1 = 18                 # K1 form bits (bit 0 whole-span pass, bit 1 deeper emission prefetch)
+PG_TUNE_TIMERS = 19             # bits: HIP timing events of K1 / stage A / stages B-C (default 7)
 
 
 class PgStats(C.Structure):
@@ -75,6 +77,10 @@ SIGNATURES = {
     "pg_dbg_partition_sums": (C.c_int, [_P, C.c_int, _P]),
     "pg_rows_checksum": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     "pg_dbg_merge_check": (C.c_int, [_P, _U64P, _U64P]),
+    "pg_route_stage_a": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P, C.POINTER(C.c_int)]),
+    "pg_route_scatter": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
+    "pg_route_finish": (C.c_int, [_P, _U64P, _SP]),
+    "pg_route_merge": (C.c_int, [_P, _P, C.c_uint64, C.c_int, C.c_int, _U64P, _SP]),
     "pg_edges": (C.c_int, [_P, _P, C.c_int, _U64P]),
     "pg_edges_export": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_set_labels": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
@@ -353,6 +359,38 @@ class Context:
         rows, s = C.c_uint64(), C.c_uint64()
         check(self.lib.pg_dbg_merge_check(self.h, C.byref(rows), C.byref(s)), "pg_dbg_merge_check")
         return rows.value, s.value
+
+    # ---------------------------------------------------- routed exchange
+    def route_stage_a(self, rec_flags=None, extra_empty: int = 0, rc0: bool = True, nparts: int = 1):
+        """Stage A of the build, held for its owners: (records per owner as
+        uint64[nparts], whether the n<k sentinel was seen)."""
+        counts = np.zeros(nparts, np.uint64)
+        sent = C.c_int(0)
+        f = None if rec_flags is None else np.ascontiguousarray(rec_flags, dtype=np.uint8)
+        check(self.lib.pg_route_stage_a(self.h, ptr(f), int(extra_empty), int(bool(rc0)), int(nparts), ptr(counts),
+                                        C.byref(sent)), "pg_route_stage_a")
+        return counts, bool(sent.value)
+
+    def route_scatter(self, nparts: int, d_out: int, out_cap: int):
+        """The held records as 16-byte rows grouped by owner at d_out; their
+        integrity sums per owner (uint64[nparts])."""
+        sums = np.zeros(nparts, np.uint64)
+        check(self.lib.pg_route_scatter(self.h, int(nparts), C.c_void_p(d_out) if d_out else None, int(out_cap),
+                                        ptr(sums)), "pg_route_scatter")
+        return sums
+
+    def route_finish(self) -> PgStats:
+        st = PgStats()
+        n = C.c_uint64()
+        check(self.lib.pg_route_finish(self.h, C.byref(n), C.byref(st)), "pg_route_finish")
+        return st
+
+    def route_merge(self, d_rows: int, n: int, nparts: int, sentinel: bool = False) -> PgStats:
+        st = PgStats()
+        nr = C.c_uint64()
+        check(self.lib.pg_route_merge(self.h, C.c_void_p(d_rows) if n else None, int(n), int(nparts),
+                                      int(bool(sentinel)), C.byref(nr), C.byref(st)), "pg_route_merge")
+        return st
 
     # -------------------------------------------------------------- walks
     def edges_count(self, rec_flags=None, rc1: bool = False) -> int:

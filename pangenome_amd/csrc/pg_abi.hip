@@ -68,6 +68,11 @@ int pg_create(pg_ctx** out, int device, int k) {
     PG_HIP(hipStreamCreateWithFlags(&x->c.stream, hipStreamNonBlocking));
     PG_HIP(hipStreamCreateWithFlags(&x->c.stream2, hipStreamNonBlocking));
     PG_HIP(hipStreamCreateWithFlags(&x->c.stream3, hipStreamNonBlocking));
+    {
+      int lo = 0, hi = 0;
+      PG_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      PG_HIP(hipStreamCreateWithPriority(&x->c.stream_hi, hipStreamNonBlocking, hi));
+    }
     for (auto& e : x->c.ev) PG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : x->c.cev) PG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     PG_HIP(hipEventCreateWithFlags(&x->c.rec_ev, hipEventDisableTiming));
@@ -105,6 +110,7 @@ void pg_destroy(pg_ctx* x) {
   for (auto e : c.cev)
     if (e) (void)hipEventDestroy(e);
   if (c.rec_ev) (void)hipEventDestroy(c.rec_ev);
+  if (c.stream_hi) (void)hipStreamDestroy(c.stream_hi);
   (void)hipStreamDestroy(c.stream3);
   (void)hipStreamDestroy(c.stream2);
   (void)hipStreamDestroy(c.stream);
@@ -285,6 +291,16 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         if (value < 0 || value > 255) throw pg::Error(PG_EINVAL, "pg_tune: K3 work blocks must be in [0, 255]");
         x->c.k3_wblk = (int)value;
         break;
+      case PG_TUNE_TIMERS:
+        if (value < 0 || value > 7) throw pg::Error(PG_EINVAL, "pg_tune: timers must be in [0, 7]");
+        x->c.t0.off = !(value & 1);
+        x->c.t1.off = !(value & 2);
+        x->c.t6.off = !(value & 4);
+        break;
+      case PG_TUNE_K1:
+        if (value < 0 || value > 3) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 3]");
+        x->c.k1_form = (int)value;
+        break;
       case PG_TUNE_K3_EMIT:
         if (value < 0 || value > 1) throw pg::Error(PG_EINVAL, "pg_tune: K3 emit form must be 0 or 1");
         x->c.k3_emit = (int)value;
@@ -453,6 +469,64 @@ int pg_rows_checksum(pg_ctx* x, const void* d_rows, const uint64_t* seg_off, uin
       throw pg::Error(PG_EINVAL, "pg_rows_checksum: bad arguments");
     PG_HIP(hipSetDevice(x->c.device));
     pg::rows_checksum(x->c, d_rows, seg_off, nseg, sums);
+  });
+}
+
+static int route_lg(int nparts, const char* what) {
+  if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1)))
+    throw pg::Error(PG_EINVAL, std::string(what) + ": nparts must be a power of two in [1, 64]");
+  return __builtin_ctz((unsigned)nparts);
+}
+
+int pg_route_stage_a(pg_ctx* x, const uint8_t* rec_flags, int extra_empty, int rc0, int nparts, uint64_t* counts,
+                     int* sentinel) {
+  return guard([&] {
+    if (!x || !counts) throw pg::Error(PG_EINVAL, "pg_route_stage_a: bad arguments");
+    const int lg = route_lg(nparts, "pg_route_stage_a");
+    PG_HIP(hipSetDevice(x->c.device));
+    x->c.route_req = true;
+    try {
+      pg::build_dbg(x->c, rec_flags, extra_empty, rc0 != 0);
+    } catch (...) {
+      x->c.route_req = false;
+      throw;
+    }
+    if (!x->c.route_ready) throw pg::Error(PG_EINVAL, "pg_route_stage_a: the build did not hold its records");
+    pg::route_counts(x->c, lg, counts);
+    if (sentinel) *sentinel = x->c.route_sentinel ? 1 : 0;
+  });
+}
+
+int pg_route_scatter(pg_ctx* x, int nparts, void* d_out, uint64_t out_cap, uint64_t* sums) {
+  return guard([&] {
+    if (!x || !sums || (!d_out && out_cap)) throw pg::Error(PG_EINVAL, "pg_route_scatter: bad arguments");
+    const int lg = route_lg(nparts, "pg_route_scatter");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::route_scatter(x->c, lg, d_out, out_cap, sums);
+  });
+}
+
+int pg_route_finish(pg_ctx* x, uint64_t* n_rdbg, pg_stats* stats) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_route_finish: ctx is NULL");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::route_finish(x->c);
+    if (n_rdbg) *n_rdbg = x->c.n_rdbg;
+    fill_stats(x->c, stats);
+  });
+}
+
+int pg_route_merge(pg_ctx* x, const void* d_rows, uint64_t n, int nparts, int sentinel, uint64_t* n_rdbg,
+                   pg_stats* stats) {
+  return guard([&] {
+    if (!x || (!d_rows && n)) throw pg::Error(PG_EINVAL, "pg_route_merge: bad arguments");
+    const int lg = route_lg(nparts, "pg_route_merge");
+    PG_HIP(hipSetDevice(x->c.device));
+    if (lg > x->c.cbits && x->c.cbits) throw pg::Error(PG_EINVAL, "pg_route_merge: more owners than coarse bins");
+    x->c.merge_sum = x->c.merge_rows = 0;
+    pg::merge_dbg(x->c, d_rows, n, 0, sentinel, lg);
+    if (n_rdbg) *n_rdbg = x->c.n_rdbg;
+    fill_stats(x->c, stats);
   });
 }
 

@@ -99,18 +99,24 @@ __host__ __device__ __forceinline__ uint64_t row_check(uint64_t w0, uint64_t w1)
 struct TableView {
   unsigned long long* prim;    // 2 words per bucket
   uint64_t bmask;              // buckets - 1
-  uint32_t qbits, sh1, sh2, pad;
+  uint32_t qbits, sh1, sh2;
+  uint32_t rot;                // the owner domain of a routed exchange: h rotated left by rot bits (0: none)
   uint64_t kmask, m1, m2, m1i, m2i;
   Slot* ovf;
   uint64_t omask;              // overflow slots - 1
   uint64_t rc_pad, rc_inv;     // rc(): 3(5^(27-k)-1)/4 and 5^-(27-k) mod 2^64 (see rc_key27)
 
+  // rotate left by 0 < r < kb within the kb key bits
+  __host__ __device__ __forceinline__ uint64_t rotk(uint64_t h, uint32_t r) const {
+    const uint32_t kb = 64u - (uint32_t)__builtin_clzll(kmask);
+    return ((h << r) | (h >> (kb - r))) & kmask;
+  }
   __host__ __device__ __forceinline__ uint64_t perm(uint64_t c) const {
     uint64_t h = (c * m1) & kmask;
     h ^= h >> sh1;
     h = (h * m2) & kmask;
     h ^= h >> sh2;
-    return h;
+    return rot ? rotk(h, rot) : h;
   }
   __host__ __device__ __forceinline__ static uint64_t unxs(uint64_t y, uint32_t s) {
     uint64_t x = y;
@@ -118,6 +124,7 @@ struct TableView {
     return x;
   }
   __host__ __device__ __forceinline__ uint64_t unperm(uint64_t h) const {
+    if (rot) h = rotk(h, 64u - (uint32_t)__builtin_clzll(kmask) - rot);
     h = unxs(h, sh2);
     h = (h * m2i) & kmask;
     h = unxs(h, sh1);

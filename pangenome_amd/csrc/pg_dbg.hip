@@ -1532,6 +1532,10 @@ struct EmitLds {
   uint32_t cnt[NS][NBIN];                     // per sub-round and bin: records
   uint32_t off[NS][NBIN + 1];                 // their exclusive scan over bins (stage offsets), total last
   unsigned long long base[NS][NBIN];          // region position of the bin's first record of the sub-round
+  __device__ __forceinline__ void zero() {    // (threads 0 .. NBIN-1; a barrier before use)
+    if (threadIdx.x < NBIN)
+      for (int q = 0; q < NS; ++q) cnt[q][threadIdx.x] = 0u;
+  }
 };
 template <int NR>
 __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[NR], const uint32_t (&m)[NR],
@@ -1598,6 +1602,11 @@ __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[
   }
 }
 
+// (A wave-level multi-split - the lanes of a bin found by 6 ballots, ranks
+// by popcount, per-wave counters scanned across the block - in place of the
+// LDS rank atomics measured slower: C3 stage A 0.477 ms at 4 waves per SIMD,
+// 0.498 capped to 5 with spills, against 0.438 for the atomics.)
+
 // K3 work pass: one queued segment per thread, every lane busy; the records
 // of a round of IBLOCK segments leave through block_emit.  The NQ sub-queues
 // are read as one concatenated list (their counts scanned in LDS); the
@@ -1638,9 +1647,8 @@ k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
     }
     s_pre[threadIdx.x + 1] = x;                    // inclusive -> s_pre[j+1]
     if (threadIdx.x == 0) s_pre[0] = 0ull;
-#pragma unroll
-    for (int q = 0; q < NX / ESUB; ++q) s_emit.cnt[q][threadIdx.x] = 0u;
   }
+  s_emit.zero();
   __syncthreads();
   uint8_t* slot = scratch[threadIdx.x];
   const unsigned long long n = s_pre[NQ];
@@ -1719,7 +1727,7 @@ k_short_emit(PackedCls cls, const long long* __restrict__ rec_start,
   __shared__ EmitLds<1> s_emit;
   __shared__ unsigned long long st_key[EST];
   __shared__ uint32_t st_mw[EST];
-  if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
+  s_emit.zero();
   __syncthreads();
   for (uint64_t r0 = blockIdx.x * (uint64_t)IBLOCK; r0 < R; r0 += (uint64_t)gridDim.x * IBLOCK) {
     const uint64_t r = r0 + threadIdx.x;
@@ -1759,7 +1767,7 @@ k_preload_emit(const PreEnt* __restrict__ e, uint64_t n, TableView T, BinOut O) 
   __shared__ EmitLds<1> s_emit;
   __shared__ unsigned long long st_key[EST];
   __shared__ uint32_t st_mw[EST];
-  if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
+  s_emit.zero();
   __syncthreads();
   for (uint64_t b = blockIdx.x * (uint64_t)(4 * IBLOCK); b < n; b += (uint64_t)gridDim.x * 4 * IBLOCK) {
     uint64_t hh[4];
@@ -1794,7 +1802,7 @@ k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsi
   __shared__ unsigned long long st_key[EST];
   __shared__ uint32_t st_mw[EST];
   __shared__ unsigned long long s_chk[2][IBLOCK / 64];
-  if (threadIdx.x < NBIN) s_emit.cnt[0][threadIdx.x] = 0u;
+  s_emit.zero();
   __syncthreads();
   unsigned long long acc = 0ull, live = 0ull;
   for (uint64_t b = blockIdx.x * (uint64_t)(4 * IBLOCK); b < n; b += (uint64_t)gridDim.x * 4 * IBLOCK) {
@@ -1809,6 +1817,54 @@ k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsi
         const Slot s = e[i];
         acc += row_check(s.key1, (uint64_t)s.mask | ((uint64_t)s.aux << 32));
         if (s.key1) { hh[t] = T.perm(s.key1 - 1ull); mm[t] = s.mask & (uint32_t)MW_MASK; ++live; }
+      }
+    }
+    block_emit<4>(O, hh, mm, s_emit, st_key, st_mw);
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    acc += __shfl_down(acc, o, 64);
+    live += __shfl_down(live, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_chk[0][threadIdx.x >> 6] = acc;
+    s_chk[1][threadIdx.x >> 6] = live;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long a = 0ull, l = 0ull;
+    for (int w = 0; w < IBLOCK / 64; ++w) { a += s_chk[0][w]; l += s_chk[1][w]; }
+    if (a || l) {
+      unsigned long long* slot = chk + 2 * (blockIdx.x % MCHK);
+      atomicAdd(slot, a);
+      atomicAdd(slot + 1, l);
+    }
+  }
+}
+
+// Routed stage A records {h, mask word} (pg_route_merge) into this owner's
+// regions: h rotated into the owner domain (T.rot), with the same checksum
+// slots as k_slots_emit.
+__global__ void __launch_bounds__(IBLOCK)
+k_route_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsigned long long* __restrict__ chk) {
+  __shared__ EmitLds<1> s_emit;
+  __shared__ unsigned long long st_key[EST];
+  __shared__ uint32_t st_mw[EST];
+  __shared__ unsigned long long s_chk[2][IBLOCK / 64];
+  s_emit.zero();
+  __syncthreads();
+  unsigned long long acc = 0ull, live = 0ull;
+  for (uint64_t b = blockIdx.x * (uint64_t)(4 * IBLOCK); b < n; b += (uint64_t)gridDim.x * 4 * IBLOCK) {
+    uint64_t hh[4];
+    uint32_t mm[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const uint64_t i = b + (uint64_t)t * IBLOCK + threadIdx.x;
+      hh[t] = 0;
+      mm[t] = 0;
+      if (i < n) {
+        const Slot s = e[i];
+        acc += row_check(s.key1, (uint64_t)s.mask | ((uint64_t)s.aux << 32));
+        if (s.mask) { hh[t] = T.rot ? T.rotk(s.key1, T.rot) : s.key1; mm[t] = s.mask & (uint32_t)MW_MASK; ++live; }
       }
     }
     block_emit<4>(O, hh, mm, s_emit, st_key, st_mw);
@@ -2431,11 +2487,14 @@ struct FillList {
   }
 };
 
-static void init_hash(Ctx& c) {
-  if (c.hash_k == c.k && c.kb) return;
-  c.tv = make_hash(c.k, c.kb);
-  c.cbits = std::min(6, c.kb);
-  c.hash_k = c.k;
+// (rot: the owner domain of a routed merge, pg_route_merge; 0 otherwise)
+static void init_hash(Ctx& c, uint32_t rot = 0) {
+  if (!(c.hash_k == c.k && c.kb)) {
+    c.tv = make_hash(c.k, c.kb);
+    c.cbits = std::min(6, c.kb);
+    c.hash_k = c.k;
+  }
+  c.tv.rot = rot;
 }
 
 // The coverage groups (records with n >= k+2), stripe-major: stripe 0 of
@@ -2744,7 +2803,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
     c.sync();
     c.ms_range = c.t6.ms();
     float tsplit = 0.f;                        // stage A's end (t1) to stage C's start
-    PG_HIP(hipEventElapsedTime(&tsplit, c.t1.b, c.t6.a));
+    if (!c.t1.off && !c.t6.off) PG_HIP(hipEventElapsedTime(&tsplit, c.t1.b, c.t6.a));   // (else 0)
     c.ms_split = (double)tsplit;
     c.ms_scan = c.ms_split + c.ms_range;
     const unsigned long long* h = c.h_out.as<unsigned long long>();
@@ -3009,10 +3068,13 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   uint64_t cap = c.region_cap_force ? c.region_cap_force : region_cap(est);
   c.ms_clear = 0;
   ACount a;
+  c.route_ready = false;
+  const bool hold = c.route_req;                    // (pg_route_stage_a: stage A only)
+  c.route_req = false;
   // after a first build the whole build is queued at once (finish_build's
   // spec form: one host round trip instead of two); the table is then sized
   // from the last build's records per window, 5 % up
-  if (c.u_ratio > 0 && !c.region_cap_force) {
+  if (c.u_ratio > 0 && !c.region_cap_force && !hold) {
     enqueue_stageA(c, cap, ntiles, rc0, extra_empty, SA_WHOLE, false);
     a.total = (uint64_t)(c.u_ratio * 1.05 * (double)c.windows_fw) + extra;
     a.maxreg = cap;
@@ -3036,6 +3098,109 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   c.ms_insert = c.t1.ms();
   c.sentinel = a.sentinel ? 1 : 0;
   c.n_records_a = a.total;
+  if (hold) {                                       // the records stay in their regions for their owners
+    const unsigned long long* h = c.h_pin.as<unsigned long long>();   // (stageA_read's copy of the cursors)
+    c.route_reg.assign(NREG, 0);
+    for (int r = 0; r < NREG; ++r) c.route_reg[r] = std::min<uint64_t>(h[CSTRIDE * r], c.capA);
+    c.route_total = a.total;
+    c.route_maxreg = a.maxreg;
+    c.route_maxbin = a.maxbin;
+    c.route_sentinel = a.sentinel;
+    c.route_ready = true;
+    return;
+  }
+  finish_build(c, a, false);
+  if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
+}
+
+// ---- routed exchange.  The owner of a stage A record is the top lg bits of
+// its coarse bin (the top bits of h = perm(key)): with 2^lg owners, owner o
+// holds bins [o, o + 1) << (cbits - lg), i.e. regions of consecutive indices,
+// so routing is a segmented copy of whole regions, not a per-record split.
+// An owner builds its table over h rotated left by lg bits (TableView.rot):
+// its keys, whose top lg bits of h are all o, then spread over the whole
+// bucket space and the table is sized from the owner's own records.
+static int route_owner(const Ctx& c, int region, int lg) { return (region / 8) >> (c.cbits - lg); }
+static void route_check(const Ctx& c, int lg, const char* what) {
+  if (!c.route_ready) throw Error(-22, std::string(what) + ": no held stage A (pg_route_stage_a)");
+  if (lg < 0 || lg > c.cbits) throw Error(-22, std::string(what) + ": owners must be a power of two <= 2^cbits");
+}
+void route_counts(Ctx& c, int lg, uint64_t* counts) {
+  route_check(c, lg, "route_counts");
+  for (int o = 0; o < (1 << lg); ++o) counts[o] = 0;
+  for (int r = 0; r < NREG; ++r) counts[route_owner(c, r, lg)] += c.route_reg[r];
+}
+
+// rows of region blockIdx.y (records [0, roff[r+1] - roff[r]) of it) to
+// out + roff[r] as 16-byte rows {h, mask word, 0}, with their owner's
+// row_check sum (one atomic per block, over CSPR words per owner)
+__global__ void __launch_bounds__(256) k_route_scatter(const unsigned long long* __restrict__ key,
+                                                       const uint32_t* __restrict__ mw, uint64_t cap,
+                                                       const unsigned long long* __restrict__ roff, Slot* __restrict__ out,
+                                                       unsigned long long* __restrict__ sums, uint32_t oshift) {
+  __shared__ unsigned long long s_red[4];
+  const uint32_t r = blockIdx.y;
+  const uint64_t o0 = roff[r], nr = roff[r + 1] - o0;
+  unsigned long long acc = 0ull;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nr; i += (uint64_t)gridDim.x * 256ull) {
+    const unsigned long long h = key[(uint64_t)r * cap + i];
+    const uint32_t m = mw[(uint64_t)r * cap + i];
+    out[o0 + i] = Slot{h, m, 0u};
+    acc += row_check(h, (uint64_t)m);
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+  if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long t = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    if (t) atomicAdd(&sums[((r / 8) >> oshift) * CSPR + (blockIdx.x % CSPR)], t);
+  }
+}
+
+void route_scatter(Ctx& c, int lg, void* d_out, uint64_t out_cap, uint64_t* sums) {
+  route_check(c, lg, "route_scatter");
+  const int np = 1 << lg;
+  const size_t nw = (NREG + 1) + (size_t)np * CSPR;
+  c.route_buf.reserve(8 * nw);
+  c.route_pin.reserve(8 * nw);
+  auto* h = c.route_pin.as<unsigned long long>();
+  uint64_t tot = 0, mx = 0;
+  for (int r = 0; r < NREG; ++r) {
+    h[r] = tot;
+    tot += c.route_reg[r];
+    mx = std::max<uint64_t>(mx, c.route_reg[r]);
+  }
+  h[NREG] = tot;
+  if (out_cap < tot) throw Error(-22, "route_scatter: output buffer too small");
+  for (size_t i = NREG + 1; i < nw; ++i) h[i] = 0ull;
+  auto* d = c.route_buf.as<unsigned long long>();
+  PG_HIP(hipMemcpyAsync(d, h, 8 * nw, hipMemcpyHostToDevice, c.stream));
+  if (tot)
+    hipLaunchKernelGGL(k_route_scatter, dim3(grid_for(mx, 256, 256), NREG), dim3(256), 0, c.stream,
+                       c.recA_key.as<unsigned long long>(), c.recA_mw.as<uint32_t>(), c.capA, d,
+                       reinterpret_cast<Slot*>(d_out), d + NREG + 1, (uint32_t)(c.cbits - lg));
+  PG_HIP(hipGetLastError());
+  PG_HIP(hipMemcpyAsync(h + NREG + 1, d + NREG + 1, 8 * (size_t)np * CSPR, hipMemcpyDeviceToHost, c.stream));
+  c.sync();
+  for (int o = 0; o < np; ++o) {
+    uint64_t t = 0;
+    for (int j = 0; j < CSPR; ++j) t += h[NREG + 1 + (size_t)o * CSPR + j];
+    sums[o] = t;
+  }
+}
+
+// the held records are the owner's (every owner is this rank: world 1):
+// stages B and C on them where they lie
+void route_finish(Ctx& c) {
+  route_check(c, 0, "route_finish");
+  c.route_ready = false;
+  init_hash(c);
+  ACount a;
+  a.total = c.route_total;
+  a.maxreg = c.route_maxreg;
+  a.maxbin = c.route_maxbin;
+  a.sentinel = c.route_sentinel;
+  c.sentinel = a.sentinel ? 1 : 0;
   finish_build(c, a, false);
   if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;
 }
@@ -3209,8 +3374,11 @@ void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nse
 
 // OR-merge received exchange records into a fresh owner table (stage A from
 // the records, then stages B and C as a build).
-void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, int sentinel) {
-  init_hash(c);
+// rot >= 0 (pg_route_merge): the rows are routed stage A records {h, mask
+// word} of this owner, re-binned on h rotated left by rot bits.
+void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, int sentinel, int rot) {
+  init_hash(c, rot > 0 ? (uint32_t)rot : 0u);
+  c.route_ready = false;
   c.early_split_used = false;
   uint64_t cap = region_cap(n + 64);
   ACount a;
@@ -3226,8 +3394,8 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
     PG_HIP(hipStreamWaitEvent(c.stream2, c.ev[0], 0));
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
     if (n) {
-      hipLaunchKernelGGL(k_slots_emit, dim3(grid_for(n, 4 * IBLOCK, 4096)), dim3(IBLOCK), 0, c.stream,
-                         reinterpret_cast<const Slot*>(d_pairs), n, c.tv, O,
+      hipLaunchKernelGGL(rot >= 0 ? k_route_emit : k_slots_emit, dim3(grid_for(n, 4 * IBLOCK, 4096)), dim3(IBLOCK), 0,
+                         c.stream, reinterpret_cast<const Slot*>(d_pairs), n, c.tv, O,
                          c.flags.as<unsigned long long>() + N_FLAGS / 2);
       PG_HIP(hipGetLastError());
     }

@@ -118,14 +118,18 @@ struct PinBuf {
 
 // Per-kernel timing on the context's stream (HIP events), so callers can
 // price the dominant kernel against the HBM roofline.
+// (off: no event is recorded and ms() is 0 - PG_TUNE_TIMERS 0, to price the
+// timing events themselves)
 struct Timer {
   hipEvent_t a = nullptr, b = nullptr;
+  bool off = false;
   void init() {
     if (!a) { PG_HIP(hipEventCreate(&a)); PG_HIP(hipEventCreate(&b)); }
   }
-  void start(hipStream_t s) { PG_HIP(hipEventRecord(a, s)); }
-  void stop(hipStream_t s) { PG_HIP(hipEventRecord(b, s)); }
+  void start(hipStream_t s) { if (!off) PG_HIP(hipEventRecord(a, s)); }
+  void stop(hipStream_t s) { if (!off) PG_HIP(hipEventRecord(b, s)); }
   double ms() {
+    if (off) return 0.0;
     float t = 0;
     PG_HIP(hipEventSynchronize(b));
     PG_HIP(hipEventElapsedTime(&t, a, b));
@@ -145,6 +149,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;  // side stream: K3 work passes overlap the next coverage pass
   hipStream_t stream3 = nullptr;  // copy stream: chunked host uploads (pg_parse_host, pg_build_host)
+  hipStream_t stream_hi = nullptr; // high priority: K1's header pass and record table beside the emission
   hipEvent_t ev[16] = {};         // ordering events between the two streams
   hipEvent_t rec_ev = nullptr;    // the record table's copy to the host (K1)
   hipEvent_t cev[16] = {};        // chunk-landed events of the copy stream
@@ -152,6 +157,7 @@ struct Ctx {
   int k3_chunks = 0;              // pg_tune: K3 chunks (0 = by tile count)
   int k3_wblk = 0;                // pg_tune: work blocks per CU, low 4 bits; last chunk's, high 4 bits (0 = 2)
   int k3_emit = 0;                // pg_tune: work pass (0 = two halves per segment, 1 = one)
+  int k1_form = 0;                // pg_tune: K1 form bits (PG_TUNE_K1; default: the per-step span pass)
   int k3_tail = 0;                // pg_tune: last K3 chunk in 16ths of the others (0 = 10)
   int k3_head = 0;                // pg_tune: first K3 chunk in 16ths of the others (0 = 16)
   int k3_cover = 0;               // pg_tune: coverage pass (0 = packed form, 1 = LDS-staged members, 2 = quad form)
@@ -183,6 +189,15 @@ struct Ctx {
   DevBuf p2;                      // uint32 per 16 bases: 2-bit codes (class & 3), the packed base stream
   DevBuf e16;                     // uint8 per 16 bases: nonzero if any is not ACGT
   bool cls_full = false;          // every chunk of `cls` written (ensure_cls)
+  // ---- routed exchange (pg_route_*): the last build's stage A records held
+  // in their regions for their owners instead of stages B/C
+  bool route_req = false;         // the next build_dbg stops after stage A
+  bool route_ready = false;       // stage A records held (route_reg: per region, clipped)
+  uint64_t route_total = 0, route_maxreg = 0, route_maxbin = 0;
+  unsigned route_sentinel = 0;
+  std::vector<uint64_t> route_reg;
+  DevBuf route_buf;               // region offsets and owner sums of pg_route_scatter
+  PinBuf route_pin;
   uint64_t n_cls = 0;             // length of the compacted stream (bases before the first header too)
   DevBuf scratch;                 // rocPRIM temp storage
   DevBuf rec_pack;                // the scan total + int64 [5][rec_cap]: the record table for one copy
@@ -353,7 +368,11 @@ void build_rdbg(Ctx& c);
 uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap);
 uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap);
 uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts);
-void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel);
+void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel, int rot = -1);
+// routed exchange: owners of the held stage A records (2^lg owners)
+void route_counts(Ctx& c, int lg, uint64_t* counts);
+void route_scatter(Ctx& c, int lg, void* d_out, uint64_t out_cap, uint64_t* sums);
+void route_finish(Ctx& c);
 void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums);
 // pg_persist.hip
 struct PreEnt {                   // one staged oakht slot: oriented key, 12-bit mask, count

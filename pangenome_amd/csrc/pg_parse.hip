@@ -187,6 +187,7 @@ struct Fn {
   long long last, last2;
   uint32_t o;                                       // bit s: out-state for in-state s
 };
+constexpr uint32_t FN_TODO = 0xFFFFFFFFu;           // (o: a span k_span_whole left to k_span_fix)
 __host__ __device__ __forceinline__ Fn fn_identity() { return Fn{0, 0, 0, 0, -1, -1, 2u}; }
 struct FnThen {                                     // a, then b (associative, not commutative)
   __host__ __device__ __forceinline__ Fn operator()(const Fn& a, const Fn& b) const {
@@ -214,6 +215,184 @@ __device__ __forceinline__ void load_span(const uint8_t* buf, uint64_t p0, uint6
   }
 }
 
+__device__ __forceinline__ int wave_min_i32(int x) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const int y = __shfl_xor(x, o, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+
+// The per-step form of the span pass: per 1 KiB wave step either the fast
+// step (below) or the general step.  vs(s) = the lane's 16 bytes of step s.
+// The function of the `nsteps` 1 KiB steps from p0 (nothing at or past n),
+// the same on every lane.
+template <bool UNROLL, class StepBytes>
+__device__ __forceinline__ Fn seg_fn(uint64_t n, uint64_t p0, int nsteps, int lane, uint32_t carry, StepBytes vs) {
+  uint32_t c0 = 0, c1 = 0, fo = 2u;                           // identity: out(s) = s
+  uint32_t nl = 0, hdr = 0;
+  int top = -1, second = -1;
+  auto last_two = [&](uint32_t nlm, uint64_t p) {             // the span's last two '\n'
+    if (nlm) {
+      const int rel = (int)(p - p0);
+      const int t = 31 - __builtin_clz(nlm);
+      const uint32_t rest = nlm & ~(1u << t);
+      second = rest ? rel + 31 - __builtin_clz(rest) : top;
+      top = rel + t;
+    }
+  };
+  auto step = [&](int s) {
+    const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
+    const uint4 v = vs(s);
+    // Fast step (wave-uniform): every byte below n - 1, no '>' in the step,
+    // and the span-so-far sends either in-state to out-state 0 - then no
+    // header line is open or starts, and every byte but '\n' is content
+    if (fo == 0u && p0 + (uint64_t)(s + 1) * WSTEP < n) {
+      uint32_t gt = 0, nlm = 0;
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        gt |= zmatch(w[d], 0x3E3E3E3Eu);
+        nlm |= pack4(zmatch(w[d], 0x0A0A0A0Au)) << (4 * d);
+      }
+      if (!__ballot(gt != 0u)) {
+        carry = (uint32_t)(__ballot((nlm >> 15) & 1u) >> 63) & 1u;
+        const uint32_t cnt = (uint32_t)__builtin_popcount(nlm);
+        c0 += 16u - cnt;
+        c1 += 16u - cnt;
+        nl += cnt;
+        last_two(nlm, p);
+        return;
+      }
+    }
+    const LaneStep ls = lane_step(v, p, n, lane, carry);
+    // lane-local counts for span in-state 0 / 1: a lane's in-state is fixed by
+    // a line start in a lower lane, else it is the step's in-state fo(s)
+    const uint32_t m0 = lane_content(ls, lane_region(ls, 0)), m1 = lane_content(ls, lane_region(ls, 1));
+    const uint32_t f0 = fo & 1u, f1 = (fo >> 1) & 1u;         // span-so-far out-states
+    const bool det = (ls.B & ls.lt) != 0;
+    const uint32_t d = lane_in(ls, 0);
+    c0 += __builtin_popcount((det ? d : f0) ? m1 : m0);
+    c1 += __builtin_popcount((det ? d : f1) ? m1 : m0);
+    fo = step_out(ls, f0) | step_out(ls, f1) << 1;
+    nl += __builtin_popcount(ls.nlm);
+    hdr += __builtin_popcount(ls.hs);
+    last_two(ls.nlm, p);
+  };
+  if constexpr (UNROLL) {
+#pragma unroll
+    for (int s = 0; s < WSTEPS; ++s) {
+      if (s >= nsteps || p0 + (uint64_t)s * WSTEP >= n) break;   // wave-uniform
+      step(s);
+    }
+  } else {
+#pragma unroll 1
+    for (int s = 0; s < nsteps; ++s) {
+      if (p0 + (uint64_t)s * WSTEP >= n) break;
+      step(s);
+    }
+  }
+  // per lane: c0, c1 <= 256 and nl, hdr <= 256, so the packed sums stay in 16 bits
+  const uint32_t cs = __builtin_amdgcn_readlane(wave_incl_sum(c0 | c1 << 16), 63);
+  const uint32_t cnts = __builtin_amdgcn_readlane(wave_incl_sum(nl | hdr << 16), 63);
+  const int last = wave_max_i32(top);
+  const int last2 = wave_max_i32(top != last ? top : second);
+  const long long b = (long long)p0;
+  return Fn{cs & 0xFFFFu, cs >> 16, cnts & 0xFFFFu, cnts >> 16, last >= 0 ? b + last : -1,
+            last2 >= 0 ? b + last2 : -1, fo};
+}
+
+// K1's span pass, whole-span form (PG_TUNE_K1 = 1): one wave per 16 KiB
+// span -> its function of the in-state.  A span wholly below byte n - 1 with
+// no '>' in it is counted in one pass, 4 KiB per round with the next rounds'
+// loads in flight (76 VGPRs, 6 waves per SIMD) - per dword the exact
+// zero-byte test of w ^ '\n' summed with v_bcnt (bytes == '\n' = 32 -
+// popcount(t | x | 0x7F7F7F7F), t = (x & 0x7F7F7F7F) + 0x7F7F7F7F) and the
+// any-zero test of w ^ '>' ORed up, no ballot or branch per step.  Its
+// function then follows from the newline count, the first newline (in-state 1
+// without a line start at the span start: the header bytes before it are no
+// content) and the last two (the record table's line ends), found afterwards
+// by re-reading the first / last steps (L2).  Any other span is marked
+// (o = FN_TODO) for k_span_fix.
+__device__ __forceinline__ void span_whole(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0, uint64_t nspan,
+                                         Fn* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t span = span0 + (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
+  if (span >= nspan) return;                                  // wave-uniform
+  const uint64_t p0 = span * WSPAN;
+  const uint32_t carry = p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u);
+  auto step_at = [&](int s) {
+    const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
+    return p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+  };
+  if (p0 + WSPAN < n) {
+    constexpr int R = 4;                                      // steps per round
+    uint32_t acc = 0, g = 0;
+    uint4 cur[R], nxt[R];
+    const uint4* src = reinterpret_cast<const uint4*>(buf + p0) + lane;
+#pragma unroll
+    for (int j = 0; j < R; ++j) cur[j] = src[j * 64];
+#pragma unroll
+    for (int r = 0; r < WSTEPS / R; ++r) {
+      if (r + 1 < WSTEPS / R) {
+#pragma unroll
+        for (int j = 0; j < R; ++j) nxt[j] = src[((r + 1) * R + j) * 64];
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        const uint32_t w[4] = {cur[j].x, cur[j].y, cur[j].z, cur[j].w};
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const uint32_t x = w[d] ^ 0x0A0A0A0Au;
+          const uint32_t t = (x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+          acc += (uint32_t)__builtin_popcount(t | x | 0x7F7F7F7Fu);
+          const uint32_t y = w[d] ^ 0x3E3E3E3Eu;
+          g |= (y - 0x01010101u) & ~y;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < R; ++j) cur[j] = nxt[j];
+    }
+    if (!__ballot((g & 0x80808080u) != 0u)) {
+      const uint32_t nl_lane = 32u * 4u * WSTEPS - acc;
+      const uint32_t nl = __builtin_amdgcn_readlane(wave_incl_sum(nl_lane), 63);
+      int first = 0x7FFFFFFF, last = -1, last2 = -1;
+      if (nl) {
+        if (!carry) {
+          for (int s = 0; s < WSTEPS; ++s) {                  // the first '\n' (wave-uniform exit)
+            const uint32_t m = eq16(step_at(s), 0x0A0A0A0Au);
+            first = wave_min_i32(m ? s * WSTEP + lane * 16 + __builtin_ctz(m) : 0x7FFFFFFF);
+            if (first != 0x7FFFFFFF) break;
+          }
+        }
+        int found = 0;
+        for (int s = WSTEPS - 1; s >= 0; --s) {               // the last two (wave-uniform exit)
+          const uint32_t m = eq16(step_at(s), 0x0A0A0A0Au);
+          const int t1 = m ? s * WSTEP + lane * 16 + 31 - __builtin_clz(m) : -1;
+          const uint32_t rest = m ? m & ~(1u << (31 - __builtin_clz(m))) : 0u;
+          const int t2 = rest ? s * WSTEP + lane * 16 + 31 - __builtin_clz(rest) : -1;
+          const int a1 = wave_max_i32(t1);
+          const int a2 = wave_max_i32(t1 != a1 ? t1 : t2);
+          if (found == 0) { last = a1; last2 = a2; found = (a1 >= 0) + (a2 >= 0); }
+          else if (a1 >= 0) { last2 = a1; found = 2; }
+          if (found >= 2) break;
+        }
+      }
+      if (lane == 0) {
+        const long long b = (long long)p0;
+        const unsigned long long c0 = WSPAN - nl;
+        unsigned long long c1;
+        uint32_t o;
+        if (!nl) { c1 = carry ? WSPAN : 0ull; o = carry ? 0u : 2u; }
+        else { c1 = carry ? c0 : c0 - (unsigned long long)first; o = 0u; }
+        out[span] = Fn{c0, c1, nl, 0ull, last >= 0 ? b + last : -1, last2 >= 0 ? b + last2 : -1, o};
+      }
+      return;
+    }
+  }
+  if (lane == 0) out[span].o = FN_TODO;                       // (k_span_fix)
+}
+// The per-step form on all 16 loads in flight (PG_TUNE_K1 = 0).
 __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
                                                      uint64_t nspan, Fn* __restrict__ out) {
   const int lane = threadIdx.x & 63;
@@ -286,6 +465,46 @@ __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__
   }
 }
 
+__global__ void __launch_bounds__(PBLOCK) k_span_whole(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
+                                                       uint64_t nspan, Fn* __restrict__ out) {
+  span_whole(buf, n, span0, nspan, out);
+}
+// The spans k_span_whole left (a '>' in them, or the file's last): a block of
+// 16 waves per 64 spans finds them by their marker; per such span wave w
+// takes step w (its function by the per-step form), and one thread composes
+// the 16 (a span's general steps are a serial chain of ballots one wave would
+// walk alone: ~16 us).
+constexpr int FBLOCK = 64 * WSTEPS;
+__global__ void __launch_bounds__(FBLOCK) k_span_fix(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
+                                                     uint64_t nspan, Fn* __restrict__ out) {
+  __shared__ Fn s_f[WSTEPS];
+  __shared__ unsigned long long s_todo;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t base = span0 + (uint64_t)blockIdx.x * 64;
+  if (w == 0) {
+    const uint64_t mine = base + lane;
+    const unsigned long long t = __ballot(mine < nspan && out[mine].o == FN_TODO);
+    if (lane == 0) s_todo = t;
+  }
+  __syncthreads();
+  for (unsigned long long todo = s_todo; todo; todo &= todo - 1) {   // block-uniform
+    const uint64_t span = base + (uint64_t)__builtin_ctzll(todo);
+    const uint64_t ps = span * WSPAN + (uint64_t)w * WSTEP;
+    const uint32_t carry = ps == 0 ? 1u : (ps - 1 < n && buf[ps - 1] == 10 ? 1u : 0u);
+    const uint64_t p = ps + (uint64_t)lane * 16;
+    const uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+    const Fn f = seg_fn<true>(n, ps, 1, lane, carry, [&](int) { return v; });
+    if (lane == 0) s_f[w] = f;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      Fn r = s_f[0];
+      for (int q = 1; q < WSTEPS; ++q) r = FnThen{}(r, s_f[q]);
+      out[span] = r;
+    }
+    __syncthreads();
+  }
+}
+
 __constant__ uint8_t c_byte_class[256];
 
 // The packed word and exception byte of 16 class bytes (4 dwords, 4 classes
@@ -306,6 +525,7 @@ __device__ __forceinline__ uint32_t pack_word(const uint4& v, uint32_t& exc) {
   return out;
 }
 
+template <int PF>
 __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
                                                  uint64_t nspan, const Fn* __restrict__ incl,
                                                  uint8_t* __restrict__ out, uint32_t* __restrict__ p2,
@@ -340,12 +560,22 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
   uint32_t state = pre.o & 1u;
   uint32_t carry = p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u);
   // one step of prefetch: occupancy (LDS round trip per step) beats depth here
+  // (PF = 2: two steps in flight ahead, PG_TUNE_K1 bit 1)
   uint64_t p = p0 + (uint64_t)lane * 16;
   uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+  uint4 v2 = make_uint4(0, 0, 0, 0);
+  if (PF == 2 && p + WSTEP < n) v2 = load16(buf, p + WSTEP, n);
   for (int s = 0; s < WSTEPS; ++s) {
     if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
     const uint64_t pn = p + WSTEP;
-    const uint4 vn = (s + 1 < WSTEPS && pn < n) ? load16(buf, pn, n) : make_uint4(0, 0, 0, 0);
+    uint4 vn;
+    if (PF == 2) {
+      vn = v2;
+      const uint64_t pnn = pn + WSTEP;
+      v2 = (s + 2 < WSTEPS && pnn < n) ? load16(buf, pnn, n) : make_uint4(0, 0, 0, 0);
+    } else {
+      vn = (s + 1 < WSTEPS && pn < n) ? load16(buf, pn, n) : make_uint4(0, 0, 0, 0);
+    }
     uint32_t ctot;
     // Fast step (wave-uniform): in-state 0, every byte below n - 1, no '>',
     // at most one '\n' per lane and every other byte one of ACGTacgt - the
@@ -437,22 +667,19 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
   }
 }
 
-// The record table's header entries, before (and beside) the emission: each
-// header's byte span and its record's start in the compacted stream.  Only
-// the spans a header starts in, or whose first line continues one, do any
-// work (C3: ~100 of 31 K spans); they step through their 16 KiB with the
-// general step's line logic and content counts.  With the record table out
-// of k_emit, its round trip to the host runs while the emission does.
-__global__ void __launch_bounds__(PBLOCK) k_headers(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
-                                                    uint64_t nspan, const Fn* __restrict__ incl, uint64_t rcap,
-                                                    long long* __restrict__ rec_start,
-                                                    long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t span = span0 + (uint64_t)blockIdx.x * WAVES + (threadIdx.x >> 6);
-  if (span >= nspan) return;                                  // wave-uniform
-  const Fn pre = span ? incl[span - 1] : fn_identity();
+// The record table's header entries, beside the emission: each header's byte
+// span and its record's start in the compacted stream.  Only the spans a
+// header starts in, or whose first line continues one, do any work (C3: ~100
+// of 31 K spans).  A block of 4 waves per 64 spans finds them by one ballot
+// and deals them out to its waves; a wave steps through its span's 16 KiB
+// (all loads in flight) with the general step's line logic and content
+// counts.  Small blocks and high wave priority: beside the emission they are
+// placed and issued at once (blocks of 16 waves, one per step, found no room
+// there: ~180 us; alone they took ~10 us on the critical path).
+__device__ __forceinline__ void header_span(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span, int lane,
+                                            const Fn& pre, uint64_t rcap, long long* __restrict__ rec_start,
+                                            long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
   uint32_t state = pre.o & 1u;
-  if (incl[span].hdr == pre.hdr && !state) return;            // no header starts or ends here
   const uint64_t p0 = span * WSPAN;
   unsigned long long off = pre.c0, rec = pre.hdr;
   uint4 v[WSTEPS];                                            // (every load in flight at once)
@@ -488,6 +715,32 @@ __global__ void __launch_bounds__(PBLOCK) k_headers(const uint8_t* __restrict__ 
     off += tot & 0xFFFFu;
     rec += tot >> 16;
     state = step_out(ls, state);
+  }
+}
+__global__ void __launch_bounds__(PBLOCK) k_headers(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span0,
+                                                    uint64_t nspan, const Fn* __restrict__ incl, uint64_t rcap,
+                                                    long long* __restrict__ rec_start,
+                                                    long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
+  __builtin_amdgcn_s_setprio(3);
+  __shared__ unsigned long long s_todo;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t base = span0 + (uint64_t)blockIdx.x * 64;
+  if (w == 0) {
+    const uint64_t mine = base + lane;
+    bool need = false;
+    if (mine < nspan) {                                       // a header starts or ends here
+      const Fn pre = mine ? incl[mine - 1] : fn_identity();
+      need = incl[mine].hdr != pre.hdr || (pre.o & 1u);
+    }
+    const unsigned long long t = __ballot(need);
+    if (lane == 0) s_todo = t;
+  }
+  __syncthreads();
+  int j = 0;
+  for (unsigned long long todo = s_todo; todo; todo &= todo - 1, ++j) {   // wave w: every WAVES-th of them
+    if ((j & (WAVES - 1)) != w) continue;
+    const uint64_t span = base + (uint64_t)__builtin_ctzll(todo);
+    header_span(buf, n, span, lane, span ? incl[span - 1] : fn_identity(), rcap, rec_start, hdr_start, hdr_end);
   }
 }
 
@@ -608,7 +861,6 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   c.t0.init();
   c.t0.start(st);
   const uint64_t nspan = (n + WSPAN - 1) / WSPAN;
-  const unsigned nblk = (unsigned)((nspan + WAVES - 1) / WAVES);
   c.span_sum.reserve(sizeof(Fn) * nspan);
   c.span_start.reserve(sizeof(Fn) * nspan);
   auto* fns = c.span_sum.as<Fn>();
@@ -619,6 +871,20 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   auto scan = [&](uint64_t upto) {
     size_t b = c.scratch.cap;
     PG_HIP(rocprim::inclusive_scan(c.scratch.p, b, fns, incl, (size_t)upto, FnThen{}, st));
+  };
+  // span functions of spans s0 .. s1 (k_span_whole + k_span_fix, or the
+  // per-step k_span_sum)
+  auto span_pass = [&](uint64_t s0, uint64_t s1) {
+    const unsigned g = (unsigned)((s1 - s0 + WAVES - 1) / WAVES);
+    if (c.k1_form & 1) {
+      hipLaunchKernelGGL(k_span_whole, dim3(g), dim3(PBLOCK), 0, st, c.d_fasta, n, s0, s1, fns);
+      PG_HIP(hipGetLastError());
+      hipLaunchKernelGGL(k_span_fix, dim3((unsigned)((s1 - s0 + 63) / 64)), dim3(FBLOCK), 0, st, c.d_fasta, n, s0, s1,
+                         fns);
+    } else {
+      hipLaunchKernelGGL(k_span_sum, dim3(g), dim3(PBLOCK), 0, st, c.d_fasta, n, s0, s1, fns);
+    }
+    PG_HIP(hipGetLastError());
   };
   c.cls.reserve(n + 64);
   c.p2.reserve(4 * (n / 16 + 8));
@@ -636,7 +902,8 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     c.h_pin.reserve(64 + 40 * rcap);
   };
   auto emit = [&](uint64_t s0, uint64_t s1) {
-    hipLaunchKernelGGL(k_emit, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta, n, s0,
+    hipLaunchKernelGGL((c.k1_form & 2) ? k_emit<2> : k_emit<1>, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)),
+                       dim3(PBLOCK), 0, st, c.d_fasta, n, s0,
                        s1, incl, c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>());
     PG_HIP(hipGetLastError());
     // boundaries s0 .. s1 (s1 = nspan: the stream's end, incl[nspan - 1])
@@ -648,12 +915,12 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   // of the spans so far (k_records, total = incl[s1 - 1]) and its copy to the
   // host, marked by rec_ev: queued before the spans' emission, so the host
   // reads the table while the emission runs
-  // (on `rs`: the context's stream, or for a whole-file parse the second
-  // stream, beside the emission)
+  // (on `rs`: the context's stream, or for a whole-file parse the
+  // high-priority stream, beside the emission)
   hipStream_t rs = st;
   auto records = [&](uint64_t s0, uint64_t s1, uint64_t rcap) {
     auto* hdr = c.rec_hdr.as<long long>();
-    hipLaunchKernelGGL(k_headers, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, rs, c.d_fasta, n,
+    hipLaunchKernelGGL(k_headers, dim3((unsigned)((s1 - s0 + 63) / 64)), dim3(PBLOCK), 0, rs, c.d_fasta, n,
                        s0, s1, incl, rcap, c.rec_start.as<long long>(), hdr, hdr + rcap);
     PG_HIP(hipGetLastError());
   };
@@ -708,8 +975,7 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
       const uint64_t s0 = off / WSPAN, s1 = std::min(nspan, (off + len + WSPAN - 1) / WSPAN);
       PG_HIP(hipStreamWaitEvent(st, c.cev[i & 15], 0));
       up.consumed(i);
-      hipLaunchKernelGGL(k_span_sum, dim3((unsigned)((s1 - s0 + WAVES - 1) / WAVES)), dim3(PBLOCK), 0, st, c.d_fasta,
-                         n, s0, s1, fns);
+      span_pass(s0, s1);
       PG_HIP(hipGetLastError());
       scan(s1);
       records(s0, s1, rcap0);
@@ -738,15 +1004,15 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     }
     upload->finish();
   } else {
-    hipLaunchKernelGGL(k_span_sum, dim3(nblk), dim3(PBLOCK), 0, st, c.d_fasta, n, (uint64_t)0, nspan, fns);
+    span_pass(0, nspan);
     PG_HIP(hipGetLastError());
     scan(nspan);
     // the header pass, the record table and its copy to the host on the
-    // second stream, beside the emission (they read the FASTA's header
-    // spans and the scan, nothing the emission writes)
+    // high-priority stream, beside the emission (they read the FASTA's
+    // header spans and the scan, nothing the emission writes)
     PG_HIP(hipEventRecord(c.ev[14], st));
-    PG_HIP(hipStreamWaitEvent(c.stream2, c.ev[14], 0));
-    rs = c.stream2;
+    PG_HIP(hipStreamWaitEvent(c.stream_hi, c.ev[14], 0));
+    rs = c.stream_hi;
     records(0, nspan, rcap0);
     pending = {0, nspan};
   }

@@ -422,6 +422,68 @@ def exchange_and_reduce(table, world: int, rank: int, device, sentinel_local: bo
                          want_sum=want_sum, route=chk) + (sent,)
 
 
+class _Routed:
+    """A shard whose last build held its stage A records for their owners
+    (route_stage_a), seen by _route / _owner_reduce as a table: its
+    "partition" is the held records grouped by owner (whole stage A regions:
+    the owner is the top bits of the record's h), its "merge" the owner's
+    build from the received records (stages A, B, C once)."""
+
+    def __init__(self, shard, nparts: int, counts):
+        self.sh, self.nparts, self.counts = shard, nparts, np.asarray(counts, np.uint64)
+
+    def partition(self, nparts, ptr=None, cap=0):
+        if nparts != self.nparts:
+            raise ValueError("routed records are held for %d owners, not %d" % (self.nparts, nparts))
+        if ptr is not None:
+            self.sums = self.sh.route_scatter(nparts, ptr, cap)
+        return self.counts
+
+    def partition_sums(self, nparts):
+        return self.sums
+
+    def entries(self):
+        return int(self.counts.sum())
+
+    def rows_checksum(self, d_rows, seg_off):
+        return self.sh.rows_checksum(d_rows, seg_off)
+
+    def merge(self, ptr, n, sentinel=False):
+        self.sh.route_merge(ptr, n, self.nparts, sentinel)
+
+    def merge_check(self):
+        return self.sh.merge_check()
+
+    def build_rdbg(self):
+        return self.sh.build_rdbg()
+
+
+def exchange_routed(shard, world: int, rank: int, device, flags, extra: int, rc0: bool, group=None, tm=None,
+                    force: bool = False):
+    """The N>1 build-and-reduce step with the owners building once: stage A
+    of this rank's records (held, not built: route_stage_a), the records to
+    their owners in one all-to-all (the owner = the top log2(world) bits of
+    h, so a rank's run for one owner is whole stage A regions: a segmented
+    copy, pg_route_scatter), and each owner's stages A (re-binning), B and
+    C over what it received (pg_route_merge) - no local table, no
+    pg_dbg_partition, no second full build.  World 1: stages B and C on the
+    held records where they lie (pg_route_finish; force: through the
+    scatter, the own run's device copy and the owner merge as at N > 1, to
+    price them).  The same integrity checks
+    as exchange_and_reduce (per-run sums from the scatter to the merge, record
+    conservation).  world must be a power of two.  Returns (n_dbg_total,
+    n_rdbg_total, n_rdbg_local, bytes_sent); `tm` accumulates partition /
+    all_to_all / merge seconds (partition = the scatter of the held regions)."""
+    counts, sentinel = shard.route_stage_a(flags, extra, rc0, world)
+    if world == 1 and not force:
+        t0 = perf_counter()
+        st = shard.route_finish()
+        if tm is not None:
+            tm["merge"] = tm.get("merge", 0.0) + (perf_counter() - t0)
+        return int(st.n_dbg), int(st.n_rdbg), int(st.n_rdbg), 0
+    return exchange_and_reduce(_Routed(shard, world, counts), world, rank, device, sentinel, group, tm)
+
+
 def stream_chunks(flags, seq_len, limit: int) -> list:
     """A rank's flagged records as consecutive chunks of at most `limit`
     forward bases each (a longer record is a chunk of its own): record flag
@@ -779,6 +841,23 @@ class GpuShard:
 
     def rows_checksum(self, d_rows, seg_off):
         return self.ctx.rows_checksum(d_rows, seg_off)
+
+    # the routed exchange (exchange_routed): stage A held for the owners
+    def route_stage_a(self, flags, extra, rc0, nparts):
+        return self.ctx.route_stage_a(flags, int(extra), bool(rc0), int(nparts))
+
+    def route_scatter(self, nparts, ptr, cap):
+        return self.ctx.route_scatter(nparts, ptr, cap)
+
+    def route_finish(self):
+        st = self.ctx.route_finish()
+        self.n_entries = int(st.n_slots)
+        return st
+
+    def route_merge(self, ptr, n, nparts, sentinel=False):
+        st = self.ctx.route_merge(ptr, n, nparts, sentinel)
+        self.n_entries = int(st.n_slots)
+        return st
 
     def build_rdbg(self):
         return self.ctx.build_rdbg()

@@ -182,13 +182,13 @@ class NumpyTable:
         uniq, start = np.unique(c, return_index=True)
         self.c, self.mw = uniq, np.bitwise_or.reduceat(word, start) if c.size else word
 
-    def _owner(self, nparts):
-        z = self.c * np.uint64(0x9E3779B97F4A7C15)
+    def _owner(self, nparts, routed=False):
+        z = self.c * np.uint64(0x9E3779B97F4A7C15 if not routed else 0xC2B2AE3D27D4EB4F)
         return ((z >> np.uint64(40)) % np.uint64(nparts)).astype(np.int64)
 
-    def partition(self, nparts, ptr=None, cap=0):
+    def partition(self, nparts, ptr=None, cap=0, routed=False):
         from pangenome_amd.dist import row_check_sum
-        own = self._owner(nparts)
+        own = self._owner(nparts, routed)
         counts = np.bincount(own, minlength=nparts).astype(np.uint64)
         if ptr is not None:
             buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * cap)).from_address(ptr)).reshape(cap, 2)
@@ -309,6 +309,25 @@ class OracleShard:
 
     def merge_check(self):
         return self.table.merge_check()
+
+    # the routed exchange: the local table's entries stand in for the held
+    # stage A records, grouped by an owner function of their own
+    def route_stage_a(self, flags, extra, rc0, nparts):
+        sent = self.build(flags, extra, rc0)
+        self.route_n = nparts
+        return self.table.partition(nparts, routed=True), sent
+
+    def route_scatter(self, nparts, ptr, cap):
+        assert nparts == self.route_n
+        self.table.partition(nparts, ptr, cap, routed=True)
+        return self.table.partition_sums(nparts)
+
+    def route_finish(self):
+        return self.table.build_rdbg()
+
+    def route_merge(self, ptr, n, nparts, sentinel=False):
+        self.table.merge(ptr, n, sentinel)
+        return self.table.build_rdbg()
 
     def build_rdbg(self):
         return self.table.build_rdbg()

@@ -77,6 +77,54 @@ def test_sharded_exchange_matches_single_process(oracle_mod, world, a2a_rows):
     assert sum(out[r][2] for r in range(world)) == ref_rdbg
 
 
+def _routed_worker(rank, world, port, fasta, k, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch.distributed as dist
+    from dist_util import OracleShard
+    from pangenome_amd.dist import exchange_routed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    recs = _records(fasta)
+    mine = b"".join(r if r.endswith(b"\n") else r + b"\n" for r in recs[rank::world])
+    sh = OracleShard(k)
+    meta = sh.load(np.frombuffer(mine, np.uint8))
+    flags = np.ones(meta["seq_len"].shape[0], np.uint8)
+    tm = {}
+    res = exchange_routed(sh, world, rank, "cpu", flags, 0, True, tm=tm)
+    q.put((rank, res + (sorted(tm),)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_routed_exchange_matches_single_process(oracle_mod, world):
+    """exchange_routed (the owners build once from routed stage A records):
+    the sharded totals equal the single-process build; world 1 builds where
+    the records lie, with no exchange at all."""
+    from pangenome_amd import synth
+    k = 27
+    fasta = synth.pangenome(6, 30_000, snp=0.01, indel=1e-3, seed=43) + b">tiny\nACG\n"
+    ref = oracle_mod.OracleRun(fasta, k, 2)
+    ref_dbg = ref.dbg()[0].shape[0]
+    ref_rdbg = ref.rdbg().shape[0]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_routed_worker, args=(r, world, port, fasta, k, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        n_dbg, n_rdbg, _, sent, phases = out[r]
+        assert (n_dbg, n_rdbg) == (ref_dbg, ref_rdbg)
+        assert phases == (["merge"] if world == 1 else ["all_to_all", "merge", "partition", "rows"])
+    assert sum(out[r][2] for r in range(world)) == ref_rdbg
+
+
 def _stream_worker(rank, world, port, q, fasta, k):
     import sys
     sys.path.insert(0, ROOT)

@@ -59,6 +59,54 @@ def _exchange_rank_sharded(rank, world, port, q, shards):
     _exchange_rank(rank, world, port, q, shards[rank])
 
 
+def _routed_rank(rank, world, port, q, shards, force):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from pangenome_amd._lib import Context
+    from pangenome_amd.dist import exchange_routed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = Context(27, 0)
+    out = []
+    for rep in range(2):                                    # (the second build reuses the context's buffers)
+        ctx.set_fasta(shards[rank])
+        ctx.parse()
+        res = exchange_routed(ctx, world, rank, torch.device("cuda", 0), None, 0, True, force=force)
+        keys, masks = ctx.dbg()
+        out.append((res, keys, masks, ctx.rdbg()))
+    q.put((rank, out))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,force", [(1, False), (1, True), (2, False), (4, False)])
+def test_routed_exchange_vs_oracle(oracle_mod, world, force):
+    """dist.exchange_routed through the library: stage A held and routed by
+    the top bits of h (pg_route_stage_a / pg_route_scatter), each owner's
+    stages A-C over what it received on h rotated into its domain
+    (pg_route_merge), or at world 1 stages B/C where the records lie
+    (pg_route_finish).  The owners' dBG (keys and masks) and rdBG are
+    disjoint and their union is the oracle's, twice in a row."""
+    from pangenome_amd import synth
+    fasta = synth.pangenome(8, 200_000, snp=0.005, indel=5e-4, seed=97)
+    recs = [b">" + r for r in fasta.split(b">")[1:]] + [b">short\nACGTA\n", b">tiny\nAC\n"]
+    shards = [b"".join(recs[r::world]) for r in range(world)]
+    ref = oracle_mod.OracleRun(b"".join(recs), 27, 2)
+    ref_keys, ref_masks = ref.dbg()
+    ref_rdbg = ref.rdbg()
+    res = spawn_ranks(world, _routed_rank, (shards, force))
+    for rep in range(2):
+        for r in range(world):
+            n_dbg, n_rdbg, _, _ = res[r][rep][0]
+            assert (n_dbg, n_rdbg) == (ref_keys.shape[0], ref_rdbg.shape[0])
+        keys = np.concatenate([res[r][rep][1] for r in range(world)])
+        masks = np.concatenate([res[r][rep][2] for r in range(world)])
+        o = np.argsort(keys, kind="stable")
+        assert np.array_equal(keys[o], ref_keys) and np.array_equal(masks[o], ref_masks)
+        union = np.sort(np.concatenate([res[r][rep][3] for r in range(world)]))
+        assert np.array_equal(union, ref_rdbg)
+
+
 def _cli_rank(rank, world, port, q, argv, chunk, cwd, dbg_chunk=2 ** 33, stream=None):
     sys.path.insert(0, ROOT)
     import torch
