@@ -22,7 +22,8 @@ import sys
 tag = sys.argv[1] if len(sys.argv) > 1 else "tr"
 config = sys.argv[2] if len(sys.argv) > 2 else "c3"
 SPANS = {
-    "k1_parse": r"k_span_sum|lookback_scan|scan_impl|k_emit\b|k_emit\(|k_records|k_pack_records|k_pack_fix",
+    "k1_parse": r"k_span_sum|k_span_whole|k_span_fix|lookback_scan|scan_impl|k_emit\b|k_emit\(|k_emit<|k_headers|"
+                r"k_records|k_pack_records|k_pack_fix",
     "k3a_cover_emit": r"k_cover|k_emit_work|k_short_emit",
     "k3b_split": r"k_split",
     "k3c_range": r"k_build_range",
