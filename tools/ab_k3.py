@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--genomes", type=int, default=100)
     ap.add_argument("--tune", action="append", default=[])
     ap.add_argument("--host", action="store_true", help="pg_build_host from the page-cache-warm mmap instead")
-    ap.add_argument("--alt", action="store_true", help="(--host) alternate two batches (genomes 0-99, 100-199)")
+    ap.add_argument("--alt", action="store_true", help="alternate two batches (genomes 0-99, 100-199), as bench.py does")
     ap.add_argument("--env", action="append", default=[], help="per-variant environment NAME=V (index-aligned with --tune)")
     args = ap.parse_args()
     import torch
@@ -44,7 +44,7 @@ def main():
         p2 = os.path.join(tmp, "c3b.fa")
         synth.write_pangenome(p2, args.genomes, 5_000_000, first_index=args.genomes, workers=16)
         mms.append(kmer.seq2bytes(p2))
-    d = torch.from_numpy(np.array(mm)).to("cuda:0")
+    ds = [torch.from_numpy(np.array(m)).to("cuda:0") for m in mms]   # (--alt: both batches in HBM)
     if not args.host:
         os.unlink(p)
     digs = [json.load(open(os.path.join(ROOT, "tests", "golden", "scale", n + ".json"))) for n in ("c3a", "c3b")] \
@@ -74,6 +74,7 @@ def main():
             if args.host:
                 st = ctx.build_host(mms[b], True)
             else:
+                d = ds[b]
                 st = ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d)
             ms = 1e3 * (time.perf_counter() - t1)
             ok = dig is None or (st.n_dbg, st.n_rdbg) == (dig["n_dbg"], dig["n_rdbg"])
