@@ -32,7 +32,7 @@ for step in "$@"; do
     benchc4) run bench_c4 900 python bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline --no-cli ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
-    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange --no-concurrent ;;
     pmcsq) bash tools/pmc_kernels.sh "k_emit_work|k_cover_p|k_build_range|k_emit\(|k_span_sum|k_split" sq ;;
     pmc) bash tools/pmc_kernels.sh "k_span_sum|k_emit|k_records|k_pack_fix|k_cover|k_short_emit|k_split|k_build_range|rocprim" tr traffic ;;
     parse) run pytest_parse 600 python -u -m pytest tests/test_gpu_parse.py -x -v --timeout 120 --timeout-method thread ;;
