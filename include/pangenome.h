@@ -359,6 +359,12 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * (ms_parse), bit 1 stage A (ms_insert), bit 2 stages B/C (ms_split,
  * ms_range); 7 (default) = all, 0 = none (the spans read 0). */
 #define PG_TUNE_TIMERS 19
+/* PG_TUNE_K3_ANCHORS: anchors per tile and reference of the packed coverage
+ * pass (3, 4, 5, 6 or 8; 0 = 4).  More anchors find the drift of more of the
+ * short runs between two indels, so fewer windows go to the work pass as
+ * records (C3: 27.6 M stage A records with 3, 24.2 M with 4, 21.8 M with 8),
+ * at a dearer drift search (C3 step: 4 is the fastest). */
+#define PG_TUNE_K3_ANCHORS 20
 int pg_tune(pg_ctx* ctx, int what, int64_t value);
 
 /* Device bytes the library's buffers hold in this process now (peak == 0)

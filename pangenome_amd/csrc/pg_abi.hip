@@ -297,6 +297,11 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         x->c.t1.off = !(value & 2);
         x->c.t6.off = !(value & 4);
         break;
+      case PG_TUNE_K3_ANCHORS:
+        if (value != 0 && (value < 3 || value > 6) && value != 8)
+          throw pg::Error(PG_EINVAL, "pg_tune: K3 anchors must be 3, 4, 5, 6 or 8 (0 = the default)");
+        x->c.k3_anchors = (int)value;
+        break;
       case PG_TUNE_K1:
         if (value < 0 || value > 3) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 3]");
         x->c.k1_form = (int)value;

@@ -368,8 +368,10 @@ __device__ __forceinline__ void cover_search(uint8_t (*s_cls)[SPAN + 16], uint8_
 #pragma unroll
   for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
-    if ((((ri ? dm1 : dm0) >> m) & 1u) && (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) == ~0u)
-      need |= 1u << p;
+    unsigned all = ~0u;
+#pragma unroll
+    for (int ai = 0; ai < NANCH; ++ai) all &= best[m][ri][ai];
+    if ((((ri ? dm1 : dm0) >> m) & 1u) && all == ~0u) need |= 1u << p;
   }
   if (!need) return;                                          // (block-uniform)
   __syncthreads();
@@ -816,8 +818,10 @@ __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4
 #pragma unroll
   for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
-    if ((((ri ? dm1 : dm0) >> m) & 1u) && (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) == ~0u)
-      need |= 1u << p;
+    unsigned all = ~0u;
+#pragma unroll
+    for (int ai = 0; ai < NANCH; ++ai) all &= best[m][ri][ai];
+    if ((((ri ? dm1 : dm0) >> m) & 1u) && all == ~0u) need |= 1u << p;
   }
   if (!need) return;                                          // (block-uniform)
   __syncthreads();
@@ -1070,42 +1074,26 @@ constexpr int RSTAGEW = (RSPAN + 15) / 16 + 2;    // staged words per reference 
 constexpr int RDW = (RPADW + RSTAGEW + 16 + 3) / 4 * 4;   // + tail: a lane's 12-word read stays inside
 constexpr int LW = 7;                             // packed words per lane: 64 windows + k+1 bases, any alignment
 static_assert(IW * 4 == 64 && CBLOCK == 64 * QM, "a lane owns 4 segments; a wave owns a member");
+// Anchors per (member, reference) in the packed pass, astep_p bases apart.  A
+// window is covered under any drift its tile's anchors found, so a run of
+// windows between two drift changes (the member's own indels, shared by both
+// references) that no anchor falls in is lost to the work pass: with 3
+// anchors per 4096-window tile that cost C3 ~25 % more stage A records than
+// the ideal coverage of the two references (tools/cover_loss.py).
+#ifndef PG_HWIN2P
+#define PG_HWIN2P 56
+#endif
+constexpr int HWIN2P = PG_HWIN2P;                 // the first search: the XCD's hint +- HWIN2P
+constexpr int NAP_DEFAULT = 4;                    // pg_tune PG_TUNE_K3_ANCHORS: 3, 4, 5, 6 or 8
+template <int NAP>
+constexpr int astep_p() { return (TILE - ALEN - 16) / (NAP - 1); }
 
+template <int NAP>
 struct Drifts2 {
   int n;
-  int U[NANCH], lo[NANCH], hi[NANCH];             // U: s_ref base index of the member's word-grid base
-  int d[NANCH];                                   // the drift (q - p) itself
+  int U[NAP], lo[NAP], hi[NAP];                   // U: s_ref base index of the member's word-grid base
+  int d[NAP];                                     // the drift (q - p) itself
 };
-// the drift set of one (member, reference): drifts_of's rule, with U = the
-// s_ref base index that member base 16 D (record position pos16) maps to
-__device__ __forceinline__ Drifts2 drifts_p(const unsigned* s_best, long long qt, long long pos16, long long rbase,
-                                            long long rfn, long long plo, long long phi, int k) {
-  Drifts2 D;
-  D.n = 0;
-#pragma unroll
-  for (int j = 0; j < NANCH; ++j) D.U[j] = D.lo[j] = D.hi[j] = D.d[j] = 0;
-  const long long pl = plo + 1 > 1 ? plo + 1 : 1;
-  const long long ph = rfn - k - IW < phi - IW - k ? rfn - k - IW : phi - IW - k;
-#pragma unroll
-  for (int ai = 0; ai < NANCH; ++ai) {
-    const unsigned b = s_best[ai];
-    if (b == ~0u) continue;
-    const int d = (int)(b & 0xFFFFu) - DRIFT;
-    const int u = (int)(rbase + pos16 - d);
-    bool dup = false;
-#pragma unroll
-    for (int j = 0; j < ai; ++j) dup |= j < D.n && D.U[j] == u;
-    if (dup) continue;
-    const long long lo = pl + d - qt, hi = ph + d - qt;
-    const int l32 = (int)(lo < -(1ll << 30) ? -(1ll << 30) : lo), h32 = (int)(hi > (1ll << 30) ? (1ll << 30) : hi);
-#pragma unroll
-    for (int j = 0; j <= ai; ++j)
-      if (j == D.n) { D.lo[j] = l32; D.hi[j] = h32; D.U[j] = u; D.d[j] = d; }
-    ++D.n;
-  }
-  return D;
-}
-
 __device__ __forceinline__ uint32_t p2_word(const uint32_t* p2, long long i, uint64_t n_p2) {
   return (i >= 0 && (uint64_t)i < n_p2) ? p2[i] : 0u;
 }
@@ -1141,21 +1129,21 @@ __device__ __forceinline__ void cover_barrier() {
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
-__device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2], const uint32_t (*s_ref)[RDW],
-                                               const TriGeo* tri, unsigned (*best)[2][NANCH], uint32_t dm0,
+template <int NAP>
+__device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NAP][2], const uint32_t (*s_ref)[RDW],
+                                               const TriGeo* tri, unsigned (*best)[2][NAP], uint32_t dm0,
                                                uint32_t dm1) {
-  constexpr int NT = QM * 2 * NANCH;
-  static_assert(NT * 8 <= CBLOCK && 2 * HWIN2 + 1 + 15 <= 8 * 16, "one round of 8 lanes per triple");
+  constexpr int NT = QM * 2 * NAP;
+  constexpr int SLN = (2 * HWIN2P + 16 + 15) / 16;              // lanes per triple: 16 candidates each
   const int t = (int)threadIdx.x;
-  {
-    const int tr = t >> 3, sub = t & 7;
-    if (tr < NT) {
-      const int m = tr / (2 * NANCH), ri = (tr / NANCH) & 1, ai = tr % NANCH;
-      const TriGeo g = tri[tr];
-      const int w = (g.lo1 >> 4) + sub;
-      if (g.lo1 <= g.hi1 && 16 * w <= g.hi1)
-        drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo1, g.hi1, w, &best[m][ri][ai]);
-    }
+#pragma unroll
+  for (int tr = t / SLN; tr < NT; tr += CBLOCK / SLN) {          // (NT * SLN / CBLOCK rounds)
+    const int sub = t % SLN;
+    const int m = tr / (2 * NAP), ri = (tr / NAP) & 1, ai = tr % NAP;
+    const TriGeo g = tri[tr];
+    const int w = (g.lo1 >> 4) + sub;
+    if (g.lo1 <= g.hi1 && 16 * w <= g.hi1)
+      drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo1, g.hi1, w, &best[m][ri][ai]);
   }
   cover_barrier();
   // pairs whose three anchors all missed: decided by every wave from the
@@ -1166,8 +1154,10 @@ __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2]
 #pragma unroll
   for (int p = 0; p < 2 * QM; ++p) {
     const int m = p >> 1, ri = p & 1;
-    if ((((ri ? dm1 : dm0) >> m) & 1u) && (best[m][ri][0] & best[m][ri][1] & best[m][ri][2]) == ~0u)
-      need |= 1u << p;
+    unsigned all = ~0u;
+#pragma unroll
+    for (int ai = 0; ai < NAP; ++ai) all &= best[m][ri][ai];
+    if ((((ri ? dm1 : dm0) >> m) & 1u) && all == ~0u) need |= 1u << p;
   }
   if (!need) return;                                          // (block-uniform)
   cover_barrier();
@@ -1176,8 +1166,8 @@ __device__ __forceinline__ void cover_search_p(const uint32_t (*s_anc)[NANCH][2]
     const int m = p >> 1, ri = p & 1;
     if (!((need >> p) & 1u)) continue;
 #pragma unroll 1
-    for (int ai = 0; ai < NANCH; ++ai) {
-      const TriGeo g = tri[(m * 2 + ri) * NANCH + ai];
+    for (int ai = 0; ai < NAP; ++ai) {
+      const TriGeo g = tri[(m * 2 + ri) * NAP + ai];
       for (int w = (g.lo >> 4) + t; 16 * w <= g.hi; w += CBLOCK)
         drift_task_p(s_anc[m][ai][0], s_anc[m][ai][1], s_ref[ri], g.ibhi, g.lo, g.hi, w, &best[m][ri][ai]);
     }
@@ -1216,18 +1206,21 @@ __device__ __forceinline__ uint32_t even_bits(uint32_t x) {
   return (x | (x >> 8)) & 0x0000FFFFu;
 }
 
+template <int NAP>
 __global__ void __launch_bounds__(CBLOCK, 8)
 k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint64_t n_p2,
           const uint8_t* __restrict__ cls_dbg, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue, unsigned long long* __restrict__ qcount,
           unsigned long long qcap, int k, int ref, long long rfs, long long rfn, int ref2, long long r2s,
           long long r2n, int* __restrict__ hints, int nrec, uint64_t ngroups, uint32_t b0, uint32_t b1, uint32_t bt) {
+  static_assert(NAP >= 2 && QM * NAP + QM * 2 * NAP <= CBLOCK, "anchor loads and triple geometry: one thread each");
+  constexpr int ASTEPP = astep_p<NAP>();
   __shared__ __attribute__((aligned(16))) uint32_t s_ref[2][RDW];
-  __shared__ uint32_t s_anc[QM][NANCH][2];
-  __shared__ unsigned s_best[QM][2][NANCH];
+  __shared__ uint32_t s_anc[QM][NAP][2];
+  __shared__ unsigned s_best[QM][2][NAP];
   __shared__ uint32_t s_scan[CBLOCK / 64];
   __shared__ unsigned long long s_qbase;
-  __shared__ Drifts2 s_dr[QM][2];
-  __shared__ TriGeo s_tri[QM * 2 * NANCH];
+  __shared__ Drifts2<NAP> s_dr[QM][2];
+  __shared__ TriGeo s_tri[QM * 2 * NAP];
   __shared__ uint32_t s_rexc;
   uint64_t g, ge;
   xcd_chunk(ngroups, b0, b1, bt, blockIdx.x & 7, g, ge);
@@ -1281,19 +1274,19 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
         eex |= *reinterpret_cast<const uint32_t*>(e16 + a + 4 * i);
   }
   if (t == 0) s_rexc = 0u;
-  if (t < QM * NANCH) {                            // anchors: 32 bases = 2 words each
-    const int m = t / NANCH, ai = t % NANCH;
+  if (t < QM * NAP) {                              // anchors: 32 bases = 2 words each
+    const int m = t / NAP, ai = t % NAP;
     long long rs = mrs[0];
 #pragma unroll
     for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
-    const long long ga = rs + qt + 8 + (long long)ai * ASTEP, x = ga >> 4;
+    const long long ga = rs + qt + 8 + (long long)ai * ASTEPP, x = ga >> 4;
     const uint32_t sb = 2u * (uint32_t)(ga & 15);
     uint32_t P0 = 0, P1 = 0, P2 = 0;
     if ((dm0 >> m) & 1u) { P0 = p2_word(p2, x, n_p2); P1 = p2_word(p2, x + 1, n_p2); P2 = p2_word(p2, x + 2, n_p2); }
     s_anc[m][ai][0] = __builtin_amdgcn_alignbit(P1, P0, sb);
     s_anc[m][ai][1] = __builtin_amdgcn_alignbit(P2, P1, sb);
-  } else if (t >= 192 && t < 192 + QM * 2 * NANCH) {   // triples: search geometry around the XCD's hint
-    const int x = t - 192, m = x / (2 * NANCH), ri = (x / NANCH) & 1, ai = x % NANCH;
+  } else if (t >= CBLOCK - QM * 2 * NAP) {         // triples: search geometry around the XCD's hint
+    const int x = t - (CBLOCK - QM * 2 * NAP), m = x / (2 * NAP), ri = (x / NAP) & 1, ai = x % NAP;
     (&s_best[0][0][0])[x] = ~0u;
     TriGeo G{0, 0, -1, 0, -1};
     if ((((ri ? dm1 : dm0) >> m) & 1u)) {
@@ -1301,12 +1294,12 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
       const int hh = hints[(size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + td.r];
       const int h = hh < 0 ? DRIFT : hh;
       const RefGeo& R = ri ? rg[1] : rg[0];
-      const long long a = qt + 8 + (long long)ai * ASTEP;
+      const long long a = qt + 8 + (long long)ai * ASTEPP;
       G.ibhi = (int)(R.rbase + a + DRIFT);
       G.lo = max(G.ibhi - 2 * DRIFT, (int)(R.rbase + R.plo));
       G.hi = a + ALEN > td.rn ? -1 : min(G.ibhi, (int)(R.rbase + R.phi) - ALEN);
-      G.lo1 = max(G.lo, G.ibhi - (h + HWIN2));
-      G.hi1 = min(G.hi, G.ibhi - (h - HWIN2));
+      G.lo1 = max(G.lo, G.ibhi - (h + HWIN2P));
+      G.hi1 = min(G.hi, G.ibhi - (h - HWIN2P));
     }
     s_tri[x] = G;
   }
@@ -1342,19 +1335,45 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
     if (rexc & 2u) dm1 = 0u;
   }
   if (dm0) cover_search_p(s_anc, s_ref, s_tri, s_best, dm0, dm1);
-  if (t < 2 * QM) {                                // hints and drift sets: one lane per (member, reference)
-    const int m = t >> 1, ri = t & 1;
+  if (t < QM * 2 * NAP) {                          // hints and drift sets: one lane per (member, reference, anchor)
+    const int m = t / (2 * NAP), ri = (t / NAP) & 1, ai = t % NAP;
     if ((((ri ? dm1 : dm0) >> m) & 1u)) {
+      const unsigned* B = s_best[m][ri];
+      const unsigned b = B[ai];
+      // the set holds each distinct drift once, in anchor order: this anchor's
+      // slot is the number of distinct drifts the anchors before it found
+      auto first = [&](int j) {                     // anchor j found a drift no anchor before it found
+        if (B[j] == ~0u) return false;
+        for (int i = 0; i < j; ++i)
+          if ((B[i] & 0xFFFFu) == (B[j] & 0xFFFFu)) return false;
+        return true;
+      };
+      int slot = 0;
+      for (int j = 0; j < ai; ++j) slot += first(j) ? 1 : 0;
+      const bool keep = first(ai);
+      bool last = b != ~0u;                         // the last anchor that found one
+      for (int j = ai + 1; j < NAP; ++j) last &= B[j] == ~0u;
       long long rs = mrs[0];
-      int r = descs[QM * g].r;
 #pragma unroll
       for (int y = 1; y < QM; ++y) rs = m == y ? mrs[y] : rs;
-      r = descs[QM * g + m].r;
+      const int r = descs[QM * g + m].r;
       (void)PG_BOK(r >= 0 && r < nrec, 52, (long long)r, (long long)nrec);
-      publish_hint(s_best[m][ri], hints + (size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + r);
-      const RefGeo R = ri ? rg[1] : rg[0];
-      const long long pos16 = 16 * ((rs + qt - 1) >> 4) - rs;   // record position of the member's word grid
-      s_dr[m][ri] = drifts_p(s_best[m][ri], qt, pos16, R.rbase, R.rfn, R.plo, R.phi, k);
+      // the hint: the drift nearest the record's next stripe
+      if (last) hints[(size_t)(blockIdx.x & 7) * 2 * nrec + (ri ? nrec : 0) + r] = (int)(b & 0xFFFFu);
+      Drifts2<NAP>& D = s_dr[m][ri];
+      if (keep) {
+        const RefGeo R = ri ? rg[1] : rg[0];
+        const long long pos16 = 16 * ((rs + qt - 1) >> 4) - rs;   // record position of the member's word grid
+        const int d = (int)(b & 0xFFFFu) - DRIFT;
+        const long long pl = R.plo + 1 > 1 ? R.plo + 1 : 1;
+        const long long ph = R.rfn - k - IW < R.phi - IW - k ? R.rfn - k - IW : R.phi - IW - k;
+        const long long lo = pl + d - qt, hi = ph + d - qt;
+        D.U[slot] = (int)(R.rbase + pos16 - d);
+        D.lo[slot] = (int)(lo < -(1ll << 30) ? -(1ll << 30) : lo);
+        D.hi[slot] = (int)(hi > (1ll << 30) ? (1ll << 30) : hi);
+        D.d[slot] = d;
+      }
+      if (ai == NAP - 1) D.n = slot + (keep ? 1 : 0);
     }
   }
   cover_barrier();
@@ -1381,9 +1400,8 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
     for (int ri = 0; ri < 2; ++ri) {
       if (ri && !((dm1 >> m) & 1u)) break;
       const int nd = __builtin_amdgcn_readfirstlane(s_dr[m][ri].n);
-#pragma unroll
-      for (int j = 0; j < NANCH; ++j) {
-        if (j >= nd) break;
+#pragma unroll 1
+      for (int j = 0; j < nd; ++j) {
         const int U = __builtin_amdgcn_readfirstlane(s_dr[m][ri].U[j]);
         const int lo = __builtin_amdgcn_readfirstlane(s_dr[m][ri].lo[j]);
         const int hi = __builtin_amdgcn_readfirstlane(s_dr[m][ri].hi[j]);
@@ -1483,6 +1501,18 @@ k_cover_p(const uint32_t* __restrict__ p2, const uint8_t* __restrict__ e16, uint
         queue[sub * qcap + s_qbase + pos] = WorkItem{rs, rn - k, qt + 64 * l + 16 * s, cov[s], 0u};
       ++pos;
     }
+}
+
+// the packed coverage pass with na anchors per (member, reference)
+template <typename... A>
+static void launch_cover_p(int na, dim3 grid, hipStream_t s, A... a) {
+  switch (na) {
+    case 3: hipLaunchKernelGGL(k_cover_p<3>, grid, dim3(CBLOCK), 0, s, a...); break;
+    case 4: hipLaunchKernelGGL(k_cover_p<4>, grid, dim3(CBLOCK), 0, s, a...); break;
+    case 5: hipLaunchKernelGGL(k_cover_p<5>, grid, dim3(CBLOCK), 0, s, a...); break;
+    case 6: hipLaunchKernelGGL(k_cover_p<6>, grid, dim3(CBLOCK), 0, s, a...); break;
+    default: hipLaunchKernelGGL(k_cover_p<8>, grid, dim3(CBLOCK), 0, s, a...); break;
+  }
 }
 
 #ifdef PG_DEBUG_BOUNDS
@@ -2979,10 +3009,10 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
                          (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
                          c.k3_hint.as<int>(), (int)c.n_records, ntiles, cb[i], cb[i + 1], cbt);
     else if (gc[i])
-      hipLaunchKernelGGL(k_cover_p, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, c.p2.as<uint32_t>(),
-                         c.e16.as<uint8_t>(), (uint64_t)(c.p2.cap / 4), cls, td, qi, qni, (unsigned long long)qcapc[i], c.k,
-                         c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
-                         cb[i], cb[i + 1], cbt);
+      launch_cover_p(c.k3_anchors ? c.k3_anchors : NAP_DEFAULT, dim3((unsigned)gc[i]), s0, c.p2.as<uint32_t>(),
+                     c.e16.as<uint8_t>(), (uint64_t)(c.p2.cap / 4), cls, td, qi, qni, (unsigned long long)qcapc[i], c.k,
+                     c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
+                     cb[i], cb[i + 1], cbt);
     PG_HIP(hipGetLastError());
 #ifdef PG_DEBUG_BOUNDS
     for (int j = 0; j < nch; ++j)                 // this chunk's counters in range, the later ones still zero

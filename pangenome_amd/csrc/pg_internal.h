@@ -161,6 +161,7 @@ struct Ctx {
   int k3_tail = 0;                // pg_tune: last K3 chunk in 16ths of the others (0 = 10)
   int k3_head = 0;                // pg_tune: first K3 chunk in 16ths of the others (0 = 16)
   int k3_cover = 0;               // pg_tune: coverage pass (0 = packed form, 1 = LDS-staged members, 2 = quad form)
+  int k3_anchors = 0;             // pg_tune: packed coverage pass anchors per tile and reference (0 = 4)
   int early_split = 1;            // pg_tune: pg_build_host splits each landed chunk's records (stage B under the upload)
   uint64_t h2d_chunk = 64ull << 20;   // pg_tune: bytes per H2D chunk of pg_parse_host
   uint64_t h2d_tail = 0;              // pg_tune: bytes of pg_build_host's last H2D chunk (0: uniform chunks)

@@ -270,6 +270,33 @@ def test_k3_cover_forms_vs_oracle(oracle_mod, k):
 
 
 @pytest.mark.parametrize("k", [15, 27])
+def test_k3_anchor_counts_vs_oracle(oracle_mod, k):
+    """The packed coverage pass at 3, 4, 6 and 8 anchors per tile and reference
+    (PG_TUNE_K3_ANCHORS) gives the oracle's dBG and rdBG; with indels dense
+    enough for several drift changes per tile, more anchors leave fewer stage A
+    records (the runs between two indels that an anchor falls in are covered)."""
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context, PG_TUNE_K3_ANCHORS
+    fasta = synth.pangenome(9, 150_000, snp=1e-3, indel=5e-4, seed=470 + k, width=61)
+    ref = oracle_mod.OracleRun(fasta, k, 2)
+    rk, rm = ref.dbg()
+    recs = {}
+    for na in (3, 4, 6, 8, 0):
+        ctx = Context(k)
+        ctx.tune(PG_TUNE_K3_ANCHORS, na)
+        ctx.set_fasta(fasta)
+        ctx.parse()
+        st = ctx.build(None, 0, True)
+        keys, masks = ctx.dbg()
+        assert np.array_equal(keys, rk) and np.array_equal(masks, rm), na
+        assert np.array_equal(ctx.rdbg(), ref.rdbg()), na
+        recs[na] = st.n_records_a
+        ctx.close()
+    assert recs[8] < recs[6] < recs[4] < recs[3], recs
+    assert abs(recs[0] - recs[4]) <= recs[4] // 100, recs      # 0 = 4 (hints may differ run to run)
+
+
+@pytest.mark.parametrize("k", [15, 27])
 def test_k3_packed_exceptions_vs_oracle(oracle_mod, k):
     """The packed coverage pass around bases that are not ACGT (their 2-bit
     code is not their class): N runs, IUPAC codes in both cases and '$' in
