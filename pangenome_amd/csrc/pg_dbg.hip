@@ -272,6 +272,79 @@ __device__ __forceinline__ void segment_records(const uint8_t* s_cls, long long 
   }
 }
 
+// The work pass's packed form of an interior k = 27 segment whose 64 staged
+// bases are all ACGT (no exception chunk): the bases are read as 2-bit codes
+// (= their classes) from four packed words in registers, shifted so that code
+// 0 is position q0 - 1 - no LDS row, no byte reads.  init_keys27 from the
+// codes: 7 bytes of 4 codes, each looked up in K5 (the base-5 value of its 4
+// digits forward, low 16 bits, and reversed, high 16), combined in 32-bit
+// pieces of 12 digits; the reverse strand's key from the reversed digits R
+// as Kr = sum (3 - d_j) 5^(26-j) = 3 (5^27 - 1) / 4 - R, and R from 5 R
+// (28 digits, the last one 0) by the exact division K / 5 = K * INV5.
+constexpr uint64_t KR27 = 5587935447692871093ull;   // 3 (5^27 - 1) / 4
+__device__ __forceinline__ uint32_t k5_entry(uint32_t b) {
+  uint32_t t = 0, tr = 0;
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t d = digit_fw((b >> (2 * i)) & 3u);
+    t = t * 5u + digit_fw((b >> (2 * (3 - i))) & 3u);
+    tr = tr * 5u + d;
+  }
+  return t | tr << 16;
+}
+__device__ __forceinline__ void init_keys27_pk(const uint32_t (&cw)[4], const uint32_t* k5, uint64_t& K,
+                                               uint64_t& Kr) {
+  const uint32_t v0 = __builtin_amdgcn_alignbit(cw[1], cw[0], 2), v1 = __builtin_amdgcn_alignbit(cw[2], cw[1], 2);
+  uint32_t t[7];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) t[c] = k5[(v0 >> (8 * c)) & 0xFFu];
+  t[4] = k5[v1 & 0xFFu];
+  t[5] = k5[(v1 >> 8) & 0xFFu];
+  t[6] = k5[(v1 >> 16) & 0x3Fu];                  // digits 24 .. 26 (27: 0)
+  auto lo16 = [&](int c) { return t[c] & 0xFFFFu; };
+  auto hi16 = [&](int c) { return t[c] >> 16; };
+  const uint32_t lo = __umul24(__umul24(lo16(2), 625u) + lo16(1), 625u) + lo16(0);
+  const uint32_t mid = __umul24(__umul24(lo16(5), 625u) + lo16(4), 625u) + lo16(3);
+  K = ((uint64_t)lo16(6) * 244140625ull + mid) * 244140625ull + lo;        // 5^12
+  const uint32_t hr = __umul24(__umul24(hi16(0), 625u) + hi16(1), 625u) + hi16(2);
+  const uint32_t mr = __umul24(__umul24(hi16(3), 625u) + hi16(4), 625u) + hi16(5);
+  const uint64_t r5 = (uint64_t)hr * 152587890625ull + (uint64_t)mr * 625ull + hi16(6);   // 5^16, 5^4
+  Kr = KR27 - r5 * INV5;
+}
+// segment_records' interior path with code i = base q0 - 1 + i of the record
+template <bool RC, int X0, int NX>
+__device__ __forceinline__ void segment_records_pk(const uint32_t (&cw)[4], const uint32_t* k5, uint64_t shift,
+                                                   const TableView& T, uint32_t covered, uint64_t& K, uint64_t& Kr,
+                                                   uint64_t (&hh)[NX], uint32_t (&mm)[NX]) {
+  static_assert(X0 + NX + 28 <= 48, "codes of the shifted 128 bits");
+  auto code = [&](int i) -> uint32_t { return (cw[i >> 4] >> (2 * (i & 15))) & 3u; };
+  if (X0 == 0) init_keys27_pk(cw, k5, K, Kr);
+#pragma unroll
+  for (int x = 0; x < NX; ++x) {
+    const int xi = X0 + x;
+    const uint32_t p = code(xi), s = code(xi + 28);
+    if (xi) {                                      // Nu // 5 + alpha * 5^(k-1) (:1072)
+      const uint32_t din = code(xi + 27);
+      K = (K - digit_fw(p)) * INV5 + (uint64_t)digit_fw(din) * shift;
+      Kr = (Kr - (uint64_t)digit_rc(p) * shift) * 5 + digit_rc(din);
+    }
+    const uint32_t mf = (lam_fw(p) << OFFBIT) | lam_fw(s) | PRES_A;
+    uint64_t c;
+    uint32_t m;
+    if (RC) {
+      const uint32_t mr = (lam_rc(s) << OFFBIT) | lam_rc(p) | PRES_A;
+      const bool lt = K < Kr, eq = K == Kr;
+      c = lt ? K : Kr;
+      m = eq ? (mf | mr) : lt ? (mf | (mr << B_SHIFT)) : (mr | (mf << B_SHIFT));
+    } else {
+      const bool le = K <= Kr;
+      c = le ? K : Kr;
+      m = le ? mf : (mf << B_SHIFT);
+    }
+    mm[x] = ((covered >> xi) & 1u) ? 0u : m;
+    hh[x] = T.perm(c);
+  }
+}
+
 // A segment left with work after the coverage pass (k_cover).
 struct WorkItem {
   long long rs, last, q0;
@@ -1646,6 +1719,7 @@ __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[
 // ~2x the waves per CU; the emission stage is then an LDS array of its own,
 // the rows being still in use); NP = 1: all 16 at once, the stage reusing
 // the rows.
+constexpr bool PK_ON = !(PG_EXP_BITS & (1 << 20));   // (experiment build: the byte form for every segment)
 template <bool RC, int NP>
 __global__ void __launch_bounds__(IBLOCK)
 k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
@@ -1665,7 +1739,9 @@ k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
   __shared__ __attribute__((aligned(16))) uint8_t stage2[NP == 2 ? 12 * EST : 16];
   __shared__ unsigned long long s_pre[NQ + 1];
   __shared__ EmitLds<NX / ESUB> s_emit;
+  __shared__ uint32_t s_k5[256];
   static_assert(sizeof(scratch) >= 12 * EST, "the emission stage reuses the segment rows");
+  static_assert(IBLOCK == 256, "one K5 entry per thread");
   uint8_t* const st = NP == 2 ? &stage2[0] : &scratch[0][0];
   if (threadIdx.x < 64) {
     const unsigned long long c = qcount[QSTRIDE * threadIdx.x];
@@ -1679,6 +1755,7 @@ k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
     if (threadIdx.x == 0) s_pre[0] = 0ull;
   }
   s_emit.zero();
+  s_k5[threadIdx.x] = k5_entry(threadIdx.x);
   __syncthreads();
   uint8_t* slot = scratch[threadIdx.x];
   const unsigned long long n = s_pre[NQ];
@@ -1691,6 +1768,8 @@ k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
     uint32_t mm[NX];
     WorkItem w{0, -1, 0, 0u, 0u};
     long long aligned = 0;
+    bool pk = false;                               // the packed form (segment_records_pk)
+    uint32_t cw[4] = {0u, 0u, 0u, 0u};
     if (i < n) {
       int lo = 0;                                  // largest j with s_pre[j] <= i
 #pragma unroll
@@ -1708,17 +1787,30 @@ k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
       uint32_t pw[4], ex[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) { pw[j] = pc.p2[c0 + j]; ex[j] = pc.e16[c0 + j]; }
+      pk = PK_ON && k == 27 && !(ex[0] | ex[1] | ex[2] | ex[3]) && w.q0 > 0 && w.q0 + IW <= w.last;
+      if (pk) {
+        // code 0 = position q0 - 1: the 128 bits shifted right by 2 (from + 1 - aligned) in [0, 32]
+        const uint32_t sh = 2u * (uint32_t)(from + 1 - aligned);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint4 v;
-        if (ex[j]) v = *reinterpret_cast<const uint4*>(pc.cls + aligned + 16 * j);
-        else v = make_uint4(unpack4(pw[j], 0), unpack4(pw[j], 1), unpack4(pw[j], 2), unpack4(pw[j], 3));
-        s32[4 * j] = v.x; s32[4 * j + 1] = v.y; s32[4 * j + 2] = v.z; s32[4 * j + 3] = v.w;
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t nx = j < 3 ? pw[j + 1] : 0u;
+          cw[j] = sh >= 32u ? nx : sh ? __builtin_amdgcn_alignbit(nx, pw[j], sh) : pw[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uint4 v;
+          if (ex[j]) v = *reinterpret_cast<const uint4*>(pc.cls + aligned + 16 * j);
+          else v = make_uint4(unpack4(pw[j], 0), unpack4(pw[j], 1), unpack4(pw[j], 2), unpack4(pw[j], 3));
+          s32[4 * j] = v.x; s32[4 * j + 1] = v.y; s32[4 * j + 2] = v.z; s32[4 * j + 3] = v.w;
+        }
       }
     }
     auto part = [&](auto P) {
       constexpr int X0 = decltype(P)::value * NX;
-      if (i < n) {
+      if (i < n && pk) {
+        segment_records_pk<RC, X0, NX>(cw, s_k5, shift, T, w.covered, K, Kr, hh, mm);
+      } else if (i < n) {
         segment_records<RC, X0, NX>(slot, w.rs - aligned, w.q0, w.last, k, shift, T, w.covered, K, Kr, hh, mm);
       } else {
 #pragma unroll
