@@ -1640,15 +1640,15 @@ struct EmitLds {
       for (int q = 0; q < NS; ++q) cnt[q][threadIdx.x] = 0u;
   }
 };
-template <int NR>
+template <int NR, int SUB = ESUB>
 __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[NR], const uint32_t (&m)[NR],
-                                           EmitLds<NR / ESUB>& L, unsigned long long* st_key, uint32_t* st_mw) {
-  constexpr int NS = NR / ESUB;
-  static_assert(NR % ESUB == 0 && NBIN == 64, "whole sub-rounds; one wave scans the bins");
+                                           EmitLds<NR / SUB>& L, unsigned long long* st_key, uint32_t* st_mw) {
+  constexpr int NS = NR / SUB;
+  static_assert(NR % SUB == 0 && NBIN == 64, "whole sub-rounds; one wave scans the bins");
   const int t = (int)threadIdx.x;
   uint32_t rk[NR];
 #pragma unroll
-  for (int j = 0; j < NR; ++j) rk[j] = m[j] ? atomicAdd(&L.cnt[j / ESUB][(uint32_t)(h[j] >> O.shift)], 1u) : 0u;
+  for (int j = 0; j < NR; ++j) rk[j] = m[j] ? atomicAdd(&L.cnt[j / SUB][(uint32_t)(h[j] >> O.shift)], 1u) : 0u;
   __syncthreads();
   const uint32_t x = blockIdx.x & 7;
   if (t < NBIN) {
@@ -1678,7 +1678,7 @@ __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[
 #pragma unroll
   for (int q = 0; q < NS; ++q) {
 #pragma unroll
-    for (int j = q * ESUB; j < (q + 1) * ESUB; ++j)
+    for (int j = q * SUB; j < (q + 1) * SUB; ++j)
       if (m[j]) {
         const uint32_t at = L.off[q][(uint32_t)(h[j] >> O.shift)] + rk[j];
         st_key[at] = h[j];
@@ -1719,6 +1719,13 @@ __device__ __forceinline__ void block_emit(const BinOut& O, const uint64_t (&h)[
 // ~2x the waves per CU; the emission stage is then an LDS array of its own,
 // the rows being still in use); NP = 1: all 16 at once, the stage reusing
 // the rows.
+#ifndef PG_WSUB
+#define PG_WSUB 4
+#endif
+// the work pass's emission sub-round (records per thread): 8 (one 24 KiB
+// stage per half segment, 3 blocks per CU) measured slower than 4 (stage A
+// 0.432 vs 0.413 ms)
+constexpr int WSUB = PG_WSUB;
 constexpr bool PK_ON = !(PG_EXP_BITS & (1 << 20));   // (experiment build: the byte form for every segment)
 template <bool RC, int NP>
 __global__ void __launch_bounds__(IBLOCK)
@@ -1736,11 +1743,11 @@ k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
   constexpr int SROW = 68;
   static_assert(SROW % 8 == 4 && SROW >= 64, "odd dword stride, 64 staged bytes");
   __shared__ __attribute__((aligned(16))) uint8_t scratch[IBLOCK][SROW];
-  __shared__ __attribute__((aligned(16))) uint8_t stage2[NP == 2 ? 12 * EST : 16];
+  __shared__ __attribute__((aligned(16))) uint8_t stage2[NP == 2 ? 12 * IBLOCK * WSUB : 16];
   __shared__ unsigned long long s_pre[NQ + 1];
-  __shared__ EmitLds<NX / ESUB> s_emit;
+  __shared__ EmitLds<NX / WSUB> s_emit;
   __shared__ uint32_t s_k5[256];
-  static_assert(sizeof(scratch) >= 12 * EST, "the emission stage reuses the segment rows");
+  static_assert(NP == 2 || sizeof(scratch) >= 12 * IBLOCK * WSUB, "the emission stage reuses the segment rows");
   static_assert(IBLOCK == 256, "one K5 entry per thread");
   uint8_t* const st = NP == 2 ? &stage2[0] : &scratch[0][0];
   if (threadIdx.x < 64) {
@@ -1822,8 +1829,8 @@ k_emit_work(PackedCls pc, const WorkItem* __restrict__ queue,
         for (int x = 0; x < NX; ++x) acc ^= hh[x] + mm[x];
         if (acc == 42ull) O.flags[3] = 1u;
       } else {
-        block_emit<NX>(O, hh, mm, s_emit, reinterpret_cast<unsigned long long*>(st),
-                       reinterpret_cast<uint32_t*>(st + 8 * EST));
+        block_emit<NX, WSUB>(O, hh, mm, s_emit, reinterpret_cast<unsigned long long*>(st),
+                             reinterpret_cast<uint32_t*>(st + 8 * IBLOCK * WSUB));
       }
     };
     part(std::integral_constant<int, 0>{});
@@ -2047,14 +2054,24 @@ __device__ __forceinline__ uint64_t part_at(const Recs& I, uint32_t p, const uns
 // partitions p * nb + b.  A block takes SCH consecutive records of one region
 // (bpr blocks per region), ranks them per bin in LDS, reserves each bin's run
 // with one global atomic, sorts them by bin in LDS and writes the runs
-// coalesced.  3 blocks (24 waves) per CU.
-constexpr int SB = 512, SR = 8, SCH = SB * SR;
+// coalesced.  2 blocks (16 waves) per CU: 6144 records per round (72 KiB of
+// LDS) write longer runs per bin than 4096 at 3 blocks per CU (C3 split 0.151-
+// 0.153 vs 0.161-0.162 ms; 2048 or 8192 per round: 0.173-0.196 ms), and at
+// 4 waves per SIMD (the occupancy the LDS allows) the 12 records per thread
+// stay in registers: 0.138-0.139 ms (profiles/r05_ab_split_geometry.log).
+#ifndef PG_SPLIT_SR
+#define PG_SPLIT_SR 12
+#endif
+#ifndef PG_SPLIT_SB
+#define PG_SPLIT_SB 512
+#endif
+constexpr int SB = PG_SPLIT_SB, SR = PG_SPLIT_SR, SCH = SB * SR;
 constexpr int SPLIT_BITS = 7;                 // bits per split pass
 constexpr int SMAXB = 1 << SPLIT_BITS;
 // start (NULL: 0): per input region, the records below it are already split
 // (pg_build_host's early split); a block loops over its region's records in
 // steps of bpr * SCH.
-__global__ void __launch_bounds__(SB, 6)
+__global__ void __launch_bounds__(SB, 4)
 k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t shift, uint32_t nb, uint32_t bpr,
         unsigned* __restrict__ flags) {
   __shared__ uint32_t s_cnt[SMAXB], s_pos[SMAXB];
