@@ -586,10 +586,14 @@ __global__ void __launch_bounds__(PBLOCK) k_emit(const uint8_t* __restrict__ buf
                       !__ballot(fl.gt || !fl.acgt || (fl.nlm & (fl.nlm - 1u)) != 0u);
     if (fast) {
       carry = (uint32_t)(__ballot((fl.nlm >> 15) & 1u) >> 63) & 1u;
-      const uint32_t mine = 16u - (uint32_t)__builtin_popcount(fl.nlm);
-      const uint32_t incl = wave_incl_sum(mine);
-      const uint32_t excl = incl - mine;
-      ctot = __builtin_amdgcn_readlane(incl, 63);
+      // a lane holds 16 or 15 bases (at most one '\n'): its offset is 16 per
+      // lane below it less the lanes below holding a '\n' (one ballot and a
+      // mask count instead of a dependent chain of DPP adds)
+      const uint64_t nlb = __ballot(fl.nlm != 0u);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(nlb >> 32),
+                                                        __builtin_amdgcn_mbcnt_lo((uint32_t)nlb, 0u));
+      const uint32_t excl = 16u * (uint32_t)lane - below;
+      ctot = 16u * 64u - (uint32_t)__builtin_popcountll(nlb);
       // drop the '\n' at byte j (j = 16: none): bytes past it move down by one
       const uint32_t j = fl.nlm ? (uint32_t)__builtin_ctz(fl.nlm) : 16u;
       uint32_t y[4];
