@@ -60,7 +60,9 @@ typedef struct pg_stats {
                               the table's partitions chunk by chunk under the upload
                               (PG_TUNE_EARLY_SPLIT) and stage C read them; bits
                               8..15: stages B/C re-runs of the last build (a plan
-                              or a capacity that did not hold)                     */
+                              or a capacity that did not hold); bits 16..23: the
+                              k_split passes of stage B (0 when split under the
+                              upload)                                             */
   uint64_t n_work_items;   /* K3 stage A work-pass items: 16-window segments the
                               coverage pass left, 64 class bytes read each        */
 } pg_stats;
@@ -71,6 +73,15 @@ int pg_create(pg_ctx** out, int device, int k);
 void pg_destroy(pg_ctx* ctx);
 const char* pg_last_error(void);
 int pg_get_k(const pg_ctx* ctx);
+/* Order this context after a caller's stream: every stream of the context
+ * waits (on the device, hipStreamWaitEvent; the host does not block) for
+ * the work queued on `stream` (a hipStream_t; NULL = the null stream) when
+ * the call is made.  For callers whose allocator hands out memory that
+ * work still queued on their stream may touch (a torch caching-allocator
+ * block freed behind a queued copy or collective) before they pass it to
+ * an entry point that writes or reads it.  Every entry point returns with
+ * its own device work complete, so the other direction needs nothing. */
+int pg_stream_wait(pg_ctx* ctx, void* stream);
 
 /* ---- input: the mmapped FASTA the reference reads with seq2bytes
  *      (kmer_numba.py:117-119).  Host bytes are copied to HBM; device bytes
@@ -211,6 +222,12 @@ int pg_route_finish(pg_ctx* ctx, uint64_t* n_rdbg, pg_stats* stats);
  * pg_dbg_export / pg_rdbg_export return plain keys. */
 int pg_route_merge(pg_ctx* ctx, const void* d_rows, uint64_t n, int nparts, int sentinel, uint64_t* n_rdbg,
                    pg_stats* stats);
+/* pg_route_merge over nseg segments of rows (segment s: n[s] rows at the
+ * device pointer d_segs[s]) as one owner table: a sub-log received as one
+ * run per round and source, merged without concatenating it first.
+ * pg_dbg_merge_check reports the rows of every segment together. */
+int pg_route_merge_segs(pg_ctx* ctx, const void* const* d_segs, const uint64_t* n, int nseg, int nparts, int sentinel,
+                        uint64_t* n_rdbg, pg_stats* stats);
 
 /* ---- edge pass: rdbg_edge_weight_jit_ (kmer_numba.py:1808-1827) ->
  *      rdbg_edge_weight (:1446-1518).  rec_flags as above (walked records);

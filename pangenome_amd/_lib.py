@@ -61,6 +61,7 @@ SIGNATURES = {
     "pg_destroy": (None, [_P]),
     "pg_last_error": (C.c_char_p, []),
     "pg_get_k": (C.c_int, [_P]),
+    "pg_stream_wait": (C.c_int, [_P, _P]),
     "pg_set_fasta": (C.c_int, [_P, _P, C.c_uint64]),
     "pg_set_fasta_device": (C.c_int, [_P, _P, C.c_uint64]),
     "pg_parse": (C.c_int, [_P, _U64P, _U64P]),
@@ -82,6 +83,7 @@ SIGNATURES = {
     "pg_route_scatter": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
     "pg_route_finish": (C.c_int, [_P, _U64P, _SP]),
     "pg_route_merge": (C.c_int, [_P, _P, C.c_uint64, C.c_int, C.c_int, _U64P, _SP]),
+    "pg_route_merge_segs": (C.c_int, [_P, C.POINTER(C.c_void_p), _P, C.c_int, C.c_int, C.c_int, _U64P, _SP]),
     "pg_edges": (C.c_int, [_P, _P, C.c_int, _U64P]),
     "pg_edges_export": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
     "pg_set_labels": (C.c_int, [_P, _P, _P, _P, C.c_uint64]),
@@ -270,6 +272,13 @@ class Context:
         self.n_records, self.n_bases = st.n_records, st.n_bases
         return st
 
+    def stream_wait(self, stream_handle: int):
+        """This context's streams wait (on the device) for the work queued so
+        far on the HIP stream `stream_handle` (e.g. torch's current stream's
+        .cuda_stream): pg_stream_wait."""
+        check(self.lib.pg_stream_wait(self.h, C.c_void_p(stream_handle) if stream_handle else None),
+              "pg_stream_wait")
+
     def tune(self, what: int, value: int):
         check(self.lib.pg_tune(self.h, int(what), int(value)), "pg_tune")
 
@@ -391,6 +400,18 @@ class Context:
         nr = C.c_uint64()
         check(self.lib.pg_route_merge(self.h, C.c_void_p(d_rows) if n else None, int(n), int(nparts),
                                       int(bool(sentinel)), C.byref(nr), C.byref(st)), "pg_route_merge")
+        return st
+
+    def route_merge_segs(self, segs, nparts: int, sentinel: bool = False) -> PgStats:
+        """route_merge over several runs of rows [(device pointer, rows), ...]
+        merged as one owner table (pg_route_merge_segs)."""
+        st = PgStats()
+        nr = C.c_uint64()
+        m = len(segs)
+        ptrs = (C.c_void_p * max(m, 1))(*[C.c_void_p(p) if n else None for p, n in segs])
+        ns = np.ascontiguousarray([int(n) for _, n in segs] or [0], dtype=np.uint64)
+        check(self.lib.pg_route_merge_segs(self.h, ptrs, ptr(ns), m, int(nparts), int(bool(sentinel)), C.byref(nr),
+                                           C.byref(st)), "pg_route_merge_segs")
         return st
 
     # -------------------------------------------------------------- walks

@@ -47,7 +47,8 @@ static void fill_stats(const pg::Ctx& c, pg_stats* s) {
   s->ms_split = c.ms_split;
   s->ms_range = c.ms_range;
   s->sentinel = c.sentinel;
-  s->build_flags = (c.early_split_used ? 1u : 0u) | ((uint64_t)std::min(255, std::max(0, c.bc_attempts - 1)) << 8);
+  s->build_flags = (c.early_split_used ? 1u : 0u) | ((uint64_t)std::min(255, std::max(0, c.bc_attempts - 1)) << 8) |
+                   ((uint64_t)std::min(255, std::max(0, c.split_passes)) << 16);
   s->n_work_items = c.work_items;
 }
 
@@ -76,6 +77,7 @@ int pg_create(pg_ctx** out, int device, int k) {
     for (auto& e : x->c.ev) PG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (auto& e : x->c.cev) PG_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     PG_HIP(hipEventCreateWithFlags(&x->c.rec_ev, hipEventDisableTiming));
+    PG_HIP(hipEventCreateWithFlags(&x->c.ext_ev, hipEventDisableTiming));
     PG_HIP(hipDeviceGetAttribute(&x->c.n_cu, hipDeviceAttributeMultiprocessorCount, device));
     *out = x;
   });
@@ -110,6 +112,7 @@ void pg_destroy(pg_ctx* x) {
   for (auto e : c.cev)
     if (e) (void)hipEventDestroy(e);
   if (c.rec_ev) (void)hipEventDestroy(c.rec_ev);
+  if (c.ext_ev) (void)hipEventDestroy(c.ext_ev);
   if (c.stream_hi) (void)hipStreamDestroy(c.stream_hi);
   (void)hipStreamDestroy(c.stream3);
   (void)hipStreamDestroy(c.stream2);
@@ -118,6 +121,17 @@ void pg_destroy(pg_ctx* x) {
 }
 
 int pg_get_k(const pg_ctx* x) { return x ? x->c.k : -1; }
+
+int pg_stream_wait(pg_ctx* x, void* stream) {
+  return guard([&] {
+    if (!x) throw pg::Error(PG_EINVAL, "pg_stream_wait: ctx is NULL");
+    pg::Ctx& c = x->c;
+    PG_HIP(hipSetDevice(c.device));
+    PG_HIP(hipEventRecord(c.ext_ev, reinterpret_cast<hipStream_t>(stream)));
+    for (hipStream_t s : {c.stream, c.stream2, c.stream3, c.stream_hi})
+      if (s) PG_HIP(hipStreamWaitEvent(s, c.ext_ev, 0));
+  });
+}
 
 int pg_set_fasta(pg_ctx* x, const uint8_t* host, uint64_t n) {
   return guard([&] {
@@ -252,7 +266,9 @@ int pg_build_device(pg_ctx* x, const uint8_t* dev, uint64_t n, int rc0, uint64_t
     pg::parse_fasta(c);
     pg::build_dbg(c, nullptr, 0, rc0 != 0);
     pg::build_rdbg(c);
-    c.ms_parse = c.t0.ms();                    // K1 on the stream (HIP events; the emission overlaps the host)
+    // K1 on the stream (HIP events; the emission overlaps the host); an empty
+    // input returns from parse_fasta before its events are recorded
+    c.ms_parse = n ? c.t0.ms() : 0.0;
     if (n_rdbg) *n_rdbg = c.n_rdbg;
     fill_stats(c, stats);
   });
@@ -530,6 +546,22 @@ int pg_route_merge(pg_ctx* x, const void* d_rows, uint64_t n, int nparts, int se
     if (lg > x->c.cbits && x->c.cbits) throw pg::Error(PG_EINVAL, "pg_route_merge: more owners than coarse bins");
     x->c.merge_sum = x->c.merge_rows = 0;
     pg::merge_dbg(x->c, d_rows, n, 0, sentinel, lg);
+    if (n_rdbg) *n_rdbg = x->c.n_rdbg;
+    fill_stats(x->c, stats);
+  });
+}
+
+int pg_route_merge_segs(pg_ctx* x, const void* const* d_segs, const uint64_t* n, int nseg, int nparts, int sentinel,
+                       uint64_t* n_rdbg, pg_stats* stats) {
+  return guard([&] {
+    if (!x || nseg < 0 || (nseg && (!d_segs || !n))) throw pg::Error(PG_EINVAL, "pg_route_merge_segs: bad arguments");
+    for (int s = 0; s < nseg; ++s)
+      if (n[s] && !d_segs[s]) throw pg::Error(PG_EINVAL, "pg_route_merge_segs: a non-empty segment has no rows");
+    const int lg = route_lg(nparts, "pg_route_merge_segs");
+    PG_HIP(hipSetDevice(x->c.device));
+    if (lg > x->c.cbits && x->c.cbits) throw pg::Error(PG_EINVAL, "pg_route_merge_segs: more owners than coarse bins");
+    x->c.merge_sum = x->c.merge_rows = 0;
+    pg::merge_dbg_segs(x->c, d_segs, n, nseg, sentinel, lg);
     if (n_rdbg) *n_rdbg = x->c.n_rdbg;
     fill_stats(x->c, stats);
   });

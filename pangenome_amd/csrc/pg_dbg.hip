@@ -2921,6 +2921,7 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
       PG_HIP(hipGetLastError());
       in = out;
     }
+    c.split_passes = use_pre ? 0 : (int)lv.size();
     unsigned long long* k5 = c.k5_ctr.as<unsigned long long>();
     const RdbgOut ro{c.rseg.as<unsigned long long>(), k5, rcap};
     c.t6.start(c.stream);
@@ -3242,6 +3243,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
     c.route_reg.assign(NREG, 0);
     for (int r = 0; r < NREG; ++r) c.route_reg[r] = std::min<uint64_t>(h[CSTRIDE * r], c.capA);
     c.route_total = a.total;
+    if (c.windows_fw) c.u_ratio = (double)a.total / (double)c.windows_fw;   // (the next held stage A's regions)
     c.route_maxreg = a.maxreg;
     c.route_maxbin = a.maxbin;
     c.route_sentinel = a.sentinel;
@@ -3522,9 +3524,18 @@ void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nse
 // rot >= 0 (pg_route_merge): the rows are routed stage A records {h, mask
 // word} of this owner, re-binned on h rotated left by rot bits.
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, int sentinel, int rot) {
+  merge_dbg_segs(c, &d_pairs, &n, 1, sentinel, rot);
+}
+
+// The same merge over nseg segments of rows (segment s: ns[s] rows at
+// segs[s]), emitted into one stage A: a routed owner's sub-log as the runs it
+// received round by round, with no device-side concatenation.
+void merge_dbg_segs(Ctx& c, const void* const* segs, const uint64_t* ns, int nseg, int sentinel, int rot) {
   init_hash(c, rot > 0 ? (uint32_t)rot : 0u);
   c.route_ready = false;
   c.early_split_used = false;
+  uint64_t n = 0;
+  for (int s = 0; s < nseg; ++s) n += ns[s];
   uint64_t cap = region_cap(n + 64);
   ACount a;
   // every record count is known here (n): stages B/C go right behind stage A
@@ -3538,9 +3549,10 @@ void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, i
     PG_HIP(hipEventRecord(c.ev[0], c.stream));           // the side stream (stage B/C fills) after all of this
     PG_HIP(hipStreamWaitEvent(c.stream2, c.ev[0], 0));
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
-    if (n) {
-      hipLaunchKernelGGL(rot >= 0 ? k_route_emit : k_slots_emit, dim3(grid_for(n, 4 * IBLOCK, 4096)), dim3(IBLOCK), 0,
-                         c.stream, reinterpret_cast<const Slot*>(d_pairs), n, c.tv, O,
+    for (int s = 0; s < nseg; ++s) {
+      if (!ns[s]) continue;
+      hipLaunchKernelGGL(rot >= 0 ? k_route_emit : k_slots_emit, dim3(grid_for(ns[s], 4 * IBLOCK, 4096)), dim3(IBLOCK),
+                         0, c.stream, reinterpret_cast<const Slot*>(segs[s]), ns[s], c.tv, O,
                          c.flags.as<unsigned long long>() + N_FLAGS / 2);
       PG_HIP(hipGetLastError());
     }

@@ -151,6 +151,7 @@ struct Ctx {
   hipStream_t stream3 = nullptr;  // copy stream: chunked host uploads (pg_parse_host, pg_build_host)
   hipStream_t stream_hi = nullptr; // high priority: K1's header pass and record table beside the emission
   hipEvent_t ev[16] = {};         // ordering events between the two streams
+  hipEvent_t ext_ev = nullptr;    // pg_stream_wait: the caller's stream's queued work, waited on by ours
   hipEvent_t rec_ev = nullptr;    // the record table's copy to the host (K1)
   hipEvent_t cev[16] = {};        // chunk-landed events of the copy stream
   int n_cu = 256;                 // compute units (persistent-kernel grids)
@@ -234,6 +235,7 @@ struct Ctx {
   double w_ratio = 0;                 // last host build: forward windows per input byte
   bool early_split_used = false;      // the last pg_build_host's stage C read the early split's partitions
   int bc_attempts = 0;                // stages B/C runs of the last build (1: no re-run)
+  int split_passes = 0;               // stage B k_split passes of the last build (0: split under the upload)
   // the largest partition of each split level that a build had to re-run
   // for (at table bits lv_keep_bb): later builds' plans start from them
   std::vector<uint64_t> lv_keep;
@@ -370,6 +372,7 @@ uint64_t export_dbg(Ctx& c, uint64_t* h_keys, uint16_t* h_masks, uint64_t cap);
 uint64_t export_rdbg(Ctx& c, uint64_t* h_keys, uint64_t cap);
 uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64_t* h_counts);
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t cap_hint, int sentinel, int rot = -1);
+void merge_dbg_segs(Ctx& c, const void* const* segs, const uint64_t* ns, int nseg, int sentinel, int rot);
 // routed exchange: owners of the held stage A records (2^lg owners)
 void route_counts(Ctx& c, int lg, uint64_t* counts);
 void route_scatter(Ctx& c, int lg, void* d_out, uint64_t out_cap, uint64_t* sums);

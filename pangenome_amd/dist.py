@@ -17,9 +17,14 @@ per-base work of every pass runs on each rank's own GPU over its own records:
              (saturating at 255, so summing saturated counts and saturating
              again is exact), rank 0 gathers them and places the union in the
              reference's oakht slot layout (pg_dbg_load + pg_dbg_dump).
-4. rdBG      owner exchange: entries are owner-partitioned by key hash and
-             moved with one all-to-all (RCCL over xGMI); owners OR-merge and
-             apply the rdBG rule to their partition (exchange_and_reduce).
+4. rdBG      owner exchange: the pass's stage A records are held for their
+             owners (the top bits of the table hash) and moved with one
+             all-to-all (RCCL over xGMI); owners build their partition once
+             from them, rdBG rule included (exchange_routed, the same step
+             the N>1 bench times).  After -d / -r, whose staged npz slots no
+             stage A rebuilds, and at a world that is not a power of two,
+             the local table's entries are exchanged instead
+             (exchange_and_reduce).
              The owners' rdBG keys are all-gathered (C3: 1.9 M keys, 15 MB),
              and every rank loads them as its walk membership table (the
              `-D` path, :2093).
@@ -104,16 +109,25 @@ class ExchangeIntegrityError(RuntimeError):
     and the stage where the sums first disagree)."""
 
 
-def _fence(device):
+def _fence(device, table=None):
     """The library runs on its own non-blocking streams, which do not wait on
     torch's: before native code reads or writes memory the torch allocator
-    handed out, everything torch's streams (the current one, RCCL's) queued
-    must be done — a block freed behind queued work (a clone, a collective)
-    is handed out again at once to the next torch.empty on the same stream.
-    (PG_DEBUG_NO_FENCE=1, diagnostics only: round 4's unfenced behaviour.)"""
+    handed out, everything torch's current stream queued (a clone, the wait
+    on an RCCL collective) must be done - a block freed behind queued work is
+    handed out again at once to the next torch.empty on the same stream.
+    With a `table` that can (stream_wait: pg_stream_wait), the library's
+    streams wait on an event of torch's current stream, on the device (the
+    host does not block); otherwise the device is synchronised.  (Every
+    library call returns with its device work done, so torch needs no fence
+    after it.)  PG_DEBUG_NO_FENCE=1, diagnostics only: round 4's unfenced
+    behaviour."""
     if _is_cuda(device) and not _NO_FENCE:
         import torch
-        torch.cuda.synchronize(device)
+        wait = getattr(table, "stream_wait", None)
+        if wait is not None:
+            wait(torch.cuda.current_stream(device).cuda_stream)
+        else:
+            torch.cuda.synchronize(device)
 
 
 def _fmix64(k):
@@ -142,7 +156,7 @@ def _seg_sums(shard, buf, offsets, device) -> list:
     if len(offsets) < 2:
         return []
     if getattr(buf, "is_cuda", False):
-        _fence(device)
+        _fence(device, shard)
         return [int(x) for x in shard.rows_checksum(buf.data_ptr(), np.asarray(offsets, np.uint64))]
     a = buf.numpy() if hasattr(buf, "numpy") else np.asarray(buf)
     return [row_check_sum(a[offsets[i]:offsets[i + 1]]) for i in range(len(offsets) - 1)]
@@ -196,7 +210,7 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     send = _poisoned(torch.empty((max(total, 1), 2), dtype=torch.int64, device=device))
     sums = np.zeros(world * P, np.uint64)
     if total:
-        _fence(device)
+        _fence(device, table)
         table.partition(world * P, send.data_ptr(), total)   # (returns after the scatter)
         sums = np.asarray(table.partition_sums(world * P), np.uint64)
     t1 = perf_counter()
@@ -214,23 +228,35 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     want = H[:, rank, P + 1:2 * P + 1].copy().view(np.uint64)
     rsplit = rh.sum(axis=1).tolist()
     nrecv = int(sum(rsplit))
-    recv = _poisoned(torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm))
     ssplit = counts.sum(axis=1).tolist()
-    if stage:
+    alias = world == 1 and SELF_COPY and not stage
+    # world 1: the rank's only run is its own, and the send buffer already
+    # holds it where the receive would put it (no copy, no second buffer)
+    recv = send if alias else _poisoned(torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm))
+    if alias:
+        pass
+    elif stage:
         dist.all_to_all_single(recv[:nrecv], send.cpu()[:total], output_split_sizes=rsplit,
                                input_split_sizes=ssplit, group=group)
         recv = recv.to(device)
     else:
         _all_to_all_rows(recv, send, rsplit, ssplit, comm, group, big=int(H[:, :, :P].sum(axis=2).max()),
                          self_copy=SELF_COPY)
-    # every received (source, sub-log) run against its sender's sum
+    # every received (source, sub-log) run against its sender's sum (world 1:
+    # nothing moved - the scatter's buffer is the receive - and the owner's
+    # merge checks the same sums over what it reads)
     off = np.concatenate([[0], np.cumsum(rh.reshape(-1))]).astype(np.int64).tolist()
-    got = _seg_sums(table, recv, off, device)
+    got = [int(x) for x in want.reshape(-1)] if alias else _seg_sums(table, recv, off, device)
     bad = [(s, p) for s in range(world) for p in range(P) if got[s * P + p] != int(want[s, p])]
     if defer is not None:
+        # the caller's next all-reduce carries the check; the closure keeps the
+        # send buffer's piece sums, not the buffer (unless it is the receive)
+        pieces = _piece_sums(table, send, counts.sum(axis=1), rh.sum(axis=1), world, device) \
+            if send is not recv else None
+        snd = send if send is recv else None
         defer["bad"] = bad
-        defer["diagnose"] = lambda: _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm,
-                                              group, where)
+        defer["diagnose"] = lambda: _diagnose(table, snd, recv, counts, sums, rh, bad, world, P, rank, device, comm,
+                                              group, where, pieces)
     else:
         flag = torch.tensor([1 if bad else 0], dtype=torch.int64, device=comm)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
@@ -247,29 +273,47 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     return recv[:nrecv], rh, want_l, 16 * (total - int(counts[rank].sum())), bool(H[:, :, P].any())
 
 
-def _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm, group, where):
+def _piece_count(ssplit, rsplit) -> int:
+    return max(1, int(-(-max(int(np.max(ssplit)), int(np.max(rsplit)), 1) // A2A_ROWS)))
+
+
+def _piece_offsets(split, world: int, npc: int):
+    base = np.concatenate([[0], np.cumsum(split)]).astype(np.int64)
+    return [[int(min(base[o] + j * A2A_ROWS, base[o + 1])) for j in range(npc + 1)] for o in range(world)]
+
+
+def _piece_sums(table, send, ssplit, rsplit, world: int, device, npc=None):
+    """(npc, this rank's send buffer summed per owner and A2A_ROWS piece as a
+    (world, npc) uint64 array)."""
+    npc = npc or _piece_count(ssplit, rsplit)
+    so = _piece_offsets(ssplit, world, npc)
+    return npc, np.array([_seg_sums(table, send, so[o], device) for o in range(world)], np.uint64).reshape(world, npc)
+
+
+def _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm, group, where, pieces=None):
     """A received run's sum disagreed somewhere: every rank sums its send and
     receive messages per A2A_ROWS piece, the senders' piece sums go to every
     rank, and every rank raises, the receivers naming the pieces that
-    differ."""
+    differ.  The piece count is the largest over the ranks (one MAX
+    all-reduce before any rank diverges), a rank with fewer pieces padding
+    with empty ones, so every rank reaches the all-gather.  `pieces`: this
+    rank's send piece sums computed before its send buffer was released
+    (then `send` is None)."""
     import torch
     import torch.distributed as dist
     ssplit, rsplit = counts.sum(axis=1), rh.sum(axis=1)
-    npc = max(1, int(-(-max(int(ssplit.max()), int(rsplit.max()), 1) // A2A_ROWS)))
-
-    def piece_offsets(split):
-        base = np.concatenate([[0], np.cumsum(split)]).astype(np.int64)
-        return [[int(min(base[o] + j * A2A_ROWS, base[o + 1])) for j in range(npc + 1)] for o in range(world)]
-    so, ro = piece_offsets(ssplit), piece_offsets(rsplit)
-    mine = np.array([_seg_sums(table, send, so[o], device) for o in range(world)], np.uint64).reshape(world, npc)
+    npc_t = torch.tensor([pieces[0] if pieces else _piece_count(ssplit, rsplit)], dtype=torch.int64, device=comm)
+    dist.all_reduce(npc_t, op=dist.ReduceOp.MAX, group=group)
+    npc = int(npc_t.item())
+    if pieces is not None:
+        mine = np.zeros((world, npc), np.uint64)
+        mine[:, :pieces[0]] = pieces[1]                 # (pieces past a rank's own count are empty: sum 0)
+    else:
+        mine = _piece_sums(table, send, ssplit, rsplit, world, device, npc)[1]
+    ro = _piece_offsets(rsplit, world, npc)
     psum = sums.reshape(world, P)
     with np.errstate(over="ignore"):
         changed = [o for o in range(world) if int(mine[o].sum(dtype=np.uint64)) != int(psum[o].sum(dtype=np.uint64))]
-    npc_t = torch.tensor([npc], dtype=torch.int64, device=comm)
-    dist.all_reduce(npc_t, op=dist.ReduceOp.MAX, group=group)
-    if int(npc_t.item()) != npc:
-        raise ExchangeIntegrityError("%s: received run sums differ (rank %d: %s); piece counts differ across ranks"
-                                     % (where or "exchange", rank, bad))
     t = torch.from_numpy(mine.view(np.int64).reshape(-1)).to(comm)
     allp = [torch.empty_like(t) for _ in range(world)]
     dist.all_gather(allp, t, group=group)
@@ -350,7 +394,7 @@ def _merge_checked(table, buf, n: int, sentinel: bool, want_sum: int, device, wh
     between the all-to-all and the merge.  Returns None, or the mismatch as a
     message for the caller to raise on every rank at its next collective
     (raising here alone would leave the other ranks waiting in it)."""
-    _fence(device)
+    _fence(device, table)
     table.merge(buf.data_ptr() if n else 0, n, sentinel=sentinel)
     if hasattr(table, "merge_check"):
         rows, s = table.merge_check()
@@ -390,7 +434,7 @@ def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=No
     n = int(recv.shape[0])
     fail = None
     if want_sum is None:
-        _fence(device)
+        _fence(device, table)
         table.merge(recv.data_ptr(), n, sentinel=sentinel_global and rank == 0)
     else:
         fail = _merge_checked(table, recv, n, sentinel_global and rank == 0, want_sum, device,
@@ -448,6 +492,10 @@ class _Routed:
     def rows_checksum(self, d_rows, seg_off):
         return self.sh.rows_checksum(d_rows, seg_off)
 
+    @property
+    def stream_wait(self):
+        return getattr(self.sh, "stream_wait", None)
+
     def merge(self, ptr, n, sentinel=False):
         self.sh.route_merge(ptr, n, self.nparts, sentinel)
 
@@ -471,9 +519,15 @@ def exchange_routed(shard, world: int, rank: int, device, flags, extra: int, rc0
     scatter, the own run's device copy and the owner merge as at N > 1, to
     price them).  The same integrity checks
     as exchange_and_reduce (per-run sums from the scatter to the merge, record
-    conservation).  world must be a power of two.  Returns (n_dbg_total,
+    conservation).  A world that is not a power of two builds locally and
+    runs exchange_and_reduce instead (same result).  Returns (n_dbg_total,
     n_rdbg_total, n_rdbg_local, bytes_sent); `tm` accumulates partition /
     all_to_all / merge seconds (partition = the scatter of the held regions)."""
+    if not _pow2(world):
+        # (the routed owner is a top-bit range of h: 2^j owners only) any
+        # other world size runs the local-table exchange on a local build
+        st = shard.build(flags, extra, rc0)                 # (GpuShard: the flag; a Context: its stats)
+        return exchange_and_reduce(shard, world, rank, device, bool(getattr(st, "sentinel", st)), group, tm)
     counts, sentinel = shard.route_stage_a(flags, extra, rc0, world)
     if world == 1 and not force:
         t0 = perf_counter()
@@ -524,10 +578,22 @@ def _free_device_bytes(device) -> int:
     return 1 << 36
 
 
+def _pow2(n: int) -> bool:
+    return n >= 1 and not n & (n - 1)
+
+
 def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_records: int, rc0: bool, extra: int = 0,
-                    staged=None, group=None, on_chunk=None, compact_at=None, subparts=None):
+                    staged=None, group=None, on_chunk=None, compact_at=None, subparts=None, tm=None, routed=None,
+                    lib_stats=None):
     """The streaming exchange of SURVEY §8(e) for shards whose whole local
     table does not fit beside the owner partition (C5: 3.75 Gbp per GPU).
+
+    Two forms.  `routed` (the default whenever no local table is needed:
+    no `on_chunk` count gathering, no `staged` checkpoint slots, no explicit
+    `compact_at`, and a power-of-two world): _stream_routed - every chunk's
+    stage A records go straight to their owners, which build each sub-log
+    once at the end; nothing is built locally.  Otherwise the local-table
+    form below.
 
     Per chunk of records (stream_chunks): the local OR-table of the chunk
     (`shard.build`, K1 already done for the whole shard), its entries to their
@@ -549,14 +615,29 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
     only; `extra` (the n<k empty records) too.  `on_chunk()` runs after each
     chunk's build (the dump gathers its occurrence counts there).  Returns
     (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent, rounds, the owner's
-    rdBG keys)."""
+    rdBG keys - sorted within each sub-log, not across them: the callers
+    sort what they gather).  `lib_stats` (a dict, routed form): filled with the
+    library's HIP-event spans and record counts of every round and sub-log
+    merge.  `tm` (a dict) accumulates the seconds of each phase (build,
+    route = partition + all-to-all + checks, compact, final = the sub-logs'
+    merges, rdBG rules and key exports), the device synchronised at each
+    phase boundary."""
     import torch
     import torch.distributed as dist
     _, comm = _comm_device(device, group)
+    if routed is None:
+        routed = on_chunk is None and staged is None and compact_at is None and _pow2(world)
+    if routed and (on_chunk is not None or staged is not None or not _pow2(world)):
+        raise ValueError("exchange_stream: the routed form needs a power-of-two world and no local table "
+                         "(on_chunk / staged)")
+    lap = _lapper(tm, device)
     nch = torch.tensor([len(chunks)], dtype=torch.int64, device=comm)
     dist.all_reduce(nch, op=dist.ReduceOp.MAX, group=group)
     rounds = max(1, int(nch.item()))
     P = sublog_count(world, rounds, subparts)
+    if routed:
+        return _stream_routed(shard, world, rank, device, chunks, n_records, rc0, extra, group, rounds, P, lap,
+                              lib_stats)
     if compact_at is None:
         compact_at = max(1 << 20, _free_device_bytes(device) // 4 // 16)
     logs = [[] for _ in range(P)]
@@ -576,7 +657,7 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         m = int(shard.partition(1)[0])
         out = _poisoned(torch.empty((max(m, 1), 2), dtype=torch.int64, device=device))
         if m:
-            _fence(device)
+            _fence(device, shard)
             shard.partition(1, out.data_ptr(), m)
         logs[p] = [out[:m]] if m else []
         logn[p] = base[p] = m
@@ -589,11 +670,14 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
             else:
                 shard.stage(np.zeros(0, np.uint64))
         f = chunks[i] if i < len(chunks) else np.zeros(n_records, np.uint8)
+        t0 = lap("start", perf_counter())
         sentinel |= bool(shard.build(f, extra if i == 0 else 0, rc0))
         if on_chunk is not None:
             on_chunk()
+        t0 = lap("build", t0)
         recv, sub, want, s, _ = _route(shard, world, device, group, subparts=P, where="exchange round %d" % i,
                                        fail=fail[0] if fail else None)
+        t0 = lap("route", t0)
         sent += s
         # each source's run arrives as its P sub-log runs; with P > 1 each run
         # is copied out, so that compacting one sub-log frees its memory (a
@@ -608,11 +692,13 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
                     logsum[p] = (logsum[p] + want[src][p]) & M64
                 off += m
         del recv
+        t0 = lap("log", t0)
         total = sum(logn)
         if total >= compact_at:
             for p in sorted(range(P), key=lambda q: -logn[q]):
                 if logn[p] >= 2 * base[p] and len(logs[p]) > 1:
                     compact(p, i)
+        lap("compact", t0)
     # the n<k sentinel key belongs to one owner: rank 0 (sub-log 0)
     flag = torch.tensor([1 if sentinel else 0, 1 if fail else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
@@ -621,6 +707,7 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         _raise_if_any(fail[0] if fail else None, [1], rank)
     n_dbg_loc = n_rdbg_loc = 0
     keys = []
+    t0 = lap("start", perf_counter())
     for p in range(P):
         cat = (torch.cat(logs[p]) if len(logs[p]) > 1 else logs[p][0]) if logs[p] else None
         logs[p] = []
@@ -637,12 +724,115 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         n_dbg_loc += int(st.n_dbg)
         n_rdbg_loc += int(st.n_rdbg)
         keys.append(np.ascontiguousarray(shard.owner_rdbg(), dtype=np.uint64))
+    lap("final", t0)
     sums = torch.tensor([n_dbg_loc, n_rdbg_loc, 1 if fail else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
     n_dbg, n_rdbg, nfail = sums.tolist()
     if nfail:
         _raise_if_any(fail[0] if fail else None, [1], rank)
-    own = np.sort(np.concatenate(keys)) if keys else np.zeros(0, np.uint64)
+    own = np.concatenate(keys) if keys else np.zeros(0, np.uint64)      # (each sub-log's keys sorted)
+    return int(n_dbg), int(n_rdbg), n_rdbg_loc, sent, rounds, own
+
+
+def _lapper(tm, device):
+    """lap(name, t0): with a `tm` dict, synchronise the device and add the
+    seconds since t0 to tm[name]; returns the new t0."""
+    def lap(name, t0):
+        if tm is None:
+            return 0.0
+        if _is_cuda(device):
+            import torch
+            torch.cuda.synchronize(device)
+        t1 = perf_counter()
+        tm[name] = tm.get(name, 0.0) + (t1 - t0)
+        return t1
+    return lap
+
+
+def _stream_routed(shard, world: int, rank: int, device, chunks, n_records: int, rc0: bool, extra: int, group,
+                   rounds: int, P: int, lap, lib_stats=None):
+    """exchange_stream's routed form.  Per round: stage A of the chunk held
+    for its owners (pg_route_stage_a; every rank runs `rounds` rounds, an
+    empty chunk when out of records), the held regions to their owners in
+    world x P parts (the owner = the top log2(world) bits of h, its sub-log
+    the next log2(P): _route over a _Routed view, with the same integrity
+    sums from the scatter to the merge), and the received buffer kept as it
+    arrived - its runs are the sub-logs' segments.  At the end each sub-log
+    is one owner table built from all of its segments at once
+    (pg_route_merge_segs: stages A (re-binning), B and C, no concatenation),
+    its rdBG counted and its keys exported.  Owner memory: 16 B per received
+    record (C5 at N = 8: ~3.75e9 records, 60 GB) plus one sub-log's build."""
+    import torch
+    import torch.distributed as dist
+    _, comm = _comm_device(device, group)
+    nparts = world * P
+    # with `lib` (a dict): the library's own spans of every round and merge
+    # (HIP events; the shard's stats()), for the bench's per-stage roofline
+    lib = {"rounds": [], "merges": []} if lib_stats is not None and hasattr(shard, "stats") else None
+    bufs, segs = [], [[] for _ in range(P)]             # received buffers; per sub-log (device pointer, rows)
+    logn, logsum = [0] * P, [0] * P
+    sentinel, sent = False, 0
+    fail = []
+    for i in range(rounds):
+        f = chunks[i] if i < len(chunks) else np.zeros(n_records, np.uint8)
+        t0 = lap("start", perf_counter())
+        counts, s_flag = shard.route_stage_a(f, extra if i == 0 else 0, rc0, nparts)
+        sentinel |= bool(s_flag)
+        t0 = lap("build", t0)
+        if lib is not None:
+            st = shard.stats()
+            lib["rounds"].append(dict(stage_a_ms=st.ms_insert, records=int(counts.sum()), work_items=st.n_work_items,
+                                      windows=st.n_windows))
+        recv, sub, want, s, _ = _route(_Routed(shard, nparts, counts), world, device, group, subparts=P,
+                                       where="exchange round %d" % i, fail=fail[0] if fail else None)
+        t0 = lap("route", t0)
+        sent += s
+        off = 0
+        base = recv.data_ptr() if hasattr(recv, "data_ptr") else recv.ctypes.data
+        for src in range(sub.shape[0]):
+            for p in range(P):
+                m = int(sub[src, p])
+                if m:
+                    segs[p].append((base + 16 * off, m))
+                    logn[p] += m
+                    logsum[p] = (logsum[p] + want[src][p]) & M64
+                off += m
+        bufs.append(recv)
+        lap("log", t0)
+    # the n<k sentinel key belongs to one owner: rank 0 (sub-log 0)
+    flag = torch.tensor([1 if sentinel else 0, 1 if fail else 0], dtype=torch.int64, device=comm)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    sent_global = bool(flag[0].item())
+    if int(flag[1].item()):
+        _raise_if_any(fail[0] if fail else None, [1], rank)
+    n_dbg_loc = n_rdbg_loc = 0
+    keys = []
+    t0 = lap("start", perf_counter())
+    for p in range(P):
+        _fence(device, shard)
+        shard.route_merge_segs(segs[p], nparts, sentinel=sent_global and rank == 0 and p == 0)
+        rows, sm = shard.merge_check()
+        if rows != logn[p] or (sm & M64) != logsum[p]:
+            fail.append("exchange: rank %d's final merge of sub-log %d read %d records with sum %#x, the log holds %d "
+                        "with sum %#x (stage: merge)" % (rank, p, rows, sm & M64, logn[p], logsum[p]))
+        st = shard.build_rdbg()
+        n_dbg_loc += int(st.n_dbg)
+        n_rdbg_loc += int(st.n_rdbg)
+        if lib is not None:
+            lib["merges"].append(dict(rebin_ms=st.ms_insert, split_ms=st.ms_split, range_ms=st.ms_range,
+                                      records=int(logn[p]), buckets=int(st.table_capacity), n_rdbg=int(st.n_rdbg),
+                                      split_passes=int(st.build_flags) >> 16 & 255))
+        keys.append(np.ascontiguousarray(shard.owner_rdbg(), dtype=np.uint64))
+    del bufs
+    lap("final", t0)
+    sums = torch.tensor([n_dbg_loc, n_rdbg_loc, 1 if fail else 0], dtype=torch.int64, device=comm)
+    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+    n_dbg, n_rdbg, nfail = sums.tolist()
+    if nfail:
+        _raise_if_any(fail[0] if fail else None, [1], rank)
+    own = np.concatenate(keys) if keys else np.zeros(0, np.uint64)      # (each sub-log's keys sorted)
+    if lib is not None:
+        lib_stats.update(lib, subparts=P)
     return int(n_dbg), int(n_rdbg), n_rdbg_loc, sent, rounds, own
 
 
@@ -859,6 +1049,17 @@ class GpuShard:
         self.n_entries = int(st.n_slots)
         return st
 
+    def stats(self):
+        return self.ctx.stats()
+
+    def stream_wait(self, stream_handle):
+        self.ctx.stream_wait(stream_handle)
+
+    def route_merge_segs(self, segs, nparts, sentinel=False):
+        st = self.ctx.route_merge_segs(segs, nparts, sentinel)
+        self.n_entries = int(st.n_slots)
+        return st
+
     def build_rdbg(self):
         return self.ctx.build_rdbg()
 
@@ -967,6 +1168,11 @@ class DistRun:
                                             self.compact_at)
             return
         self.sentinel = self.sh.build(self.S.local(flags, self.rank), extra if self.rank == 0 else 0, rc0)
+        # the rdBG's exchange re-runs this pass's stage A held for its owners
+        # (exchange_routed) - unless rank 0 staged -r checkpoint slots, which
+        # only the build above consumed
+        self.route_plan = (self.S.local(flags, self.rank), extra if self.rank == 0 else 0, rc0) \
+            if staged is None else None
 
     def _max_local_bases(self, flags) -> int:
         sl = self.S.seq_len * np.asarray(flags, np.int64)
@@ -1052,8 +1258,17 @@ class DistRun:
             n_dbg, n_rdbg = self.streamed[:2]
             own = self.streamed[5]                          # (the sub-logs' rdBG keys)
         else:
-            n_dbg, n_rdbg, _, _ = exchange_and_reduce(self.sh, self.world, self.rank, self.device, self.sentinel,
-                                                      self.comm.group)
+            plan = getattr(self, "route_plan", None)
+            if plan is not None:
+                # the routed owner exchange (as the bench's N>1 step): the
+                # local table above served the dump's occurrence counts only
+                n_dbg, n_rdbg, _, _ = exchange_routed(self.sh, self.world, self.rank, self.device, plan[0], plan[1],
+                                                      plan[2], self.comm.group)
+            else:
+                # -d (the npz slots staged on rank 0) or a -r resume: the
+                # local table holds what no stage A can rebuild
+                n_dbg, n_rdbg, _, _ = exchange_and_reduce(self.sh, self.world, self.rank, self.device, self.sentinel,
+                                                          self.comm.group)
             own = np.ascontiguousarray(self.sh.owner_rdbg(), dtype=np.uint64)
         allk = np.sort(np.concatenate([p.view(np.uint64) for p in self.comm.allgather_bytes(own.view(np.uint8))]))
         if allk.shape[0] != n_rdbg:

@@ -329,6 +329,13 @@ class OracleShard:
         self.table.merge(ptr, n, sentinel)
         return self.table.build_rdbg()
 
+    def route_merge_segs(self, segs, nparts, sentinel=False):
+        rows = [np.ctypeslib.as_array((ctypes.c_int64 * (2 * n)).from_address(p)).reshape(n, 2)
+                for p, n in segs if n]
+        buf = np.ascontiguousarray(np.concatenate(rows)) if rows else np.zeros((1, 2), np.int64)
+        self.table.merge(buf.ctypes.data, buf.shape[0] if rows else 0, sentinel)
+        return self.table.build_rdbg()
+
     def build_rdbg(self):
         return self.table.build_rdbg()
 

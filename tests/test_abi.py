@@ -25,6 +25,23 @@ def test_library_exports_every_declared_symbol():
     assert sorted(_lib.SIGNATURES) == syms
 
 
+def test_binding_marshals_round6_entry_points():
+    """The ctypes argument lists of the round-6 entry points accept what the
+    Context methods pass (a NULL context: each returns PG_EINVAL, no device
+    touched)."""
+    from pangenome_amd import _lib
+    lib = _lib.load()
+
+    class Fake:
+        pass
+    f = Fake()
+    f.lib, f.h = lib, None
+    with pytest.raises(_lib.PangenomeError, match="pg_route_merge_segs"):
+        _lib.Context.route_merge_segs(f, [(0x1000, 3), (0, 0)], 4, True)
+    with pytest.raises(_lib.PangenomeError, match="pg_stream_wait"):
+        _lib.Context.stream_wait(f, 0)
+
+
 def test_no_device_fails_loudly():
     """Without a GPU the product raises; it never falls back to a CPU path."""
     import torch

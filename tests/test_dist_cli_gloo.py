@@ -27,11 +27,23 @@ def _cli_rank(rank, world, port, q, qry, argv, kw=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = io.StringIO()
+    used = []                                       # which owner exchange the rdBG step ran
+
+    def spy(name):
+        real = getattr(pdist, name)
+
+        def f(*a, **k):
+            used.append("%s(%s)" % (name, type(a[0]).__name__))
+            return real(*a, **k)
+        setattr(pdist, name, f)
+    spy("exchange_routed")
+    spy("exchange_and_reduce")
     try:
-        pdist.entry_point(argv, out=out, shard_factory=OracleShard, **(kw or {}))
+        pdist.entry_point(argv, out=out, shard_factory=OracleShard,
+                          **{k_: v for k_, v in (kw or {}).items() if k_ != "report"})
     finally:
         dist.destroy_process_group()
-    q.put((rank, out.getvalue()))
+    q.put((rank, out.getvalue() if kw is None or not kw.get("report") else (out.getvalue(), used)))
 
 
 def rows_of(text):
@@ -48,7 +60,13 @@ def test_dist_cli_matches_reference(name, world, tmp_path):
     q.write_bytes(fx.fasta)
     (tmp_path / "input.fsa_rdbg_weight.xyz.mcl").write_text(fx.mcl)
     argv = ["kmer_numba.py", "-i", str(q), "-k", str(fx.k), "-c", str(fx.c)]
-    outs = spawn_ranks(world, _cli_rank, (str(q), argv))
+    got = spawn_ranks(world, _cli_rank, (str(q), argv, {"report": True}))
+    outs = {r: got[r][0] for r in got}
+    # the rdBG step: the routed owner exchange (the bench's N>1 step) at a
+    # power-of-two world, the local-table exchange otherwise
+    for r in got:
+        assert got[r][1] == ["exchange_routed(OracleShard)", "exchange_and_reduce(%s)"
+                             % ("_Routed" if world & (world - 1) == 0 else "OracleShard")], got[r][1]
     assert (tmp_path / "input.fsa_rdbg_weight.xyz").read_text() == fx.xyz
     assert rows_of(outs[0]) == fx.rows
     assert all(rows_of(outs[r]) == [] for r in range(1, world))           # rank 0 prints

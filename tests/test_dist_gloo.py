@@ -125,7 +125,7 @@ def test_routed_exchange_matches_single_process(oracle_mod, world):
     assert sum(out[r][2] for r in range(world)) == ref_rdbg
 
 
-def _stream_worker(rank, world, port, q, fasta, k):
+def _stream_worker(rank, world, port, q, fasta, k, routed=False):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -141,8 +141,12 @@ def _stream_worker(rank, world, port, q, fasta, k):
     meta = sh.load(np.frombuffer(mine, np.uint8))
     R = int(meta["seq_len"].shape[0])
     chunks = stream_chunks(np.ones(R, np.uint8), meta["seq_len"], 1)     # one record per round
-    res = exchange_stream(sh, world, rank, "cpu", chunks, R, True, compact_at=1)
-    q.put((rank, res[:5]))
+    tm = {}
+    if routed:
+        res = exchange_stream(sh, world, rank, "cpu", chunks, R, True, tm=tm)
+    else:
+        res = exchange_stream(sh, world, rank, "cpu", chunks, R, True, compact_at=1, tm=tm, routed=False)
+    q.put((rank, res[:5] + (sorted(k_ for k_ in tm if k_ != "start"),)))
     dist.destroy_process_group()
 
 
@@ -157,10 +161,70 @@ def test_streamed_exchange_many_rounds_world3(oracle_mod):
     ref = oracle_mod.OracleRun(fasta, k, 2)
     out = spawn_ranks(3, _stream_worker, (fasta, k))
     for r in range(3):
-        n_dbg, n_rdbg, _, _, rounds = out[r]
+        n_dbg, n_rdbg, _, _, rounds, phases = out[r]
         assert rounds == 18
+        assert phases == ["build", "compact", "final", "log", "route"]
         assert (n_dbg, n_rdbg) == (ref.dbg()[0].shape[0], ref.rdbg().shape[0])
     assert sum(out[r][2] for r in range(3)) == ref.rdbg().shape[0]
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_routed_streamed_exchange_matches_single_process(oracle_mod, world):
+    """exchange_stream's routed form (no local table: every round's stage A
+    records straight to their owners' sub-logs, each sub-log one owner table
+    at the end from its received segments, pg_route_merge_segs): the sharded
+    totals equal the single-process build, every rank runs the same rounds,
+    and the owners' rdBG partitions are disjoint."""
+    from dist_util import spawn_ranks
+    from pangenome_amd import synth
+    k = 27
+    fasta = synth.pangenome(12, 3_000, snp=0.01, indel=1e-3, seed=47) + b">tiny\nACG\n"
+    ref = oracle_mod.OracleRun(fasta, k, 2)
+    out = spawn_ranks(world, _stream_worker, (fasta, k, True))
+    for r in range(world):
+        n_dbg, n_rdbg, _, _, rounds, phases = out[r]
+        assert rounds == -(-13 // world)
+        assert (n_dbg, n_rdbg) == (ref.dbg()[0].shape[0], ref.rdbg().shape[0])
+        assert phases == ["build", "final", "log", "route"]
+    assert sum(out[r][2] for r in range(world)) == ref.rdbg().shape[0]
+
+
+def _diagnose_worker(rank, world, port, q):
+    """_diagnose called directly with send/receive splits whose A2A_ROWS piece
+    counts differ between the ranks (rank 0: 2 pieces, rank 1: 1)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from pangenome_amd import dist as pdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pdist.A2A_ROWS = 100
+    # rows sent [to 0, to 1]: rank 0 [150, 50], rank 1 [50, 50]
+    counts = np.array([[150], [50]] if rank == 0 else [[50], [50]], np.int64)
+    rh = np.array([[150], [50]] if rank == 0 else [[50], [50]], np.int64)
+    g = torch.Generator().manual_seed(rank)
+    send = torch.randint(0, 1 << 40, (int(counts.sum()), 2), generator=g, dtype=torch.int64)
+    recv = torch.randint(0, 1 << 40, (int(rh.sum()), 2), generator=g, dtype=torch.int64)
+    sums = np.zeros(2, np.uint64)
+    bad = [(0, 0)] if rank == 0 else []
+    try:
+        pdist._diagnose(None, send, recv, counts, sums, rh, bad, world, 1, rank, "cpu", torch.device("cpu"), None,
+                        "diag")
+        q.put((rank, None))
+    except pdist.ExchangeIntegrityError as e:
+        q.put((rank, str(e)))
+    dist.destroy_process_group()
+
+
+def test_diagnose_with_uneven_piece_counts_raises_everywhere():
+    """the piece count is agreed collectively (MAX all-reduce)
+    before any rank diverges, so ranks with fewer pieces pad with empty ones
+    and every rank raises instead of one rank waiting in an all-gather."""
+    from dist_util import spawn_ranks
+    out = spawn_ranks(2, _diagnose_worker, (), timeout=60)
+    assert out[0] is not None and "from rank 0" in out[0], out
+    assert out[1] is not None and "rank 1" in out[1], out
 
 
 @pytest.mark.parametrize("world,rounds,subparts,want", [(1, 3, None, 4), (3, 17, None, 16), (3, 18, None, 16),

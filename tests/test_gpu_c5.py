@@ -101,8 +101,11 @@ def _c5_rank(rank, world, port, q, path, backend, chunk_bases, compact_at, whole
             return
     t0 = time.time()
     chunks = stream_chunks(np.ones(R, np.uint8), meta["seq_len"], chunk_bases)
-    res = exchange_stream(sh, world, rank, dev, chunks, R, True, compact_at=compact_at, subparts=subparts)
+    lib = {}
+    res = exchange_stream(sh, world, rank, dev, chunks, R, True, compact_at=compact_at, subparts=subparts,
+                          routed=False if form == "local" else None, lib_stats=lib)
     out["stream_s"] = time.time() - t0
+    out["routed"] = bool(lib)
     out["stream"] = [int(res[0]), int(res[1]), int(res[4]), rdbg_digest(np.sort(res[5]))]
     print("c5 rank: %s streamed in %.1f s: %s" % (backend, out["stream_s"], out["stream"][:3]), flush=True)
     q.put((rank, out))
@@ -122,11 +125,14 @@ def c5s_file(tmp_path_factory):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("backend", ["gloo", "nccl"])
-def test_c5_form_streamed_vs_oracle_digest(c5s_file, backend):
+@pytest.mark.parametrize("backend,form", [("gloo", "local"), ("nccl", "local"), ("nccl", "copy")])
+def test_c5_form_streamed_vs_oracle_digest(c5s_file, backend, form):
+    """The local-table form (compaction after every chunk) and the routed
+    form (stage A records straight to the owner's sub-logs)."""
     path, dg = c5s_file
-    out = spawn_ranks(1, _c5_rank, (path, backend, 125_000_000, 1, backend == "gloo", None), timeout=600)[0]
-    assert out["backend"] == backend
+    out = spawn_ranks(1, _c5_rank, (path, backend, 125_000_000, 1 if form == "local" else None, backend == "gloo",
+                                    None, form), timeout=600)[0]
+    assert out["backend"] == backend and out["routed"] == (form != "local")
     assert (out["records"], out["bases"]) == (4, dg["n_bases"])
     if "whole" in out:
         assert out["whole"] == [dg["n_dbg"], dg["n_rdbg"], dg["dbg_sha256"], dg["rdbg_sha256"]]
@@ -148,15 +154,17 @@ def c5m_file(tmp_path_factory):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("form", ["copy", "rccl", "poison"])
+@pytest.mark.parametrize("form", ["copy", "rccl", "poison", "local"])
 def test_c5m_streamed_at_2p30_vs_oracle_digest(c5m_file, form):
     """The streamed exchange at 2^30 forward bases per chunk (round 1 builds 8
-    records of 125 Mbp at once) against the oracle: the product path, RCCL
-    carrying the rank's own run, and poisoned buffers."""
+    records of 125 Mbp at once) against the oracle: the product path (routed:
+    at world 1 the scatter's buffer is the owner's log), RCCL carrying the
+    rank's own run, poisoned buffers, and the local-table form."""
     path, dg = c5m_file
     out = spawn_ranks(1, _c5_rank, (path, "nccl", 1 << 30, None, False, None, form), timeout=800)[0]
     print("c5m %s: %s" % (form, json.dumps(out, sort_keys=True)))
     assert out["self_copy"] == (form != "rccl")
+    assert out["routed"] == (form != "local")
     assert (out["records"], out["bases"]) == (10, dg["n_bases"])
     n_dbg, n_rdbg, rounds, rsha = out["stream"]
     assert rounds == 2
@@ -182,7 +190,8 @@ def test_c5_shard_full_size_vs_oracle_digest(tmp_path):
     nbytes = synth.write_c5(p, pairs=INPUTS["c5shard"]["pairs"], workers=10)
     assert nbytes == dg["fasta_bytes"]
     print("c5 shard: %d bytes generated in %.0f s" % (nbytes, time.time() - t0), flush=True)
-    forms = [("nccl_2^30_rccl", "nccl", 1 << 30, "rccl"), ("nccl_2^29_copy", "nccl", 1 << 29, "copy")]
+    forms = [("nccl_2^30_rccl", "nccl", 1 << 30, "rccl"), ("nccl_2^29_copy", "nccl", 1 << 29, "copy"),
+             ("nccl_2^30_local", "nccl", 1 << 30, "local")]
     if os.environ.get("PG_RUN_C5_GLOO") == "1":
         forms += [("gloo_2^30", "gloo", 1 << 30, "copy")]
     runs = {}
@@ -191,7 +200,8 @@ def test_c5_shard_full_size_vs_oracle_digest(tmp_path):
         print("c5 shard %s: %s" % (tag, json.dumps(runs[tag], sort_keys=True)), flush=True)
     a, b = runs["nccl_2^30_rccl"], runs["nccl_2^29_copy"]
     assert a["records"] == 30 and a["bases"] == dg["n_bases"]
-    assert a["stream"][2] == 4 and b["stream"][2] == 8
+    assert a["stream"][2] == 4 and b["stream"][2] == 8 and runs["nccl_2^30_local"]["stream"][2] == 4
+    assert a["routed"] and b["routed"] and not runs["nccl_2^30_local"]["routed"]
     for r in runs.values():
         assert [r["stream"][0], r["stream"][1], r["stream"][3]] == [dg["n_dbg"], dg["n_rdbg"], dg["rdbg_sha256"]]
     # both strands of every window, no N, odd k: closed under reverse complement

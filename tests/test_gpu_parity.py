@@ -365,6 +365,24 @@ def test_device_resident_input_and_repeat(km):
     assert np.array_equal(res[0][2], res[1][2])
 
 
+def test_build_device_empty_input():
+    """pg_build_device of an empty input, on a fresh context and
+    after a real build, succeeds with an empty dBG and zero parse time."""
+    import torch
+    from pangenome_amd import synth
+    from pangenome_amd._lib import Context
+    d = torch.frombuffer(bytearray(synth.pangenome(2, 20_000, seed=5)), dtype=torch.uint8).to("cuda:0")
+    e = torch.zeros(16, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    for warm in (False, True):
+        ctx = Context(27)
+        if warm:
+            assert ctx.build_device(d.data_ptr(), d.numel(), True, keepalive=d).n_dbg > 0
+        st = ctx.build_device(e.data_ptr(), 0, True, keepalive=e)
+        assert (st.n_records, st.n_bases, st.n_dbg, st.n_rdbg, st.ms_parse) == (0, 0, 0, 0, 0.0)
+        ctx.close()
+
+
 def test_full_size_properties(km):
     """C3-shaped input (100 genomes is too slow for the oracle; use 40 x 5 Mbp):
     size-independent invariants of the reference's dBG."""

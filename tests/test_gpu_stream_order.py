@@ -12,7 +12,9 @@ the same size - the same block - without waiting.  With a 16 GB round sent to
 self through RCCL (world 1, 512 MiB pieces) still in flight behind the next
 chunk's build, the scatter overwrote records the all-to-all and the copies had
 yet to move.  dist._fence (torch.cuda.synchronize before every native read or
-write of torch memory) closes it.
+write of torch memory) closed it; round 6's form is stream-ordered instead:
+the library's streams wait on an event of torch's current stream
+(pg_stream_wait), so the host never blocks for it.
 
 The test reproduces the hazard deterministically: a long kernel keeps torch's
 stream busy, a copy of a tensor is queued behind it, the tensor is freed and
@@ -40,8 +42,12 @@ def _table(ctx):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fenced", [False, True])
-def test_native_write_into_reused_torch_block(fenced):
+@pytest.mark.parametrize("fence", ["none", "sync", "event"])
+def test_native_write_into_reused_torch_block(fence):
+    """fence "sync": a device-wide synchronize; "event": the product form,
+    the library's streams wait on an event of torch's current stream
+    (pg_stream_wait), the host does not block."""
+    fenced = fence != "none"
     sys.path.insert(0, ROOT)
     import torch
     from pangenome_amd import dist as pdist
@@ -60,8 +66,10 @@ def test_native_write_into_reused_torch_block(fenced):
         send = torch.empty((n, 2), dtype=torch.int64, device=dev)
         if send.data_ptr() != ptr:
             pytest.skip("the allocator did not hand out the freed block")
-        if fenced:
+        if fence == "sync":
             pdist._fence(dev)
+        elif fence == "event":
+            pdist._fence(dev, ctx)
         ctx.partition(1, send.data_ptr(), n)           # the library's scatter, on its own stream
         torch.cuda.synchronize()
         intact = bool(torch.all(y == 7).item())
