@@ -584,7 +584,7 @@ def _pow2(n: int) -> bool:
 
 def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_records: int, rc0: bool, extra: int = 0,
                     staged=None, group=None, on_chunk=None, compact_at=None, subparts=None, tm=None, routed=None,
-                    lib_stats=None):
+                    lib_stats=None, keys=True):
     """The streaming exchange of SURVEY §8(e) for shards whose whole local
     table does not fit beside the owner partition (C5: 3.75 Gbp per GPU).
 
@@ -616,7 +616,8 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
     chunk's build (the dump gathers its occurrence counts there).  Returns
     (n_dbg_total, n_rdbg_total, n_rdbg_local, bytes_sent, rounds, the owner's
     rdBG keys - sorted within each sub-log, not across them: the callers
-    sort what they gather).  `lib_stats` (a dict, routed form): filled with the
+    sort what they gather; routed form with keys=False: counts only, the
+    keys are not exported and the last item is None).  `lib_stats` (a dict, routed form): filled with the
     library's HIP-event spans and record counts of every round and sub-log
     merge.  `tm` (a dict) accumulates the seconds of each phase (build,
     route = partition + all-to-all + checks, compact, final = the sub-logs'
@@ -631,13 +632,15 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
         raise ValueError("exchange_stream: the routed form needs a power-of-two world and no local table "
                          "(on_chunk / staged)")
     lap = _lapper(tm, device)
+    t0 = perf_counter()
     nch = torch.tensor([len(chunks)], dtype=torch.int64, device=comm)
     dist.all_reduce(nch, op=dist.ReduceOp.MAX, group=group)
     rounds = max(1, int(nch.item()))
     P = sublog_count(world, rounds, subparts)
+    lap("setup", t0)
     if routed:
         return _stream_routed(shard, world, rank, device, chunks, n_records, rc0, extra, group, rounds, P, lap,
-                              lib_stats)
+                              lib_stats, keys)
     if compact_at is None:
         compact_at = max(1 << 20, _free_device_bytes(device) // 4 // 16)
     logs = [[] for _ in range(P)]
@@ -750,7 +753,7 @@ def _lapper(tm, device):
 
 
 def _stream_routed(shard, world: int, rank: int, device, chunks, n_records: int, rc0: bool, extra: int, group,
-                   rounds: int, P: int, lap, lib_stats=None):
+                   rounds: int, P: int, lap, lib_stats=None, want_keys=True):
     """exchange_stream's routed form.  Per round: stage A of the chunk held
     for its owners (pg_route_stage_a; every rank runs `rounds` rounds, an
     empty chunk when out of records), the held regions to their owners in
@@ -800,6 +803,7 @@ def _stream_routed(shard, world: int, rank: int, device, chunks, n_records: int,
         bufs.append(recv)
         lap("log", t0)
     # the n<k sentinel key belongs to one owner: rank 0 (sub-log 0)
+    t0 = perf_counter()
     flag = torch.tensor([1 if sentinel else 0, 1 if fail else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     sent_global = bool(flag[0].item())
@@ -807,7 +811,7 @@ def _stream_routed(shard, world: int, rank: int, device, chunks, n_records: int,
         _raise_if_any(fail[0] if fail else None, [1], rank)
     n_dbg_loc = n_rdbg_loc = 0
     keys = []
-    t0 = lap("start", perf_counter())
+    t0 = lap("flag", t0)
     for p in range(P):
         _fence(device, shard)
         shard.route_merge_segs(segs[p], nparts, sentinel=sent_global and rank == 0 and p == 0)
@@ -822,15 +826,18 @@ def _stream_routed(shard, world: int, rank: int, device, chunks, n_records: int,
             lib["merges"].append(dict(rebin_ms=st.ms_insert, split_ms=st.ms_split, range_ms=st.ms_range,
                                       records=int(logn[p]), buckets=int(st.table_capacity), n_rdbg=int(st.n_rdbg),
                                       split_passes=int(st.build_flags) >> 16 & 255))
-        keys.append(np.ascontiguousarray(shard.owner_rdbg(), dtype=np.uint64))
+        t0 = lap("merge", t0)
+        if want_keys:
+            keys.append(np.ascontiguousarray(shard.owner_rdbg(), dtype=np.uint64))
+            t0 = lap("keys", t0)
     del bufs
-    lap("final", t0)
     sums = torch.tensor([n_dbg_loc, n_rdbg_loc, 1 if fail else 0], dtype=torch.int64, device=comm)
     dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
     n_dbg, n_rdbg, nfail = sums.tolist()
     if nfail:
         _raise_if_any(fail[0] if fail else None, [1], rank)
-    own = np.concatenate(keys) if keys else np.zeros(0, np.uint64)      # (each sub-log's keys sorted)
+    own = (np.concatenate(keys) if keys else np.zeros(0, np.uint64)) if want_keys else None   # (sorted per sub-log)
+    lap("tail", t0)
     if lib is not None:
         lib_stats.update(lib, subparts=P)
     return int(n_dbg), int(n_rdbg), n_rdbg_loc, sent, rounds, own

@@ -163,7 +163,7 @@ def test_streamed_exchange_many_rounds_world3(oracle_mod):
     for r in range(3):
         n_dbg, n_rdbg, _, _, rounds, phases = out[r]
         assert rounds == 18
-        assert phases == ["build", "compact", "final", "log", "route"]
+        assert phases == ["build", "compact", "final", "log", "route", "setup"]
         assert (n_dbg, n_rdbg) == (ref.dbg()[0].shape[0], ref.rdbg().shape[0])
     assert sum(out[r][2] for r in range(3)) == ref.rdbg().shape[0]
 
@@ -185,7 +185,7 @@ def test_routed_streamed_exchange_matches_single_process(oracle_mod, world):
         n_dbg, n_rdbg, _, _, rounds, phases = out[r]
         assert rounds == -(-13 // world)
         assert (n_dbg, n_rdbg) == (ref.dbg()[0].shape[0], ref.rdbg().shape[0])
-        assert phases == ["build", "final", "log", "route"]
+        assert phases == ["build", "flag", "keys", "log", "merge", "route", "setup", "tail"]
     assert sum(out[r][2] for r in range(world)) == ref.rdbg().shape[0]
 
 

@@ -102,7 +102,7 @@ def main():
                 t0 = time.perf_counter()
                 lib = {}
                 res = exchange_stream(sh, 1, 0, dev, chunks, R, True, tm=tm, routed=(form == "routed"),
-                                      lib_stats=lib)
+                                      lib_stats=lib, keys=(i == 0))
                 el = time.perf_counter() - t0
                 tm.pop("start", None)
                 r = {k: round(1e3 * v, 2) for k, v in tm.items()}

@@ -54,7 +54,7 @@ for step in "$@"; do
     ab) run ab_k3 600 python -u tools/ab_k3.py --steps 12 --tune base --tune K3_COVER=1 ;;
     listctr) run listctr 300 rocprofv3 -L ;;
     c5tests) run pytest_c5 1000 python -u -m pytest tests/test_gpu_c5.py -x -v -s --timeout 800 --timeout-method thread ;;
-    c5probe) run c5_probe 600 python -u tools/c5_probe.py stream routed local reps=3 ;;
+    c5probe) run c5_probe 600 python -u tools/c5_probe.py stream routed reps=4 ;;
     c5probeprof) run c5_probe_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5r -o run --output-format csv -- python -u tools/c5_probe.py stream routed reps=2 ;;
     newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_parity.py -k "empty or device_resident" -x -v --timeout 120 --timeout-method thread ;;
     benchc5q) run bench_c5q 600 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cli --no-concurrent ;;
