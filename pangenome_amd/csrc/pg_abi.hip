@@ -300,7 +300,13 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         x->c.k3_chunks = (int)value;
         break;
       case PG_TUNE_K3_COVER:
+#ifdef PG_COVER_LEGACY
         if (value < 0 || value > 2) throw pg::Error(PG_EINVAL, "pg_tune: K3 cover form must be 0, 1 or 2");
+#else
+        if (value != 0)
+          throw pg::Error(PG_EINVAL, "pg_tune: K3 cover form must be 0 (the class-byte forms 1 and 2 are built only "
+                                     "with PG_COVER_LEGACY)");
+#endif
         x->c.k3_cover = (int)value;
         break;
       case PG_TUNE_K3_WBLK:
@@ -319,7 +325,7 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         x->c.k3_anchors = (int)value;
         break;
       case PG_TUNE_K1:
-        if (value < 0 || value > 3) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 3]");
+        if (value < 0 || value > 7) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 7]");
         x->c.k1_form = (int)value;
         break;
       case PG_TUNE_K3_EMIT:

@@ -641,6 +641,7 @@ __host__ __device__ __forceinline__ void xcd_chunk(uint64_t ntiles, uint32_t b0,
 // XCD's drift hints carry over from the end of its previous chunk to the
 // start of the next.  (A persistent, software-pipelined one-tile form of this
 // kernel measured slower: 909 vs 845 us for all of C3's tiles.)
+#ifdef PG_COVER_LEGACY   // (rounds 2-3's class-byte forms: test-only builds, PG_TUNE_K3_COVER 1 / 2)
 __global__ void __launch_bounds__(CBLOCK)
 k_cover(const uint8_t* __restrict__ cls, const TileDesc* __restrict__ descs, WorkItem* __restrict__ queue,
         unsigned long long* __restrict__ qcount, unsigned long long qcap, int k, int ref, long long rfs,
@@ -859,13 +860,6 @@ __device__ __forceinline__ void drift_task_anc(const uint32_t* A, const uint8_t*
 // (its 32 bytes, realigned to dwords when staged)
 // (Checking each triple's hint drift exactly first and searching only the
 // misses measured neutral: stage A 0.599 ms either way.)
-// Search geometry of one (member, reference, anchor) triple, computed once
-// per block in the staging phase: ibhi = the reference index of drift 0's
-// candidate + DRIFT; [lo, hi] the full search range, [lo1, hi1] its part
-// within the hint window (empty if the triple does not dedup).
-struct TriGeo {
-  int ibhi, lo, hi, lo1, hi1;
-};
 __device__ __forceinline__ void cover_search_q(uint32_t (*s_anc)[NANCH][ALEN / 4], uint8_t (*s_ref)[RSZ],
                                                const TriGeo* tri, unsigned (*best)[2][NANCH], uint32_t dm0,
                                                uint32_t dm1) {
@@ -1118,6 +1112,16 @@ k_cover_q(const uint8_t* __restrict__ cls, uint64_t ncls, const TileDesc* __rest
   for (int m = 0; m < QM; ++m)
     if ((wmask >> m) & 1u) queue[sub * qcap + s_qbase + pos++] = WorkItem{mrs[m], mrn[m] - k, q0, cov[m], 0u};
 }
+
+#endif  // PG_COVER_LEGACY
+
+// Search geometry of one (member, reference, anchor) triple, computed once
+// per block in the staging phase: ibhi = the reference index of drift 0's
+// candidate + DRIFT; [lo, hi] the full search range, [lo1, hi1] its part
+// within the hint window (empty if the triple does not dedup).
+struct TriGeo {
+  int ibhi, lo, hi, lo1, hi1;
+};
 
 // ---- K3 coverage pass, packed form (the default; north_star's "2-bit
 // encode ... packed base stream").  Same groups, drift search and coverage
@@ -3051,7 +3055,9 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   const bool tail = part == SA_WHOLE || part == SA_TAIL || part == SA_FIRST_TAIL || part == SA_MORE_TAIL;
   const BinOut O = stageA_begin(c, cap, fl, begin);
   if (part == SA_TAIL) ntiles = 0;
+#ifdef PG_COVER_LEGACY
   if (c.k3_cover == 1 || c.k3_cover == 2) ensure_cls(c);   // (the class-byte coverage forms)
+#endif
 #ifdef PG_DEBUG_BOUNDS
   ensure_cls(c);                                            // (k_cover_p's debug check reads class bytes)
 #endif
@@ -3110,6 +3116,7 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   for (int i = 0; i < nch; ++i) {
     auto* qi = q + qoff[i];
     auto* qni = qn + (cbytes / 8) * i;
+#ifdef PG_COVER_LEGACY
     if (gc[i] && c.k3_cover == 1)
       hipLaunchKernelGGL(k_cover, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, td, qi, qni, (unsigned long long)qcapc[i],
                          c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,
@@ -3118,7 +3125,9 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
       hipLaunchKernelGGL(k_cover_q, dim3((unsigned)gc[i]), dim3(CBLOCK), 0, s0, cls, (uint64_t)c.cls.cap, td, qi, qni,
                          (unsigned long long)qcapc[i], c.k, c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n,
                          c.k3_hint.as<int>(), (int)c.n_records, ntiles, cb[i], cb[i + 1], cbt);
-    else if (gc[i])
+    else
+#endif
+    if (gc[i])
       launch_cover_p(c.k3_anchors ? c.k3_anchors : NAP_DEFAULT, dim3((unsigned)gc[i]), s0, c.p2.as<uint32_t>(),
                      c.e16.as<uint8_t>(), (uint64_t)(c.p2.cap / 4), cls, td, qi, qni, (unsigned long long)qcapc[i], c.k,
                      c.k3_ref, rfs, rfn, c.k3_ref2, r2s, r2n, c.k3_hint.as<int>(), (int)c.n_records, ntiles,

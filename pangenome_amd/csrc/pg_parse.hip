@@ -871,6 +871,12 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
   auto* incl = c.span_start.as<Fn>();
   size_t bytes = 0;
   PG_HIP(rocprim::inclusive_scan(nullptr, bytes, fns, incl, (size_t)nspan, FnThen{}, st));
+  {
+    size_t b2 = 0;                                          // (the chunked form's carried-in scans)
+    PG_HIP(rocprim::inclusive_scan(nullptr, b2, fns, incl, rocprim::future_value<Fn>(incl), (size_t)nspan, FnThen{},
+                                   st));
+    bytes = std::max(bytes, b2);
+  }
   c.scratch.reserve(bytes + 16);
   auto scan = [&](uint64_t upto) {
     size_t b = c.scratch.cap;
@@ -1007,6 +1013,30 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
       (*on_chunk)(Rc);
     }
     upload->finish();
+  } else if (c.k1_form & 4) {
+    // (PG_TUNE_K1 bit 2, experiment) the file in chunks of h2d_chunk bytes,
+    // each chunk's span pass, scan (carried in from the previous chunk's
+    // total on the device: rocprim::future_value) and emission back to back,
+    // so the emission re-reads bytes the span pass left in the Infinity Cache
+    const uint64_t C = std::max<uint64_t>(WSPAN, c.h2d_chunk / WSPAN * WSPAN);
+    const uint64_t cs = C / WSPAN;
+    for (uint64_t s0 = 0; s0 < nspan; s0 += cs) {
+      const uint64_t s1 = std::min(nspan, s0 + cs);
+      span_pass(s0, s1);
+      if (s0 == 0) {
+        scan(s1);
+      } else {
+        size_t b = c.scratch.cap;
+        PG_HIP(rocprim::inclusive_scan(c.scratch.p, b, fns + s0, incl + s0, rocprim::future_value<Fn>(incl + s0 - 1),
+                                       (size_t)(s1 - s0), FnThen{}, st));
+      }
+      records(s0, s1, rcap0);
+      if (s1 == nspan) {
+        pending = {s0, s1};
+      } else {
+        emit(s0, s1);
+      }
+    }
   } else {
     span_pass(0, nspan);
     PG_HIP(hipGetLastError());

@@ -219,10 +219,13 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     head[:, P] = 1 if sentinel_local else 0
     head[:, P + 1:2 * P + 1] = sums.reshape(world, P).view(np.int64)
     head[:, 2 * P + 1] = 1 if fail else 0
-    send_head = torch.from_numpy(head.reshape(-1)).to(comm)
-    heads = [torch.empty_like(send_head) for _ in range(world)]
-    dist.all_gather(heads, send_head, group=group)
-    H = torch.stack(heads).cpu().numpy().reshape(world, world, 2 * P + 2)  # [source, owner, counts|flag|sums|fail]
+    if world == 1:
+        H = head.reshape(1, 1, 2 * P + 2)            # (a one-rank all-gather is the identity)
+    else:
+        send_head = torch.from_numpy(head.reshape(-1)).to(comm)
+        heads = [torch.empty_like(send_head) for _ in range(world)]
+        dist.all_gather(heads, send_head, group=group)
+        H = torch.stack(heads).cpu().numpy().reshape(world, world, 2 * P + 2)  # [source, owner, counts|flag|sums|fail]
     _raise_if_any(fail, H[:, 0, 2 * P + 1].tolist(), rank)
     rh = H[:, rank, :P]
     want = H[:, rank, P + 1:2 * P + 1].copy().view(np.uint64)
@@ -249,14 +252,17 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     got = [int(x) for x in want.reshape(-1)] if alias else _seg_sums(table, recv, off, device)
     bad = [(s, p) for s in range(world) for p in range(P) if got[s * P + p] != int(want[s, p])]
     if defer is not None:
-        # the caller's next all-reduce carries the check; the closure keeps the
-        # send buffer's piece sums, not the buffer (unless it is the receive)
-        pieces = _piece_sums(table, send, counts.sum(axis=1), rh.sum(axis=1), world, device) \
-            if send is not recv else None
-        snd = send if send is recv else None
+        # the caller's next all-reduce carries the check.  (The closure keeps
+        # the send buffer until the caller returns - one more buffer of 16 B
+        # per sent record at the owner merge's peak, <= ~1 GB for C4-sized
+        # shards - rather than summing its pieces up front on every exchange:
+        # a pass over the whole buffer, ~0.1 ms on C3, for a failure path.)
         defer["bad"] = bad
-        defer["diagnose"] = lambda: _diagnose(table, snd, recv, counts, sums, rh, bad, world, P, rank, device, comm,
-                                              group, where, pieces)
+        defer["diagnose"] = lambda: _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm,
+                                              group, where)
+    elif world == 1:
+        if bad:
+            _diagnose(table, send, recv, counts, sums, rh, bad, world, P, rank, device, comm, group, where)
     else:
         flag = torch.tensor([1 if bad else 0], dtype=torch.int64, device=comm)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
@@ -425,11 +431,15 @@ def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=No
     import torch
     import torch.distributed as dist
     _, comm = _comm_device(device, group)
+    world = dist.get_world_size(group)
     t0 = perf_counter()
     if sentinel_global is None:
-        flag = torch.tensor([1 if sentinel_local else 0], dtype=torch.int64, device=comm)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
-        sentinel_global = bool(flag.item())
+        if world == 1:
+            sentinel_global = bool(sentinel_local)
+        else:
+            flag = torch.tensor([1 if sentinel_local else 0], dtype=torch.int64, device=comm)
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+            sentinel_global = bool(flag.item())
     # the n<k sentinel key belongs to one owner: rank 0
     n = int(recv.shape[0])
     fail = None
@@ -441,9 +451,12 @@ def _owner_reduce(table, recv, rank: int, device, sentinel_local: bool, group=No
                               "exchange: rank %d's owner merge" % rank)
     st = table.build_rdbg()
     rbad = 1 if route and route.get("bad") else 0
-    sums = torch.tensor([st.n_dbg, st.n_rdbg, 1 if fail else 0, rbad], dtype=torch.int64, device=comm)
-    dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
-    n_dbg, n_rdbg, nfail, nrbad = sums.tolist()
+    if world == 1:                                    # (a one-rank all-reduce is the identity)
+        n_dbg, n_rdbg, nfail, nrbad = int(st.n_dbg), int(st.n_rdbg), 1 if fail else 0, rbad
+    else:
+        sums = torch.tensor([st.n_dbg, st.n_rdbg, 1 if fail else 0, rbad], dtype=torch.int64, device=comm)
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM, group=group)
+        n_dbg, n_rdbg, nfail, nrbad = sums.tolist()
     if nrbad:
         route["diagnose"]()                          # (collective; raises on every rank)
     if nfail:

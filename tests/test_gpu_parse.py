@@ -69,6 +69,9 @@ def _check(buf, oracle_mod, k1=None):
         c = Context(k)
         if k1 is not None:
             c.tune(PG_TUNE_K1, k1)
+            if k1 & 4:                                # the chunked form: chunks of 2 spans (32 KiB)
+                from pangenome_amd._lib import PG_TUNE_H2D_CHUNK
+                c.tune(PG_TUNE_H2D_CHUNK, 2 * 16384)
         return c
     ctx = make(5)
     ctx.set_fasta(buf)
@@ -96,8 +99,9 @@ def _check(buf, oracle_mod, k1=None):
 
 
 # K1's forms (PG_TUNE_K1): per-step / whole-span span pass, one / two steps
-# of emission loads in flight
-K1_FORMS = [0, 1, 2, 3]
+# of emission loads in flight; bit 2: the device input in chunks (span pass,
+# carried-in scan and emission per chunk)
+K1_FORMS = [0, 1, 2, 3, 4, 5]
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
