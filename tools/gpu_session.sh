@@ -57,7 +57,8 @@ for step in "$@"; do
     c5probe) run c5_probe 600 python -u tools/c5_probe.py stream routed reps=4 ;;
     c5probeprof) run c5_probe_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5r -o run --output-format csv -- python -u tools/c5_probe.py stream routed reps=2 ;;
     newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_parity.py -k "empty or device_resident" -x -v --timeout 120 --timeout-method thread ;;
-    k1chunk) run pytest_k1chunk 600 python -u -m pytest tests/test_gpu_parse.py -k "4 or 5" -x -q --timeout 120 --timeout-method thread && run ab_k1chunk 600 python -u tools/ab_k3.py --alt --steps 16 --tune base --tune K1=4 --tune K1=4,H2D_CHUNK=134217728 --tune K1=4,H2D_CHUNK=268435456 --tune K1=4,H2D_CHUNK=33554432 ;;
+    k1) run pytest_k1 600 python -u -m pytest tests/test_gpu_parse.py -k "-8] or -24] or -40] or one_read" -x -v --timeout 300 --timeout-method thread && run ab_k1 600 python -u tools/ab_k3.py --alt --steps 16 --tune base --tune K1=8 --tune K1=24 --tune K1=40 --tune K1=72 ;;
+    k1prof) run k1_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_k1 -o run --output-format csv -- python -u tools/ab_k3.py --alt --steps 6 --tune base --tune K1=8 --tune K1=24 ;;
     benchc5q) run bench_c5q 600 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cli --no-concurrent ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
