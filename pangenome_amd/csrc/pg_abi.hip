@@ -88,7 +88,7 @@ void pg_destroy(pg_ctx* x) {
   pg::Ctx& c = x->c;
   (void)hipSetDevice(c.device);
   (void)hipStreamSynchronize(c.stream);
-  pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.k1_pub, &c.n_sel, &c.rec_start, &c.rec_len,
+  pg::DevBuf* bufs[] = {&c.fasta_own, &c.span_sum, &c.span_start, &c.n_sel, &c.rec_start, &c.rec_len,
                         &c.rec_hdr, &c.rec_ptr, &c.rec_flag, &c.cls, &c.p2, &c.e16, &c.scratch, &c.table, &c.ovf, &c.flags,
                         &c.recA_key, &c.recA_mw, &c.ctrA, &c.recS_key[0], &c.recS_key[1], &c.recS_mw[0],
                         &c.recS_mw[1], &c.ctrS, &c.snapA, &c.rseg, &c.k5_ctr, &c.tile_sched, &c.tile_desc, &c.k3_queue,
@@ -325,7 +325,7 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         x->c.k3_anchors = (int)value;
         break;
       case PG_TUNE_K1:
-        if (value < 0 || value > 255) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 255]");
+        if (value < 0 || value > 3) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 3]");
         x->c.k1_form = (int)value;
         break;
       case PG_TUNE_K3_EMIT:

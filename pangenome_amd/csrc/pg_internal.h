@@ -182,8 +182,6 @@ struct Ctx {
 
   // ---- parse products (K1)
   DevBuf span_sum, span_start;    // per 16 KiB wave span: function / inclusive prefix (K1)
-  DevBuf k1_pub;                  // one-read K1: tagged aggregate / inclusive words per block span, ticket, error
-  uint32_t k1_epoch = 0;          // one-read K1: the tag of this parse's published words (16 bits, never 0)
   DevBuf n_sel;                   // device counters
   DevBuf rec_start, rec_len;      // int64 per record: compacted offset / length
   DevBuf rec_hdr, rec_ptr;        // int64 per record: header byte span packed, `ptr` emulation

@@ -530,8 +530,7 @@ __device__ __forceinline__ uint32_t pack_word(const uint4& v, uint32_t& exc) {
 // One span's emission: each content byte -> its class code at its compacted
 // offset (staged in the wave's `stage` slice), the packed words and
 // exception bytes of the chunks the span owns whole.  `pre` = the function
-// of the spans before it.  (k_emit: a wave per span; k_parse1 calls it with
-// the span's bytes just read by its span pass, in the caches.)
+// of the spans before it.
 template <int PF>
 __device__ __forceinline__ void emit_span(const uint8_t* __restrict__ buf, uint64_t n, uint64_t span, const Fn& pre,
                                           const uint8_t* lut, uint8_t* stage, uint8_t* __restrict__ out,
@@ -761,204 +760,6 @@ __global__ void __launch_bounds__(PBLOCK) k_headers(const uint8_t* __restrict__ 
   }
 }
 
-// ---- K1 in one read (PG_TUNE_K1 bit 3; device-resident input).  A block of
-// KW waves takes a *block span* of KW consecutive 16 KiB spans by ticket (a
-// global counter: the block spans in flight are always the lowest not yet
-// done, so every wait below is for a block that is running).  Each wave loads
-// its span's 16 steps into registers once, computes the span's function (the
-// per-step pass, seg_fn), and the block composes the KW functions in LDS.
-// Wave 0 publishes the block aggregate, then looks back over the block spans
-// before it - 64 per window, one per lane - composing aggregates until it
-// meets an inclusive prefix (decoupled look-back, Merrill & Garland), and
-// publishes its own inclusive prefix.  Every wave then emits its span from
-// the registers (k_emit's steps), writes its span's inclusive function
-// (incl[], for k_pack_fix / k_records / a header re-run) and, when a header
-// starts in its span or its span starts inside a header line, the record
-// table entries (header_span's steps).  A block span is KW x 16 KiB, so the
-// look-back's front moves KW spans per hop (round 4's one-wave-per-span
-// look-back measured 0.70 ms).
-// Publication: per block span and kind (aggregate, inclusive) 6 words of 64
-// bits, each (tag << 48 | value), tag = this parse's epoch; words are stored
-// and loaded as agent-scope atomics (sc1), so a reader sees each word either
-// stale (another tag) or whole - a function is taken only when all 6 carry
-// the tag, and no ordering between the words is needed.  A look-back that
-// waits past K1_SPIN_MAX polls sets the error word and gives up (the host
-// raises): never a hang.
-constexpr int KW_DEFAULT = 8;                          // waves (spans) per block span
-constexpr uint32_t K1_SPIN_MAX = 1u << 22;
-constexpr int K1_PUB0 = 8;                             // words: [0] ticket, [1] error, [8 ..) agg, then inc
-__device__ __forceinline__ void pub_store(unsigned long long* w, unsigned long long v) {
-  __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long pub_load(const unsigned long long* w) {
-  return __hip_atomic_load(const_cast<unsigned long long*>(w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// word i of function f's publication (lane i of the publishing wave stores it)
-__device__ __forceinline__ unsigned long long fn_word(const Fn& f, int i, unsigned long long tag) {
-  const unsigned long long T = tag << 48, M = (1ull << 48) - 1ull;
-  switch (i) {
-    case 0: return T | ((unsigned long long)(f.o & 3u) << 46) | (f.c0 & ((1ull << 46) - 1ull));
-    case 1: return T | (f.c1 & M);
-    case 2: return T | (f.nl & M);
-    case 3: return T | (f.hdr & M);
-    case 4: return T | ((unsigned long long)(f.last + 1) & M);
-    default: return T | ((unsigned long long)(f.last2 + 1) & M);
-  }
-}
-__device__ __forceinline__ bool fn_read(const unsigned long long* w, unsigned long long tag, Fn& f) {
-  unsigned long long x[6];
-#pragma unroll
-  for (int i = 0; i < 6; ++i) x[i] = pub_load(w + i);
-  bool ok = true;
-#pragma unroll
-  for (int i = 0; i < 6; ++i) ok &= (x[i] >> 48) == tag;
-  const unsigned long long M = (1ull << 48) - 1ull;
-  f.c0 = x[0] & ((1ull << 46) - 1ull);
-  f.o = (uint32_t)(x[0] >> 46) & 3u;
-  f.c1 = x[1] & M;
-  f.nl = x[2] & M;
-  f.hdr = x[3] & M;
-  f.last = (long long)(x[4] & M) - 1;
-  f.last2 = (long long)(x[5] & M) - 1;
-  return ok;
-}
-__device__ __forceinline__ Fn fn_shfl_down(const Fn& f, int o) {
-  Fn r;
-  r.c0 = __shfl_down(f.c0, o, 64);
-  r.c1 = __shfl_down(f.c1, o, 64);
-  r.nl = __shfl_down(f.nl, o, 64);
-  r.hdr = __shfl_down(f.hdr, o, 64);
-  r.last = __shfl_down(f.last, o, 64);
-  r.last2 = __shfl_down(f.last2, o, 64);
-  r.o = __shfl_down(f.o, o, 64);
-  return r;
-}
-__device__ __forceinline__ Fn fn_lane0(const Fn& f) {
-  Fn r;
-  r.c0 = __shfl(f.c0, 0, 64);
-  r.c1 = __shfl(f.c1, 0, 64);
-  r.nl = __shfl(f.nl, 0, 64);
-  r.hdr = __shfl(f.hdr, 0, 64);
-  r.last = __shfl(f.last, 0, 64);
-  r.last2 = __shfl(f.last2, 0, 64);
-  r.o = __shfl(f.o, 0, 64);
-  return r;
-}
-
-// The prefix of block span t (the composition of block spans 0 .. t-1) by
-// wave 0 of its block: windows of 64 block spans, lane l looking at t-1-64i-l.
-__device__ __forceinline__ Fn k1_lookback(const unsigned long long* agg, const unsigned long long* inc, uint64_t t,
-                                          unsigned long long tag, unsigned long long* err) {
-  const int lane = threadIdx.x & 63;
-  Fn acc = fn_identity();
-  long long j = (long long)t - 1;
-  uint32_t spins = 0;
-  for (;;) {
-    const long long q = j - lane;
-    Fn fi = fn_identity(), fa = fn_identity();
-    bool vi = false, va = false;
-    if (q >= 0) {
-      vi = fn_read(inc + 8 * q, tag, fi);
-      if (!vi) va = fn_read(agg + 8 * q, tag, fa);
-    }
-    const unsigned long long I = __ballot(vi), R = __ballot(vi || va);
-    const unsigned long long live = j >= 63 ? ~0ull : ((1ull << (j + 1)) - 1ull);   // lanes with q >= 0
-    bool go = false, done = false;
-    int L = 64;
-    if (I) {
-      L = __builtin_ctzll(I);
-      const unsigned long long need = L ? ((1ull << L) - 1ull) : 0ull;
-      go = (R & need) == need;
-      done = go;
-    } else {
-      go = (R & live) == live && j >= 63;        // (q = 0 is always an inclusive once published)
-    }
-    if (!go) {
-      if (++spins > K1_SPIN_MAX) {
-        if (lane == 0) atomicOr(err, 1ull);
-        return acc;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    // x_l: the aggregates of lanes below L, the inclusive at L, nothing past it
-    Fn x = lane < L ? fa : (lane == L ? fi : fn_identity());
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const Fn y = fn_shfl_down(x, o);           // lane l + o: the earlier block span
-      if ((lane & (2 * o - 1)) == 0 && lane + o < 64) x = FnThen{}(y, x);
-    }
-    acc = FnThen{}(fn_lane0(x), acc);
-    if (done) return acc;
-    j -= 64;
-  }
-}
-
-template <int KW, bool LB>
-__global__ void __launch_bounds__(64 * KW, 4) k_parse1(const uint8_t* __restrict__ buf, uint64_t n, uint64_t nspan,
-                                                uint64_t nblk, unsigned long long* __restrict__ pub,
-                                                unsigned long long tag, Fn* __restrict__ incl,
-                                                uint8_t* __restrict__ out, uint32_t* __restrict__ p2,
-                                                uint8_t* __restrict__ e16, uint64_t rcap,
-                                                long long* __restrict__ rec_start,
-                                                long long* __restrict__ hdr_start, long long* __restrict__ hdr_end) {
-  constexpr int STAGE = WSTEP + 48;
-  __shared__ uint8_t lut[256];
-  __shared__ __attribute__((aligned(16))) uint8_t stage_all[KW][STAGE];
-  __shared__ Fn s_f[KW];
-  __shared__ Fn s_pre;
-  __shared__ unsigned long long s_t;
-  if (threadIdx.x < 256) lut[threadIdx.x] = c_byte_class[threadIdx.x];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  unsigned long long* err = pub + 1;
-  const unsigned long long* agg = pub + K1_PUB0;
-  const unsigned long long* inc = pub + K1_PUB0 + 8 * nblk;
-  for (;;) {                                                   // block-uniform
-    __syncthreads();                                           // (the last block span's LDS reads are done)
-    if (threadIdx.x == 0) s_t = atomicAdd(pub, 1ull);
-    __syncthreads();
-    const uint64_t t = s_t;
-    if (t >= nblk) return;
-    const uint64_t span = t * KW + (uint64_t)w;
-    const bool mine = span < nspan;                            // (wave-uniform)
-    const uint64_t p0 = span * WSPAN;
-    uint4 v[WSTEPS];
-    uint32_t carry = 1u;
-    Fn f = fn_identity();
-    if (mine) {
-      load_span(buf, p0, n, lane, v);
-      carry = p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u);
-      f = span_fn(v, n, p0, lane, carry);
-    }
-    if (lane == 0) s_f[w] = f;
-    __syncthreads();
-    if (w == 0) {
-      Fn a = s_f[0];
-#pragma unroll
-      for (int q = 1; q < KW; ++q) a = FnThen{}(a, s_f[q]);
-      Fn pre = fn_identity();
-      if (t == 0) {
-        if (lane < 6) pub_store(const_cast<unsigned long long*>(inc) + lane, fn_word(a, lane, tag));
-      } else {
-        if (lane < 6) pub_store(const_cast<unsigned long long*>(agg) + 8 * t + lane, fn_word(a, lane, tag));
-        if (LB) pre = k1_lookback(agg, inc, t, tag, err);   // (LB false: a timing experiment, wrong offsets)
-        const Fn ia = FnThen{}(pre, a);
-        if (lane < 6) pub_store(const_cast<unsigned long long*>(inc) + 8 * t + lane, fn_word(ia, lane, tag));
-      }
-      if (lane == 0) s_pre = pre;
-    }
-    __syncthreads();
-    if (!mine) continue;                                       // (wave-uniform; the loop head's barrier follows)
-    Fn e = s_pre;
-    for (int q = 0; q < w; ++q) e = FnThen{}(e, s_f[q]);
-    if (lane == 0) incl[span] = FnThen{}(e, f);
-    // the emission and the header entries read the span again: the bytes its
-    // span pass just loaded, from the caches (L2 / Infinity Cache), not HBM
-    emit_span<1>(buf, n, span, e, lut, stage_all[w], out, p2, e16);
-    if (f.hdr != 0 || (e.o & 1u)) header_span(buf, n, span, lane, e, rcap, rec_start, hdr_start, hdr_end);
-  }
-}
-
 // The packed word of every 16-byte chunk that spans s-1 and s share (the one
 // holding output offset own_s = incl[s-1].c0, when own_s is not a chunk
 // start, and the stream's last, partial chunk), recomputed from the class
@@ -1159,7 +960,6 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     PG_HIP(hipEventSynchronize(c.rec_ev));
   };
   reserve_records(rcap0);
-  bool k1_one_read = false;                                  // (k_parse1 ran: its error word is checked below)
   bool streaming = on_chunk != nullptr;
   std::pair<uint64_t, uint64_t> pending{0, 0};               // spans whose emission follows the table's copy
   // (the stager's last work - waiting for the DMAs and unregistering the
@@ -1219,39 +1019,6 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
       (*on_chunk)(Rc);
     }
     upload->finish();
-  } else if (c.k1_form & 8) {
-    // K1 in one read (k_parse1): emission, span functions and the header
-    // entries in one launch; the record table and its copy follow on `st`
-    if (n >= (1ull << 46)) throw Error(-22, "parse: one-read K1 takes inputs below 2^46 bytes");
-    const int kw = (c.k1_form & 16) ? 4 : (c.k1_form & 32) ? 16 : KW_DEFAULT;
-    const bool lb = !(c.k1_form & 64);
-    const uint64_t nblk = (nspan + kw - 1) / kw;
-    const size_t pw = K1_PUB0 + 16 * nblk;
-    const size_t old_cap = c.k1_pub.cap;
-    const void* old_p = c.k1_pub.p;
-    c.k1_pub.reserve(8 * pw);
-    if (c.k1_pub.p != old_p || c.k1_pub.cap != old_cap || c.k1_epoch == 0 || c.k1_epoch >= 0xFFFFu) {
-      PG_HIP(hipMemsetAsync(c.k1_pub.p, 0, c.k1_pub.cap, st));   // (new memory, or the tags wrapped)
-      c.k1_epoch = 0;
-    }
-    ++c.k1_epoch;
-    PG_HIP(hipMemsetAsync(c.k1_pub.p, 0, 16, st));              // ticket, error
-    const unsigned grid = (unsigned)std::min<uint64_t>(nblk, (uint64_t)(16 / kw) * c.n_cu);   // 16 waves per CU
-    auto go = [&](auto kern, int threads) {
-      hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, st, c.d_fasta, n, nspan, nblk,
-                         c.k1_pub.as<unsigned long long>(), (unsigned long long)c.k1_epoch, incl, c.cls.as<uint8_t>(),
-                         c.p2.as<uint32_t>(), c.e16.as<uint8_t>(), rcap0, c.rec_start.as<long long>(),
-                         c.rec_hdr.as<long long>(), c.rec_hdr.as<long long>() + rcap0);
-    };
-    if (kw == 4) lb ? go(k_parse1<4, true>, 256) : go(k_parse1<4, false>, 256);
-    else if (kw == 16) go(k_parse1<16, true>, 1024);
-    else lb ? go(k_parse1<8, true>, 512) : go(k_parse1<8, false>, 512);
-    PG_HIP(hipGetLastError());
-    hipLaunchKernelGGL(k_pack_fix, dim3(grid_for(nspan + 1, 256, 65535)), dim3(256), 0, st, incl, (uint64_t)0, nspan,
-                       c.cls.as<uint8_t>(), c.p2.as<uint32_t>(), c.e16.as<uint8_t>());
-    PG_HIP(hipGetLastError());
-    c.t0.stop(st);
-    k1_one_read = true;
   } else {
     span_pass(0, nspan);
     PG_HIP(hipGetLastError());
@@ -1286,11 +1053,6 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     }
     table_wait();
     tot = *c.h_pin.as<Fn>();
-    if (k1_one_read && attempt == 0) {
-      unsigned long long e = 0;
-      PG_HIP(hipMemcpy(&e, c.k1_pub.as<unsigned long long>() + 1, 8, hipMemcpyDeviceToHost));
-      if (e) throw Error(-5, "parse: the one-read K1's look-back gave up waiting (K1_SPIN_MAX polls)");
-    }
     R = tot.nl ? tot.hdr : 0;
     if (R <= rcap) {
       const int64_t* pk = c.h_pin.as<int64_t>() + 8;

@@ -96,9 +96,8 @@ def _check(buf, oracle_mod, k1=None):
 
 
 # K1's forms (PG_TUNE_K1): per-step / whole-span span pass, one / two steps
-# of emission loads in flight;
-# bit 3: K1 in one read (k_parse1; bit 4: 4 spans per block span, bit 5: 16)
-K1_FORMS = [0, 1, 2, 3, 8, 24, 40]
+# of emission loads in flight
+K1_FORMS = [0, 1, 2, 3]
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
@@ -393,50 +392,3 @@ def test_build_host_early_split():
     # ratios alone); from build 2 on the estimate holds
     assert used[0] == 0 and used[2] == 1 and used[3] == 0 and used[4] == 1, used
 
-
-def _big_inputs():
-    """Inputs of hundreds to thousands of 16 KiB spans (the one-read K1's
-    look-back crosses many 64-block-span windows): a pangenome at an odd line
-    width; a soup of short lines, headers, N runs, lowercase, CR and IUPAC
-    bytes; headers placed on and around every 128 KiB block-span edge."""
-    from pangenome_amd import synth
-    rng = np.random.default_rng(11)
-    soup = _soup(12, 24_000_000, b"ACGTACGTACGTacgtNNRY\r" + b"ACGT" * 20 + b"\n\n\n\n>")
-    blk = 128 * 1024
-    parts, pos = [], 0
-    for i in range(160):
-        want = (i + 1) * blk + int(rng.integers(-3, 4))
-        body = b"ACGT" * ((want - pos - 8) // 4)
-        parts.append(b">r%03d\n" % i + body[:max(0, want - pos - 6)])
-        pos += len(parts[-1])
-    edges = b"\n".join(parts) + b"\n"
-    return {"pangenome_w61": synth.pangenome(24, 1_000_000, snp=2e-3, indel=2e-4, seed=77, width=61),
-            "soup_24M": soup, "block_edges": edges}
-
-
-@pytest.mark.timeout(300)
-def test_one_read_k1_matches_two_pass_at_scale():
-    """K1 in one read (PG_TUNE_K1 8) against the two-pass K1 (0) on inputs of
-    hundreds to thousands of spans: the record table, the base count and the
-    dBG (keys and masks) are identical; one context parses inputs of
-    different sizes in turn (each parse's published words carry its own tag,
-    so a larger earlier parse's words are never taken)."""
-    from pangenome_amd._lib import PG_TUNE_K1, Context
-    ins = _big_inputs()
-    c0, c8 = Context(27), Context(27)
-    c8.tune(PG_TUNE_K1, 8)
-    for name in ("pangenome_w61", "soup_24M", "block_edges", "pangenome_w61", "block_edges"):
-        buf = ins[name]
-        res = []
-        for c in (c0, c8):
-            c.set_fasta(buf)
-            R, B = c.parse()
-            rec = c.records()
-            c.build_dbg(None, 0, True)
-            keys, masks = c.dbg()
-            res.append((R, B, {k: v.tolist() for k, v in rec.items()}, keys, masks))
-        a, b = res
-        assert a[:3] == b[:3], name
-        assert np.array_equal(a[3], b[3]) and np.array_equal(a[4], b[4]), name
-    c0.close()
-    c8.close()
