@@ -1189,10 +1189,11 @@ class DistRun:
             return
         self.sentinel = self.sh.build(self.S.local(flags, self.rank), extra if self.rank == 0 else 0, rc0)
         # the rdBG's exchange re-runs this pass's stage A held for its owners
-        # (exchange_routed) - unless rank 0 staged -r checkpoint slots, which
-        # only the build above consumed
+        # (exchange_routed) - unless this is a -r resume, whose checkpoint
+        # slots rank 0 staged into the build above only (the same decision
+        # on every rank: `resume` is global, `staged` is rank 0's)
         self.route_plan = (self.S.local(flags, self.rank), extra if self.rank == 0 else 0, rc0) \
-            if staged is None else None
+            if not (brkpt and os.path.isfile(brkpt)) else None
 
     def _max_local_bases(self, flags) -> int:
         sl = self.S.seq_len * np.asarray(flags, np.int64)

@@ -16,7 +16,7 @@ run() {  # name timeout cmd...
 for step in "$@"; do
   case $step in
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
-    testsall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+    testsall) run pytest_gpu 1100 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 900 python bench.py ;;
     benchq) run bench 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
@@ -32,7 +32,7 @@ for step in "$@"; do
     benchc4) run bench_c4 900 python bench.py --config c4 --steps 5 --warmup 2 --no-cpu-baseline --no-cli ;;
     benchsmall) run bench_small 600 python bench.py --config small --steps 5 --warmup 1 --no-cpu-baseline ;;
     benchc2) run bench_c2 600 python bench.py --config c2 --steps 20 --warmup 3 --no-cpu-baseline ;;
-    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange --no-concurrent ;;
+    prof) run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange --no-concurrent --no-c5 ;;
     pmcsq) bash tools/pmc_kernels.sh "k_emit_work|k_cover_p|k_build_range|k_emit\(|k_span_sum|k_split" sq ;;
     pmc) bash tools/pmc_kernels.sh "k_span_sum|k_emit|k_records|k_pack_fix|k_cover|k_short_emit|k_split|k_build_range|rocprim" tr traffic ;;
     parse) run pytest_parse 600 python -u -m pytest tests/test_gpu_parse.py -x -v --timeout 120 --timeout-method thread ;;
@@ -59,6 +59,8 @@ for step in "$@"; do
     newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_parity.py -k "empty or device_resident" -x -v --timeout 120 --timeout-method thread ;;
     k1) run pytest_k1 600 python -u -m pytest tests/test_gpu_parse.py -k "-8] or -24] or -40] or one_read" -x -v --timeout 300 --timeout-method thread && run ab_k1 600 python -u tools/ab_k3.py --alt --steps 16 --tune base --tune K1=8 --tune K1=24 --tune K1=40 --tune K1=72 ;;
     k1prof) run k1_prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_k1 -o run --output-format csv -- python -u tools/ab_k3.py --alt --steps 6 --tune base --tune K1=8 --tune K1=24 ;;
+    benchfull) run bench_full 900 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    c5pmc) for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_IDX_ACTIVE"; do i=$((${i:-0}+1)); run c5pmc_$i 300 timeout -s KILL 280 rocprofv3 --pmc $c --kernel-include-regex "k_cover_p|k_emit_work|k_route_scatter|k_route_emit|k_split|k_build_range|k_span_sum|k_emit" -d gpurun_out/c5pmc_$i -o pmc --output-format csv -- python -u tools/c5_probe.py stream routed reps=2; done ;;
     benchc5q) run bench_c5q 600 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-cli --no-concurrent ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

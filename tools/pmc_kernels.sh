@@ -14,7 +14,7 @@ for c in "FETCH_SIZE" "WRITE_SIZE" \
          "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_IDX_ACTIVE"; do
   i=$((i+1))
   if [ "$only" = traffic ] && [ $i -gt 2 ]; then break; fi
-  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex "$re" -d gpurun_out/pmc_${tag}_$i -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange --no-concurrent > gpurun_out/pmc_${tag}_$i.log 2>&1
+  timeout -s KILL 180 rocprofv3 --pmc $c --kernel-include-regex "$re" -d gpurun_out/pmc_${tag}_$i -o pmc --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-window --no-cli --no-exchange --no-concurrent --no-c5 > gpurun_out/pmc_${tag}_$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi
 done
