@@ -3249,6 +3249,8 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   c.n_records_a = a.total;
   if (hold) {                                       // the records stay in their regions for their owners
     const unsigned long long* h = c.h_pin.as<unsigned long long>();   // (stageA_read's copy of the cursors)
+    const unsigned* hf = reinterpret_cast<const unsigned*>(c.h_pin.as<uint8_t>() + 8 * CSTRIDE * NREG);   // (flags)
+    c.work_items = (uint64_t)hf[F_WORK_ITEMS] | ((uint64_t)hf[F_WORK_ITEMS + 1] << 32);
     c.route_reg.assign(NREG, 0);
     for (int r = 0; r < NREG; ++r) c.route_reg[r] = std::min<uint64_t>(h[CSTRIDE * r], c.capA);
     c.route_total = a.total;
