@@ -1995,7 +1995,16 @@ k_route_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsi
       hh[t] = 0;
       mm[t] = 0;
       if (i < n) {
-        const Slot s = e[i];
+        Slot s;
+        if (PG_EXP_BITS & (1 << 29)) {                          // (experiment: non-temporal loads)
+          typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+          const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(e + i));
+          s.key1 = v.x;
+          s.mask = (uint32_t)v.y;
+          s.aux = (uint32_t)(v.y >> 32);
+        } else {
+          s = e[i];
+        }
         acc += row_check(s.key1, (uint64_t)s.mask | ((uint64_t)s.aux << 32));
         if (s.mask) { hh[t] = T.rot ? T.rotk(s.key1, T.rot) : s.key1; mm[t] = s.mask & (uint32_t)MW_MASK; ++live; }
       }
@@ -2063,6 +2072,10 @@ __device__ __forceinline__ uint64_t part_at(const Recs& I, uint32_t p, const uns
 // 0.153 vs 0.161-0.162 ms; 2048 or 8192 per round: 0.173-0.196 ms), and at
 // 4 waves per SIMD (the occupancy the LDS allows) the 12 records per thread
 // stay in registers: 0.138-0.139 ms (profiles/r05_ab_split_geometry.log).
+// The records are read once, with non-temporal loads: the L2 then keeps the
+// output runs' partial lines instead of the input stream (C3 split 0.126 vs
+// 0.148 ms under rocprofv3; non-temporal stores: 0.210, both: 0.190 -
+// profiles/r06_ab_range_split.log).
 #ifndef PG_SPLIT_SR
 #define PG_SPLIT_SR 12
 #endif
@@ -2097,8 +2110,13 @@ k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t s
 #pragma unroll
     for (int e = 0; e < SR; ++e) {
       const uint32_t i = (uint32_t)e * SB + threadIdx.x;
-      key[e] = i < cnt ? I.key[in0 + i] : 0ull;
-      mw[e] = i < cnt ? I.mw[in0 + i] : 0u;
+      if (!(PG_EXP_BITS & (1 << 25))) {                         // (experiment build: plain loads)
+        key[e] = i < cnt ? __builtin_nontemporal_load(I.key + in0 + i) : 0ull;
+        mw[e] = i < cnt ? __builtin_nontemporal_load(I.mw + in0 + i) : 0u;
+      } else {
+        key[e] = i < cnt ? I.key[in0 + i] : 0ull;
+        mw[e] = i < cnt ? I.mw[in0 + i] : 0u;
+      }
     }
     __syncthreads();
 #pragma unroll
@@ -2152,8 +2170,13 @@ k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t s
       const unsigned long long pos = s_base[b] + (i - s_pos[b]);
       if (pos < O.cap) {
         const uint64_t at = ((uint64_t)p * nb + b) * O.cap + pos;
-        O.key[at] = kk;
-        O.mw[at] = s_mw[i];
+        if (PG_EXP_BITS & (1 << 24)) {                          // (experiment: non-temporal stores)
+          __builtin_nontemporal_store(kk, O.key + at);
+          __builtin_nontemporal_store(s_mw[i], O.mw + at);
+        } else {
+          O.key[at] = kk;
+          O.mw[at] = s_mw[i];
+        }
       } else {
         atomicOr(flags + 4, F_SPLIT_OVER);
       }
@@ -2204,7 +2227,10 @@ __device__ __forceinline__ uint32_t member_bits(uint32_t m) {   // bit0: A membe
 // a key whose bucket is full: the LDS overflow set (rare: out of line)
 __device__ __forceinline__ void range_or_ovl(unsigned long long* OK, uint32_t* OM, const TableView& T, uint64_t h,
                                           uint32_t m, unsigned* flags) {
-  uint32_t s = (uint32_t)(fmix64(h) >> 40) & (OVL - 1);
+  // (h is a permuted key: its low bits, below the bucket bits, are as good a
+  // start as a hash of it - C3 range 0.313 vs 0.318 ms with fmix64)
+  uint32_t s = (PG_EXP_BITS & (1 << 14)) ? (uint32_t)(fmix64(h) >> 40) & (OVL - 1)   // (experiment build)
+                                        : (uint32_t)(h >> 7) & (OVL - 1);
   for (int pr = 0; pr < OVL; ++pr) {
     const unsigned long long o2 = atomicCAS(&OK[s], 0ull, h + 1ull);
     if (o2 == 0ull || o2 == h + 1ull) {
@@ -2230,6 +2256,7 @@ __device__ __forceinline__ void range_or(unsigned long long* W, unsigned long lo
     if ((old & m) != m) atomicOr(w, (unsigned long long)m);
     return;
   }
+  if (PG_EXP_BITS & (1 << 13)) return;                         // (experiment: first word only - wrong keys)
   old = atomicCAS(w + 1, 0ull, mine);
   if (old == 0ull) return;
   if ((old >> MW_BITS) == q) {
@@ -2277,8 +2304,13 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       const unsigned long long* kp = I.key + pb + e * RB_T;
       const uint32_t* mp = I.mw + pb + e * RB_T;
       const bool ok = (uint32_t)(e * RB_T) + threadIdx.x < nn;
-      h[e] = ok ? kp[threadIdx.x] : 0ull;
-      m[e] = ok ? mp[threadIdx.x] : 0u;
+      if (PG_EXP_BITS & (1 << 22)) {                            // (experiment: non-temporal record loads)
+        h[e] = ok ? __builtin_nontemporal_load(kp + threadIdx.x) : 0ull;
+        m[e] = ok ? __builtin_nontemporal_load(mp + threadIdx.x) : 0u;
+      } else {
+        h[e] = ok ? kp[threadIdx.x] : 0ull;
+        m[e] = ok ? mp[threadIdx.x] : 0u;
+      }
     }
   };
   uint64_t n_cur = f < nparts ? part_count(I, f, z) : 0;
@@ -2333,17 +2365,36 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
     if (!(PG_EXP_BITS & 4)) load(f + G, n_nxt, nh, nm);       // in flight during this partition
     unsigned long long n_nn = f + 2 * G < nparts ? I.cursor[CSTRIDE * (uint64_t)(f + 2 * G) + z] : 0ull;  // (raw)
 #pragma unroll
-    for (int e = 0; e < RB_R; ++e)
+    for (int e = 0; e < RB_R; ++e) {
+      if (PG_EXP_BITS & (1 << 26)) {                            // (experiment: loads consumed, no merge)
+        created += (uint32_t)(ch[e] ^ cm[e]) & 1u;
+        continue;
+      }
+      if (PG_EXP_BITS & (1 << 27)) {                            // (experiment: plain LDS stores, no atomics)
+        if (cm[e]) W[2 * ((uint32_t)(ch[e] >> T.qbits) & (rng - 1))] = ((ch[e] & qmask) << MW_BITS) | cm[e];
+        continue;
+      }
       if (cm[e] && !(PG_EXP_BITS & 2))
         range_or(W, OK, OM, T, ch[e], cm[e], (uint32_t)(ch[e] >> T.qbits) & (rng - 1), qmask, flags);
+    }
+    // (Measured and dropped, profiles/r06_ab_range_split.log: batches of
+    // records with every first-word CAS of a batch in flight at once, then the
+    // second-word CASes - 0.331 ms with 4 per batch (a spill), 0.318 with 2,
+    // 0.409 with 8 (spills), against 0.317 record by record; and rounds in
+    // which each lane takes its next record still to do, selected out of its
+    // registers, so that a path runs as often as the busiest lane needs it
+    // rather than once per record - 0.364-0.372 (spills: the kernel is at its
+    // 128-VGPR budget).)
     for (uint64_t r = (uint64_t)RB_T * RB_R + threadIdx.x; r < n_cur; r += RB_T) {   // rare: a large partition
       const unsigned long long h = I.key[(uint64_t)f * I.cap + r];
       range_or(W, OK, OM, T, h, I.mw[(uint64_t)f * I.cap + r], (uint32_t)(h >> T.qbits) & (rng - 1), qmask, flags);
     }
     __syncthreads();
-    wait_vm();                                                   // the prefetch landed under the merge
-    asm volatile("" : "+v"(n_nn));
-    n_nn = n_nn < I.cap ? n_nn : I.cap;
+    if (!(PG_EXP_BITS & (1 << 28))) {
+      wait_vm();                                                 // the prefetch landed under the merge
+      asm volatile("" : "+v"(n_nn));
+      n_nn = n_nn < I.cap ? n_nn : I.cap;
+    }
     // the LDS overflow set first (its HBM probes wait on vmcnt: before the
     // range's stores, not behind them), then the range out whole; counts;
     // members queued; LDS zeroed
@@ -2366,10 +2417,21 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       const bool live = i < rng;
       const unsigned long long x = live ? W[2 * i] : 0ull, y = live ? W[2 * i + 1] : 0ull;
       if (live) {
-        if (!(PG_EXP_BITS & 1)) *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
-        W[2 * i] = 0ull;
-        W[2 * i + 1] = 0ull;
+        if (PG_EXP_BITS & (1 << 21)) {                          // (experiment: non-temporal table stores)
+          typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+          u64x2 v;
+          v.x = x;
+          v.y = y;
+          __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(T.prim + 2 * (b0 + i)));
+        } else if (!(PG_EXP_BITS & 1)) {
+          *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
+        }
+        if (!(PG_EXP_BITS & (1 << 23))) {                       // (experiment: no LDS zeroing - wrong keys)
+          W[2 * i] = 0ull;
+          W[2 * i + 1] = 0ull;
+        }
       }
+      if (PG_EXP_BITS & (1 << 16)) continue;                    // (experiment: no counts, no rdBG members)
       const uint32_t mx = (uint32_t)(x & MW_MASK), my = (uint32_t)(y & MW_MASK);
       created += (x ? 1u : 0u) + (y ? 1u : 0u);
       ndbg += ((mx >> 12) & 1u) + ((mx >> 25) & 1u) + ((my >> 12) & 1u) + ((my >> 25) & 1u);
@@ -2378,6 +2440,11 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
         push(((b0 + i) << T.qbits) | (x >> MW_BITS), bx);
         push(((b0 + i) << T.qbits) | (y >> MW_BITS), by);
       }
+    }
+    if (PG_EXP_BITS & (1 << 28)) {                              // (experiment: the prefetch waited for here)
+      wait_vm();
+      asm volatile("" : "+v"(n_nn));
+      n_nn = n_nn < I.cap ? n_nn : I.cap;
     }
     __syncthreads();
     if (PG_EXP_BITS & 4) load(f + G, n_nxt, nh, nm);
@@ -3298,8 +3365,15 @@ __global__ void __launch_bounds__(256) k_route_scatter(const unsigned long long*
   const uint64_t o0 = roff[r], nr = roff[r + 1] - o0;
   unsigned long long acc = 0ull;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nr; i += (uint64_t)gridDim.x * 256ull) {
-    const unsigned long long h = key[(uint64_t)r * cap + i];
-    const uint32_t m = mw[(uint64_t)r * cap + i];
+    unsigned long long h;
+    uint32_t m;
+    if (PG_EXP_BITS & (1 << 29)) {                              // (experiment: non-temporal loads)
+      h = __builtin_nontemporal_load(key + (uint64_t)r * cap + i);
+      m = __builtin_nontemporal_load(mw + (uint64_t)r * cap + i);
+    } else {
+      h = key[(uint64_t)r * cap + i];
+      m = mw[(uint64_t)r * cap + i];
+    }
     out[o0 + i] = Slot{h, m, 0u};
     acc += row_check(h, (uint64_t)m);
   }
