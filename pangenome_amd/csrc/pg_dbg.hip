@@ -2072,10 +2072,8 @@ __device__ __forceinline__ uint64_t part_at(const Recs& I, uint32_t p, const uns
 // 0.153 vs 0.161-0.162 ms; 2048 or 8192 per round: 0.173-0.196 ms), and at
 // 4 waves per SIMD (the occupancy the LDS allows) the 12 records per thread
 // stay in registers: 0.138-0.139 ms (profiles/r05_ab_split_geometry.log).
-// The records are read once, with non-temporal loads: the L2 then keeps the
-// output runs' partial lines instead of the input stream (C3 split 0.126 vs
-// 0.148 ms under rocprofv3; non-temporal stores: 0.210, both: 0.190 -
-// profiles/r06_ab_range_split.log).
+// NT: the records are read with non-temporal loads (SPLIT_NT_MAX below;
+// non-temporal stores measured slower: C3 0.210 ms, both 0.190).
 #ifndef PG_SPLIT_SR
 #define PG_SPLIT_SR 12
 #endif
@@ -2088,6 +2086,12 @@ constexpr int SMAXB = 1 << SPLIT_BITS;
 // start (NULL: 0): per input region, the records below it are already split
 // (pg_build_host's early split); a block loops over its region's records in
 // steps of bpr * SCH.
+// Non-temporal record loads measured faster for C3 (24 M records, one pass:
+// 0.148 -> 0.127 ms) and slower for the C5 shard's sub-logs (0.94 G records,
+// two passes: 38.8 -> 42.4 ms per pass; profiles/r06_ab_range_split.log), so
+// a build's passes use them below SPLIT_NT_MAX records.
+constexpr uint64_t SPLIT_NT_MAX = 1ull << 28;
+template <bool NT>
 __global__ void __launch_bounds__(SB, 4)
 k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t shift, uint32_t nb, uint32_t bpr,
         unsigned* __restrict__ flags) {
@@ -2110,7 +2114,7 @@ k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t s
 #pragma unroll
     for (int e = 0; e < SR; ++e) {
       const uint32_t i = (uint32_t)e * SB + threadIdx.x;
-      if (!(PG_EXP_BITS & (1 << 25))) {                         // (experiment build: plain loads)
+      if (NT) {
         key[e] = i < cnt ? __builtin_nontemporal_load(I.key + in0 + i) : 0ull;
         mw[e] = i < cnt ? __builtin_nontemporal_load(I.mw + in0 + i) : 0u;
       } else {
@@ -2304,7 +2308,8 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       const unsigned long long* kp = I.key + pb + e * RB_T;
       const uint32_t* mp = I.mw + pb + e * RB_T;
       const bool ok = (uint32_t)(e * RB_T) + threadIdx.x < nn;
-      if (PG_EXP_BITS & (1 << 22)) {                            // (experiment: non-temporal record loads)
+      // (non-temporal: read once; C3 range 0.300 vs 0.319 ms with plain loads)
+      if (!(PG_EXP_BITS & (1 << 22))) {                         // (experiment build: plain loads)
         h[e] = ok ? __builtin_nontemporal_load(kp + threadIdx.x) : 0ull;
         m[e] = ok ? __builtin_nontemporal_load(mp + threadIdx.x) : 0u;
       } else {
@@ -2986,7 +2991,8 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
         continue;
       }
       if (l.nreg * l.bpr >= (1ull << 31)) throw Error(-22, "build: split grid too large");
-      hipLaunchKernelGGL(k_split, dim3((unsigned)(l.nreg * l.bpr)), dim3(SB), 0, c.stream, in, out,
+      hipLaunchKernelGGL(a.total < SPLIT_NT_MAX ? k_split<true> : k_split<false>,
+                         dim3((unsigned)(l.nreg * l.bpr)), dim3(SB), 0, c.stream, in, out,
                          (const unsigned long long*)nullptr, (uint32_t)(kb - l.L - l.S), nb, (uint32_t)l.bpr,
                          c.flags.as<unsigned>());
       PG_HIP(hipGetLastError());
@@ -3728,7 +3734,8 @@ void build_host(Ctx& c, const uint8_t* h_src, uint64_t n, int rc0) {
                   c.capA, 8};
     const Recs out{c.recS_key[0].as<unsigned long long>(), c.recS_mw[0].as<uint32_t>(),
                    c.ctrS.as<unsigned long long>(), pre.cap, 1};
-    hipLaunchKernelGGL(k_split, dim3((unsigned)(NREG * pre_bpr)), dim3(SB), 0, c.stream, in, out,
+    hipLaunchKernelGGL(k_split<true>, dim3((unsigned)(NREG * pre_bpr)), dim3(SB),   // (chunks of a pg_build_host)
+                       0, c.stream, in, out,
                        c.snapA.as<unsigned long long>(), (uint32_t)(c.kb - c.cbits - (int)pre.S), 1u << pre.S, pre_bpr,
                        c.flags.as<unsigned>());
     PG_HIP(hipGetLastError());

@@ -50,7 +50,19 @@ constexpr int WSTEP = 64 * 16;                    // 1 KiB per wave step (16 B p
 constexpr int WSTEPS = 16;
 constexpr uint64_t WSPAN = (uint64_t)WSTEP * WSTEPS;   // 16 KiB per wave
 // load the 16 bytes at p (16-byte aligned); bytes at or past n read as 0
+// The FASTA is read with non-temporal loads (it is read twice, but 508 MB of
+// C3 does not stay cached between the passes): C3 k_span_sum 0.164 -> 0.100
+// ms, k_emit 0.194 either way (rocprofv3 medians, profiles/r06_ab_range_split.log)
+#ifndef PG_K1_NT
+#define PG_K1_NT 3                                     // bit 0: span pass, bit 1: emission (experiment builds)
+#endif
+template <bool NT = false>
 __device__ __forceinline__ uint4 load16(const uint8_t* buf, uint64_t p, uint64_t n) {
+  if (NT && p + 16 <= n) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
+    return make_uint4(x.x, x.y, x.z, x.w);
+  }
   if (p + 16 <= n) return *reinterpret_cast<const uint4*>(buf + p);
   uint32_t w[4] = {0, 0, 0, 0};
   for (int j = 0; j < 16; ++j)
@@ -206,12 +218,13 @@ struct FnThen {                                     // a, then b (associative, n
 };
 
 // all of a wave's span loads are issued before the first step is processed
+template <bool NT = false>
 __device__ __forceinline__ void load_span(const uint8_t* buf, uint64_t p0, uint64_t n, int lane,
                                           uint4 (&v)[WSTEPS]) {
 #pragma unroll
   for (int s = 0; s < WSTEPS; ++s) {
     const uint64_t p = p0 + (uint64_t)s * WSTEP + (uint64_t)lane * 16;
-    v[s] = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+    v[s] = p < n ? load16<NT>(buf, p, n) : make_uint4(0, 0, 0, 0);
   }
 }
 
@@ -462,7 +475,7 @@ __global__ void __launch_bounds__(PBLOCK) k_span_sum(const uint8_t* __restrict__
   if (span >= nspan) return;                                  // wave-uniform
   const uint64_t p0 = span * WSPAN;
   uint4 v[WSTEPS];
-  load_span(buf, p0, n, lane, v);
+  load_span<(PG_K1_NT & 1) != 0>(buf, p0, n, lane, v);
   const Fn f = span_fn(v, n, p0, lane, p0 == 0 ? 1u : (buf[p0 - 1] == 10 ? 1u : 0u));
   if (lane == 0) out[span] = f;
 }
@@ -559,9 +572,10 @@ __device__ __forceinline__ void emit_span(const uint8_t* __restrict__ buf, uint6
   // one step of prefetch: occupancy (LDS round trip per step) beats depth here
   // (PF = 2: two steps in flight ahead, PG_TUNE_K1 bit 1)
   uint64_t p = p0 + (uint64_t)lane * 16;
-  uint4 v = p < n ? load16(buf, p, n) : make_uint4(0, 0, 0, 0);
+  constexpr bool NT = (PG_K1_NT & 2) != 0;
+  uint4 v = p < n ? load16<NT>(buf, p, n) : make_uint4(0, 0, 0, 0);
   uint4 v2 = make_uint4(0, 0, 0, 0);
-  if (PF == 2 && p + WSTEP < n) v2 = load16(buf, p + WSTEP, n);
+  if (PF == 2 && p + WSTEP < n) v2 = load16<NT>(buf, p + WSTEP, n);
   for (int s = 0; s < WSTEPS; ++s) {
     if (p0 + (uint64_t)s * WSTEP >= n) break;                 // wave-uniform
     const uint64_t pn = p + WSTEP;
@@ -569,9 +583,9 @@ __device__ __forceinline__ void emit_span(const uint8_t* __restrict__ buf, uint6
     if (PF == 2) {
       vn = v2;
       const uint64_t pnn = pn + WSTEP;
-      v2 = (s + 2 < WSTEPS && pnn < n) ? load16(buf, pnn, n) : make_uint4(0, 0, 0, 0);
+      v2 = (s + 2 < WSTEPS && pnn < n) ? load16<NT>(buf, pnn, n) : make_uint4(0, 0, 0, 0);
     } else {
-      vn = (s + 1 < WSTEPS && pn < n) ? load16(buf, pn, n) : make_uint4(0, 0, 0, 0);
+      vn = (s + 1 < WSTEPS && pn < n) ? load16<NT>(buf, pn, n) : make_uint4(0, 0, 0, 0);
     }
     uint32_t ctot;
     // Fast step (wave-uniform): in-state 0, every byte below n - 1, no '>',
