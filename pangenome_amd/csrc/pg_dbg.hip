@@ -1174,6 +1174,7 @@ struct Drifts2 {
 __device__ __forceinline__ uint32_t p2_word(const uint32_t* p2, long long i, uint64_t n_p2) {
   return (i >= 0 && (uint64_t)i < n_p2) ? p2[i] : 0u;
 }
+
 // candidates ib = 16 w .. 16 w + 15 (s_ref base indices) of the anchor (A0, A1)
 // within [lo, hi]: its 32 bases against the reference's 32 from ib
 __device__ __forceinline__ void drift_task_p(uint32_t A0, uint32_t A1, const uint32_t* R, int ibhi, int lo, int hi,
