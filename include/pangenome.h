@@ -208,14 +208,20 @@ int pg_dbg_merge_check(const pg_ctx* ctx, uint64_t* rows, uint64_t* sum);
  * counts[nparts] = records per owner, *sentinel = the n<k sentinel seen. */
 int pg_route_stage_a(pg_ctx* ctx, const uint8_t* rec_flags, int extra_empty, int rc0, int nparts, uint64_t* counts,
                      int* sentinel);
-/* The held records as 16-byte rows {h, mask word, 0} grouped by owner into
- * d_out (device, capacity out_cap rows; owner o's run after owner o-1's);
- * sums[nparts] = each run's integrity sum (as pg_dbg_partition_sums). */
+/* The held records as 12-byte rows {h as two little-endian 32-bit words,
+ * mask word} grouped by owner into d_out (device, 4-byte aligned, capacity
+ * out_cap rows; owner o's run after owner o-1's); sums[nparts] = each run's
+ * integrity sum: the hash of the 16-byte {h, mask word, 0} form, as
+ * pg_dbg_partition_sums (round 6: 16-byte rows before, a quarter more bytes
+ * on the wire). */
 int pg_route_scatter(pg_ctx* ctx, int nparts, void* d_out, uint64_t out_cap, uint64_t* sums);
+/* pg_rows_checksum over 12-byte routed rows (the receiver's check of what
+ * pg_route_scatter's sums say was sent). */
+int pg_route_rows_checksum(pg_ctx* ctx, const void* d_rows, const uint64_t* seg_off, uint64_t nseg, uint64_t* sums);
 /* World 1: stages B and C on the held records where they lie (this rank
  * owns them all) - the dBG and rdBG of pg_build_dbg, no copy. */
 int pg_route_finish(pg_ctx* ctx, uint64_t* n_rdbg, pg_stats* stats);
-/* Owner `part` of `nparts`: a fresh table from the n received rows (every
+/* Owner `part` of `nparts`: a fresh table from the n received 12-byte rows (every
  * rank's run for this owner, device pointer), stages A (re-binning), B and
  * C; sentinel != 0 adds the n<k key.  pg_dbg_merge_check reports what it
  * read.  The table's hash domain is h rotated left by log2(nparts) bits:

@@ -81,6 +81,7 @@ SIGNATURES = {
     "pg_dbg_merge_check": (C.c_int, [_P, _U64P, _U64P]),
     "pg_route_stage_a": (C.c_int, [_P, _P, C.c_int, C.c_int, C.c_int, _P, C.POINTER(C.c_int)]),
     "pg_route_scatter": (C.c_int, [_P, C.c_int, _P, C.c_uint64, _P]),
+    "pg_route_rows_checksum": (C.c_int, [_P, _P, _P, C.c_uint64, _P]),
     "pg_route_finish": (C.c_int, [_P, _U64P, _SP]),
     "pg_route_merge": (C.c_int, [_P, _P, C.c_uint64, C.c_int, C.c_int, _U64P, _SP]),
     "pg_route_merge_segs": (C.c_int, [_P, C.POINTER(C.c_void_p), _P, C.c_int, C.c_int, C.c_int, _U64P, _SP]),
@@ -364,6 +365,14 @@ class Context:
                                         max(off.shape[0] - 1, 0), ptr(sums)), "pg_rows_checksum")
         return sums[:max(off.shape[0] - 1, 0)]
 
+    def route_rows_checksum(self, d_rows: int, seg_off):
+        """rows_checksum over 12-byte routed rows (pg_route_scatter's layout)."""
+        off = np.ascontiguousarray(seg_off, dtype=np.uint64)
+        sums = np.zeros(max(off.shape[0] - 1, 1), np.uint64)
+        check(self.lib.pg_route_rows_checksum(self.h, C.c_void_p(d_rows) if d_rows else None, ptr(off),
+                                              max(off.shape[0] - 1, 0), ptr(sums)), "pg_route_rows_checksum")
+        return sums[:max(off.shape[0] - 1, 0)]
+
     def merge_check(self):
         """(non-empty records, row_check sum) the last merge read."""
         rows, s = C.c_uint64(), C.c_uint64()
@@ -382,7 +391,7 @@ class Context:
         return counts, bool(sent.value)
 
     def route_scatter(self, nparts: int, d_out: int, out_cap: int):
-        """The held records as 16-byte rows grouped by owner at d_out; their
+        """The held records as 12-byte rows grouped by owner at d_out; their
         integrity sums per owner (uint64[nparts])."""
         sums = np.zeros(nparts, np.uint64)
         check(self.lib.pg_route_scatter(self.h, int(nparts), C.c_void_p(d_out) if d_out else None, int(out_cap),

@@ -499,6 +499,16 @@ int pg_rows_checksum(pg_ctx* x, const void* d_rows, const uint64_t* seg_off, uin
   });
 }
 
+int pg_route_rows_checksum(pg_ctx* x, const void* d_rows, const uint64_t* seg_off, uint64_t nseg, uint64_t* sums) {
+  return guard([&] {
+    if (!x || !seg_off || (nseg && !sums) || (!d_rows && nseg && seg_off[nseg] > seg_off[0]))
+      throw pg::Error(PG_EINVAL, "pg_route_rows_checksum: bad arguments");
+    if (reinterpret_cast<uintptr_t>(d_rows) & 3u) throw pg::Error(PG_EINVAL, "pg_route_rows_checksum: rows not 4-byte aligned");
+    PG_HIP(hipSetDevice(x->c.device));
+    pg::rows_checksum(x->c, d_rows, seg_off, nseg, sums, true);
+  });
+}
+
 static int route_lg(int nparts, const char* what) {
   if (nparts < 1 || nparts > 64 || (nparts & (nparts - 1)))
     throw pg::Error(PG_EINVAL, std::string(what) + ": nparts must be a power of two in [1, 64]");

@@ -78,6 +78,13 @@ struct alignas(16) Slot {
   unsigned int mask;   // 26-bit mask word
   unsigned int aux;
 };
+// A routed stage A record on the wire (pg_route_scatter / pg_route_merge):
+// h (low word, high word) and the 26-bit mask word, 12 bytes, 4-byte aligned.
+// Its integrity hash is row_check(h, mask word), the hash of the 16-byte
+// {h, mask word, 0} form.
+struct Row12 {
+  unsigned int w[3];
+};
 
 // Integrity check of one 16-byte exchange record (words w0 = key1, w1 = mask |
 // aux << 32).  Sums of it (mod 2^64) over a run of records are order-free, so

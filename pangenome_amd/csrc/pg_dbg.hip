@@ -1975,11 +1975,11 @@ k_slots_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsi
   }
 }
 
-// Routed stage A records {h, mask word} (pg_route_merge) into this owner's
+// Routed stage A records (12-byte rows, pg_route_merge) into this owner's
 // regions: h rotated into the owner domain (T.rot), with the same checksum
 // slots as k_slots_emit.
 __global__ void __launch_bounds__(IBLOCK)
-k_route_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsigned long long* __restrict__ chk) {
+k_route_emit(const Row12* __restrict__ e, uint64_t n, TableView T, BinOut O, unsigned long long* __restrict__ chk) {
   __shared__ EmitLds<1> s_emit;
   __shared__ unsigned long long st_key[EST];
   __shared__ uint32_t st_mw[EST];
@@ -1996,18 +1996,10 @@ k_route_emit(const Slot* __restrict__ e, uint64_t n, TableView T, BinOut O, unsi
       hh[t] = 0;
       mm[t] = 0;
       if (i < n) {
-        Slot s;
-        if (PG_EXP_BITS & (1 << 29)) {                          // (experiment: non-temporal loads)
-          typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-          const u64x2 v = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(e + i));
-          s.key1 = v.x;
-          s.mask = (uint32_t)v.y;
-          s.aux = (uint32_t)(v.y >> 32);
-        } else {
-          s = e[i];
-        }
-        acc += row_check(s.key1, (uint64_t)s.mask | ((uint64_t)s.aux << 32));
-        if (s.mask) { hh[t] = T.rot ? T.rotk(s.key1, T.rot) : s.key1; mm[t] = s.mask & (uint32_t)MW_MASK; ++live; }
+        const Row12 r = e[i];
+        const uint64_t h = (uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32);
+        acc += row_check(h, (uint64_t)r.w[2]);
+        if (r.w[2]) { hh[t] = T.rot ? T.rotk(h, T.rot) : h; mm[t] = r.w[2] & (uint32_t)MW_MASK; ++live; }
       }
     }
     block_emit<4>(O, hh, mm, s_emit, st_key, st_mw);
@@ -2631,15 +2623,21 @@ k_part_scatter(TableView T, uint64_t nw, uint64_t ntot, int nparts, unsigned lon
 // sums[s * CSPR + block % CSPR].
 constexpr int RS_SEG = 32;
 struct SegOff { unsigned long long o[RS_SEG + 1]; };
-__global__ void __launch_bounds__(256) k_rows_sum(const Slot* __restrict__ rows, SegOff so,
+__device__ __forceinline__ unsigned long long row_hash(const Slot& r) {
+  return row_check(r.key1, (uint64_t)r.mask | ((uint64_t)r.aux << 32));
+}
+__device__ __forceinline__ unsigned long long row_hash(const Row12& r) {
+  return row_check((uint64_t)r.w[0] | ((uint64_t)r.w[1] << 32), (uint64_t)r.w[2]);
+}
+template <class Row>
+__global__ void __launch_bounds__(256) k_rows_sum(const Row* __restrict__ rows, SegOff so,
                                                   unsigned long long* __restrict__ sums) {
   __shared__ unsigned long long s_red[4];
   const uint32_t s = blockIdx.y;
   const uint64_t lo = so.o[s], hi = so.o[s + 1];
   unsigned long long acc = 0ull;
   for (uint64_t i = lo + blockIdx.x * 256ull + threadIdx.x; i < hi; i += (uint64_t)gridDim.x * 256ull) {
-    const Slot r = rows[i];
-    acc += row_check(r.key1, (uint64_t)r.mask | ((uint64_t)r.aux << 32));
+    acc += row_hash(rows[i]);
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
   if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = acc;
@@ -3358,14 +3356,14 @@ void route_counts(Ctx& c, int lg, uint64_t* counts) {
 }
 
 // rows of region blockIdx.y (records [0, roff[r+1] - roff[r]) of it) to
-// out + roff[r] as 16-byte rows {h, mask word, 0}, and the block's row_check
+// out + roff[r] as 12-byte rows {h, mask word} (Row12), and the block's row_check
 // sum as a plain store to part[blockIdx.y * gridDim.x + blockIdx.x] (the
 // host adds them per owner: one atomic per block on a few owner words
 // serialised ~100 K atomics, 0.68 ms at world 1 on C3)
 constexpr int RS_ROWS = 16;                    // rows per thread and block pass
 __global__ void __launch_bounds__(256) k_route_scatter(const unsigned long long* __restrict__ key,
                                                        const uint32_t* __restrict__ mw, uint64_t cap,
-                                                       const unsigned long long* __restrict__ roff, Slot* __restrict__ out,
+                                                       const unsigned long long* __restrict__ roff, Row12* __restrict__ out,
                                                        unsigned long long* __restrict__ part) {
   __shared__ unsigned long long s_red[4];
   const uint32_t r = blockIdx.y;
@@ -3381,7 +3379,7 @@ __global__ void __launch_bounds__(256) k_route_scatter(const unsigned long long*
       h = key[(uint64_t)r * cap + i];
       m = mw[(uint64_t)r * cap + i];
     }
-    out[o0 + i] = Slot{h, m, 0u};
+    out[o0 + i] = Row12{{(uint32_t)h, (uint32_t)(h >> 32), m}};
     acc += row_check(h, (uint64_t)m);
   }
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
@@ -3415,7 +3413,7 @@ void route_scatter(Ctx& c, int lg, void* d_out, uint64_t out_cap, uint64_t* sums
   for (int o = 0; o < np; ++o) sums[o] = 0;
   if (tot) {
     hipLaunchKernelGGL(k_route_scatter, dim3(gx, NREG), dim3(256), 0, c.stream, c.recA_key.as<unsigned long long>(),
-                       c.recA_mw.as<uint32_t>(), c.capA, d, reinterpret_cast<Slot*>(d_out), d + NREG + 1);
+                       c.recA_mw.as<uint32_t>(), c.capA, d, reinterpret_cast<Row12*>(d_out), d + NREG + 1);
     PG_HIP(hipGetLastError());
     PG_HIP(hipMemcpyAsync(h + NREG + 1, d + NREG + 1, 8 * (size_t)NREG * gx, hipMemcpyDeviceToHost, c.stream));
   }
@@ -3580,7 +3578,7 @@ uint64_t partition_dbg(Ctx& c, int nparts, void* d_out, uint64_t out_cap, uint64
 
 // Sums of row_check over nseg segments of 16-byte records at d_rows
 // (segment s = records [off[s], off[s+1])), on the context's stream.
-void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums) {
+void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums, bool row12) {
   DevBuf& out = c.part_cnt;                             // (after the partition words)
   out.reserve(8 * (PCW_ROWS + RS_SEG * CSPR));
   auto* d = out.as<unsigned long long>() + PCW_ROWS;
@@ -3597,8 +3595,12 @@ void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nse
     }
     PG_HIP(hipMemsetAsync(d, 0, 8 * RS_SEG * CSPR, c.stream));
     if (mx) {
-      hipLaunchKernelGGL(k_rows_sum, dim3(grid_for(mx, 256, 2048), ns), dim3(256), 0, c.stream,
-                         reinterpret_cast<const Slot*>(d_rows), so, d);
+      if (row12)
+        hipLaunchKernelGGL(k_rows_sum<Row12>, dim3(grid_for(mx, 256, 2048), ns), dim3(256), 0, c.stream,
+                           reinterpret_cast<const Row12*>(d_rows), so, d);
+      else
+        hipLaunchKernelGGL(k_rows_sum<Slot>, dim3(grid_for(mx, 256, 2048), ns), dim3(256), 0, c.stream,
+                           reinterpret_cast<const Slot*>(d_rows), so, d);
       PG_HIP(hipGetLastError());
     }
     PG_HIP(hipMemcpyAsync(h, d, 8 * (size_t)ns * CSPR, hipMemcpyDeviceToHost, c.stream));
@@ -3613,8 +3615,8 @@ void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nse
 
 // OR-merge received exchange records into a fresh owner table (stage A from
 // the records, then stages B and C as a build).
-// rot >= 0 (pg_route_merge): the rows are routed stage A records {h, mask
-// word} of this owner, re-binned on h rotated left by rot bits.
+// rot >= 0 (pg_route_merge): the rows are routed stage A records (12-byte
+// Row12 {h, mask word}) of this owner, re-binned on h rotated left by rot bits.
 void merge_dbg(Ctx& c, const void* d_pairs, uint64_t n, uint64_t /*cap_hint*/, int sentinel, int rot) {
   merge_dbg_segs(c, &d_pairs, &n, 1, sentinel, rot);
 }
@@ -3643,9 +3645,14 @@ void merge_dbg_segs(Ctx& c, const void* const* segs, const uint64_t* ns, int nse
     if (sentinel) hipLaunchKernelGGL(k_set_flag, dim3(1), dim3(1), 0, c.stream, c.flags.as<unsigned>());
     for (int s = 0; s < nseg; ++s) {
       if (!ns[s]) continue;
-      hipLaunchKernelGGL(rot >= 0 ? k_route_emit : k_slots_emit, dim3(grid_for(ns[s], 4 * IBLOCK, 4096)), dim3(IBLOCK),
-                         0, c.stream, reinterpret_cast<const Slot*>(segs[s]), ns[s], c.tv, O,
-                         c.flags.as<unsigned long long>() + N_FLAGS / 2);
+      if (rot >= 0)
+        hipLaunchKernelGGL(k_route_emit, dim3(grid_for(ns[s], 4 * IBLOCK, 4096)), dim3(IBLOCK), 0, c.stream,
+                           reinterpret_cast<const Row12*>(segs[s]), ns[s], c.tv, O,
+                           c.flags.as<unsigned long long>() + N_FLAGS / 2);
+      else
+        hipLaunchKernelGGL(k_slots_emit, dim3(grid_for(ns[s], 4 * IBLOCK, 4096)), dim3(IBLOCK), 0, c.stream,
+                           reinterpret_cast<const Slot*>(segs[s]), ns[s], c.tv, O,
+                           c.flags.as<unsigned long long>() + N_FLAGS / 2);
       PG_HIP(hipGetLastError());
     }
     c.t1.stop(c.stream);

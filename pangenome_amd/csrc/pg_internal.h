@@ -377,7 +377,7 @@ void merge_dbg_segs(Ctx& c, const void* const* segs, const uint64_t* ns, int nse
 void route_counts(Ctx& c, int lg, uint64_t* counts);
 void route_scatter(Ctx& c, int lg, void* d_out, uint64_t out_cap, uint64_t* sums);
 void route_finish(Ctx& c);
-void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums);
+void rows_checksum(Ctx& c, const void* d_rows, const uint64_t* off, uint64_t nseg, uint64_t* sums, bool row12 = false);
 // pg_persist.hip
 struct PreEnt {                   // one staged oakht slot: oriented key, 12-bit mask, count
   unsigned long long key;

@@ -139,20 +139,28 @@ def _fmix64(k):
 
 
 def row_check_sum(rows) -> int:
-    """Sum mod 2^64 of row_check (pg_common.h) over (n, 2) int64 records on
-    the host: the CPU form of pg_rows_checksum."""
-    w = np.ascontiguousarray(np.asarray(rows)).reshape(-1, 2).view(np.uint64)
-    if w.shape[0] == 0:
+    """Sum mod 2^64 of row_check (pg_common.h) over records on the host: the
+    CPU form of pg_rows_checksum.  `rows`: 16-byte records as (n, 2) 64-bit
+    or (n, 4) 32-bit words, or 12-byte routed rows as (n, 3) 32-bit words
+    ({h low, h high, mask word}: the hash of {h, mask word, 0})."""
+    a = np.ascontiguousarray(np.asarray(rows))
+    if a.ndim == 2 and a.shape[1] == 3 and a.dtype.itemsize == 4:
+        u = a.view(np.uint32).astype(np.uint64)
+        w0, w1 = u[:, 0] | (u[:, 1] << np.uint64(32)), u[:, 2]
+    else:
+        w = a.reshape(-1).view(np.uint64).reshape(-1, 2)
+        w0, w1 = w[:, 0], w[:, 1]
+    if w0.shape[0] == 0:
         return 0
     with np.errstate(over="ignore"):
-        h = _fmix64(w[:, 0] ^ _fmix64(w[:, 1] ^ np.uint64(0x9E3779B97F4A7C15)))
+        h = _fmix64(w0 ^ _fmix64(w1 ^ np.uint64(0x9E3779B97F4A7C15)))
         return int(h.sum(dtype=np.uint64))
 
 
 def _seg_sums(shard, buf, offsets, device) -> list:
-    """row_check sums of segments [offsets[i], offsets[i+1]) of the (n, 2)
-    int64 tensor buf: on the device through the library, on the host with
-    numpy."""
+    """row_check sums of segments [offsets[i], offsets[i+1]) of the rows of
+    buf ((n, 4) int32 16-byte records, or (n, 3) int32 routed rows): on the
+    device through the library, on the host with numpy."""
     if len(offsets) < 2:
         return []
     if getattr(buf, "is_cuda", False):
@@ -170,8 +178,9 @@ def _poisoned(t):
 
 def _route(table, world: int, device, group=None, sentinel_local: bool = False, subparts: int = 1, tm=None,
            where: str = "", fail=None, defer=None):
-    """This rank's table -> owner runs of 16-byte records (pg_dbg_partition)
-    -> one all-to-all.  Every rank's run lengths and their integrity sums,
+    """This rank's table -> owner runs of records (pg_dbg_partition's 16-byte
+    records, or a _Routed table's 12-byte rows: table.row_words 32-bit words
+    per row) -> one all-to-all.  Every rank's run lengths and their integrity sums,
     with its n<k sentinel flag, go to every rank in one small all-gather: the
     whole (source, owner) matrix gives this rank's receive sizes, the largest
     peer message (the piece count of _all_to_all_rows), the global sentinel
@@ -183,13 +192,13 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     (record conservation), and every received (source, sub-log) run must
     carry the sum its sender computed while scattering it; a mismatch on any
     rank raises ExchangeIntegrityError on every rank (one MAX all-reduce of a
-    flag), naming `where`, the peer, the sub-log and the 512 MiB piece.
+    flag), naming `where`, the peer, the sub-log and the A2A_ROWS piece.
     `fail`: a failed check of this rank since the last collective (a
     message): it travels in the count matrix and every rank raises.
     `defer` (a dict): the received-run check skips its own all-reduce and
     leaves `bad` (this rank's mismatching runs) and `diagnose` (the
     collective that raises) for the caller's next all-reduce to carry.
-    Returns (the records this rank owns as an (n, 2) int64 tensor on
+    Returns (the records this rank owns as an (n, row_words) int32 tensor on
     `device`, the received counts per (source rank, sub-log) as a (world, P)
     array, their expected sums as a (world, P) array of Python ints, bytes
     sent to other ranks, whether any rank saw the sentinel).  `tm` (a dict)
@@ -198,6 +207,7 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     import torch
     import torch.distributed as dist
     P = subparts
+    W = getattr(table, "row_words", 4)
     stage, comm = _comm_device(device, group)
     rank = dist.get_rank(group)
     t0 = perf_counter()
@@ -207,7 +217,7 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     if n_ent is not None and total != n_ent and not fail:
         fail = ("%s: rank %d's partition holds %d records for a table of %d entries (stage: partition)"
                 % (where or "exchange", rank, total, n_ent))
-    send = _poisoned(torch.empty((max(total, 1), 2), dtype=torch.int64, device=device))
+    send = _poisoned(torch.empty((max(total, 1), W), dtype=torch.int32, device=device))
     sums = np.zeros(world * P, np.uint64)
     if total:
         _fence(device, table)
@@ -235,7 +245,7 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     alias = world == 1 and SELF_COPY and not stage
     # world 1: the rank's only run is its own, and the send buffer already
     # holds it where the receive would put it (no copy, no second buffer)
-    recv = send if alias else _poisoned(torch.empty((max(nrecv, 1), 2), dtype=torch.int64, device=comm))
+    recv = send if alias else _poisoned(torch.empty((max(nrecv, 1), W), dtype=torch.int32, device=comm))
     if alias:
         pass
     elif stage:
@@ -253,7 +263,7 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
     bad = [(s, p) for s in range(world) for p in range(P) if got[s * P + p] != int(want[s, p])]
     if defer is not None:
         # the caller's next all-reduce carries the check.  (The closure keeps
-        # the send buffer until the caller returns - one more buffer of 16 B
+        # the send buffer until the caller returns - one more buffer of 12 B
         # per sent record at the owner merge's peak, <= ~1 GB for C4-sized
         # shards - rather than summing its pieces up front on every exchange:
         # a pass over the whole buffer, ~0.1 ms on C3, for a failure path.)
@@ -276,7 +286,7 @@ def _route(table, world: int, device, group=None, sentinel_local: bool = False, 
         tm["all_to_all"] = tm.get("all_to_all", 0.0) + (t2 - t1)
         tm["rows"] = tm.get("rows", 0) + total
     want_l = [[int(want[s, p]) for p in range(P)] for s in range(world)]
-    return recv[:nrecv], rh, want_l, 16 * (total - int(counts[rank].sum())), bool(H[:, :, P].any())
+    return recv[:nrecv], rh, want_l, 4 * W * (total - int(counts[rank].sum())), bool(H[:, :, P].any())
 
 
 def _piece_count(ssplit, rsplit) -> int:
@@ -346,7 +356,7 @@ A2A_ROWS = 1 << 25
 
 
 def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None, big=None, self_copy=True):
-    """all_to_all of (n, 2) int64 rows in pieces of at most A2A_ROWS rows per
+    """all_to_all of rows (a 2-D tensor, any row width) in pieces of at most A2A_ROWS rows per
     peer (every rank runs the same number of pieces: the largest message of
     any rank decides; `big`, when the caller knows it, else one MAX
     all-reduce finds it).  Views of contiguous runs; the rank's own run is a
@@ -384,7 +394,8 @@ def _all_to_all_rows(recv, send, rsplit, ssplit, comm, group=None, big=None, sel
         if lists:
             dist.all_to_all(outs, ins, group=group)
         else:
-            tmp = torch.empty((max(1, sum(x.shape[0] for x in outs)), 2), dtype=recv.dtype, device=recv.device)
+            tmp = torch.empty((max(1, sum(x.shape[0] for x in outs)),) + tuple(recv.shape[1:]), dtype=recv.dtype,
+                              device=recv.device)
             n = sum(x.shape[0] for x in outs)
             dist.all_to_all_single(tmp[:n], torch.cat(ins), output_split_sizes=[x.shape[0] for x in outs],
                                    input_split_sizes=[x.shape[0] for x in ins], group=group)
@@ -486,6 +497,8 @@ class _Routed:
     the owner is the top bits of the record's h), its "merge" the owner's
     build from the received records (stages A, B, C once)."""
 
+    row_words = 3                                       # 12-byte rows {h, mask word} (pg_route_scatter)
+
     def __init__(self, shard, nparts: int, counts):
         self.sh, self.nparts, self.counts = shard, nparts, np.asarray(counts, np.uint64)
 
@@ -503,7 +516,7 @@ class _Routed:
         return int(self.counts.sum())
 
     def rows_checksum(self, d_rows, seg_off):
-        return self.sh.rows_checksum(d_rows, seg_off)
+        return self.sh.route_rows_checksum(d_rows, seg_off)
 
     @property
     def stream_wait(self):
@@ -671,7 +684,7 @@ def exchange_stream(shard, world: int, rank: int, device, chunks: list, n_record
             fail.append(f)
         del cat
         m = int(shard.partition(1)[0])
-        out = _poisoned(torch.empty((max(m, 1), 2), dtype=torch.int64, device=device))
+        out = _poisoned(torch.empty((max(m, 1), 4), dtype=torch.int32, device=device))
         if m:
             _fence(device, shard)
             shard.partition(1, out.data_ptr(), m)
@@ -809,7 +822,7 @@ def _stream_routed(shard, world: int, rank: int, device, chunks, n_records: int,
             for p in range(P):
                 m = int(sub[src, p])
                 if m:
-                    segs[p].append((base + 16 * off, m))
+                    segs[p].append((base + 12 * off, m))
                     logn[p] += m
                     logsum[p] = (logsum[p] + want[src][p]) & M64
                 off += m
@@ -1051,6 +1064,9 @@ class GpuShard:
 
     def rows_checksum(self, d_rows, seg_off):
         return self.ctx.rows_checksum(d_rows, seg_off)
+
+    def route_rows_checksum(self, d_rows, seg_off):
+        return self.ctx.route_rows_checksum(d_rows, seg_off)
 
     # the routed exchange (exchange_routed): stage A held for the owners
     def route_stage_a(self, flags, extra, rc0, nparts):

@@ -187,14 +187,23 @@ class NumpyTable:
         return ((z >> np.uint64(40)) % np.uint64(nparts)).astype(np.int64)
 
     def partition(self, nparts, ptr=None, cap=0, routed=False):
+        """routed: 12-byte rows {key + 1 (two 32-bit words), mask word}, as
+        pg_route_scatter lays them out; else 16-byte records {key + 1, mask}."""
         from pangenome_amd.dist import row_check_sum
         own = self._owner(nparts, routed)
         counts = np.bincount(own, minlength=nparts).astype(np.uint64)
         if ptr is not None:
-            buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * cap)).from_address(ptr)).reshape(cap, 2)
             order = np.argsort(own, kind="stable")
-            buf[:, 0] = (self.c[order] + np.uint64(1)).view(np.int64)
-            buf[:, 1] = self.mw[order].view(np.int64)
+            if routed:
+                buf = np.ctypeslib.as_array((ctypes.c_uint32 * (3 * cap)).from_address(ptr)).reshape(cap, 3)
+                k1 = self.c[order] + np.uint64(1)
+                buf[:, 0] = (k1 & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+                buf[:, 1] = (k1 >> np.uint64(32)).astype(np.uint32)
+                buf[:, 2] = self.mw[order].astype(np.uint32)
+            else:
+                buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * cap)).from_address(ptr)).reshape(cap, 2)
+                buf[:, 0] = (self.c[order] + np.uint64(1)).view(np.int64)
+                buf[:, 1] = self.mw[order].view(np.int64)
             off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
             self.psums = np.array([row_check_sum(buf[off[i]:off[i + 1]]) for i in range(nparts)], np.uint64)
         return counts
@@ -205,9 +214,14 @@ class NumpyTable:
     def entries(self):
         return int(self.c.shape[0])
 
-    def merge(self, ptr, n, sentinel=False):
+    def merge(self, ptr, n, sentinel=False, routed=False):
         from pangenome_amd.dist import row_check_sum
-        if n:
+        if n and routed:
+            buf = np.ctypeslib.as_array((ctypes.c_uint32 * (3 * n)).from_address(ptr)).reshape(n, 3)
+            k1 = buf[:, 0].astype(np.uint64) | (buf[:, 1].astype(np.uint64) << np.uint64(32))
+            self.mcheck = (int(np.count_nonzero(k1)), row_check_sum(buf))
+            self._set(k1 - np.uint64(1), buf[:, 2].astype(np.uint64))
+        elif n:
             buf = np.ctypeslib.as_array((ctypes.c_int64 * (2 * n)).from_address(ptr)).reshape(n, 2)
             self.mcheck = (int(np.count_nonzero(buf[:, 0])), row_check_sum(buf))
             self._set(buf[:, 0].view(np.uint64) - np.uint64(1), buf[:, 1].view(np.uint64))
@@ -326,15 +340,22 @@ class OracleShard:
         return self.table.build_rdbg()
 
     def route_merge(self, ptr, n, nparts, sentinel=False):
-        self.table.merge(ptr, n, sentinel)
+        self.table.merge(ptr, n, sentinel, routed=True)
         return self.table.build_rdbg()
 
     def route_merge_segs(self, segs, nparts, sentinel=False):
-        rows = [np.ctypeslib.as_array((ctypes.c_int64 * (2 * n)).from_address(p)).reshape(n, 2)
+        rows = [np.ctypeslib.as_array((ctypes.c_uint32 * (3 * n)).from_address(p)).reshape(n, 3)
                 for p, n in segs if n]
-        buf = np.ascontiguousarray(np.concatenate(rows)) if rows else np.zeros((1, 2), np.int64)
-        self.table.merge(buf.ctypes.data, buf.shape[0] if rows else 0, sentinel)
+        buf = np.ascontiguousarray(np.concatenate(rows)) if rows else np.zeros((1, 3), np.uint32)
+        self.table.merge(buf.ctypes.data, buf.shape[0] if rows else 0, sentinel, routed=True)
         return self.table.build_rdbg()
+
+    def route_rows_checksum(self, d_rows, seg_off):
+        from pangenome_amd.dist import row_check_sum
+        off = np.asarray(seg_off, np.int64)
+        n = int(off[-1]) if off.size else 0
+        buf = np.ctypeslib.as_array((ctypes.c_uint32 * (3 * max(n, 1))).from_address(d_rows)).reshape(-1, 3)
+        return [row_check_sum(buf[off[i]:off[i + 1]]) for i in range(off.size - 1)]
 
     def build_rdbg(self):
         return self.table.build_rdbg()

@@ -40,6 +40,23 @@ def test_binding_marshals_round6_entry_points():
         _lib.Context.route_merge_segs(f, [(0x1000, 3), (0, 0)], 4, True)
     with pytest.raises(_lib.PangenomeError, match="pg_stream_wait"):
         _lib.Context.stream_wait(f, 0)
+    with pytest.raises(_lib.PangenomeError, match="pg_route_rows_checksum"):
+        _lib.Context.route_rows_checksum(f, 0x1000, np.array([0, 3, 5], np.uint64))
+
+
+def test_routed_row_hash_matches_the_16_byte_form():
+    """A 12-byte routed row {h, mask word} hashes as the 16-byte record
+    {h, mask word, 0} (the senders' sums and the receivers' checks agree
+    across the two layouts)."""
+    from pangenome_amd.dist import row_check_sum
+    rng = np.random.default_rng(6)
+    h = rng.integers(0, 2 ** 63, 1000, dtype=np.uint64)
+    m = rng.integers(0, 2 ** 26, 1000, dtype=np.uint64)
+    r16 = np.stack([h, m], axis=1).view(np.int64)
+    r12 = np.stack([(h & np.uint64(0xFFFFFFFF)).astype(np.uint32), (h >> np.uint64(32)).astype(np.uint32),
+                    m.astype(np.uint32)], axis=1)
+    assert row_check_sum(r12) == row_check_sum(r16) == row_check_sum(r16.view(np.int32).reshape(-1, 4))
+    assert row_check_sum(r12[:0]) == 0
 
 
 def test_no_device_fails_loudly():

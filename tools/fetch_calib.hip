@@ -24,6 +24,25 @@ __global__ void c_stream16(const uint4* __restrict__ p, uint64_t n16, unsigned* 
   if (acc == 0x9e3779b9u) sink[0] = acc;
 }
 
+// the same stream with non-temporal loads (K1's FASTA passes, the split and
+// range passes' records)
+__global__ void c_stream16nt(const uint4* __restrict__ p, uint64_t n16, unsigned* sink) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  unsigned acc = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n16; i += (uint64_t)gridDim.x * blockDim.x) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + i);
+    acc ^= v.x ^ v.y ^ v.z ^ v.w;
+  }
+  if (acc == 0x9e3779b9u) sink[0] = acc;
+}
+// 8 B per lane, non-temporal (the split / range passes' keys)
+__global__ void c_stream8nt(const unsigned long long* __restrict__ p, uint64_t n8, unsigned* sink) {
+  unsigned long long acc = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n8; i += (uint64_t)gridDim.x * blockDim.x)
+    acc ^= __builtin_nontemporal_load(p + i);
+  if (acc == 0x9e3779b9ull) sink[0] = (unsigned)acc;
+}
+
 // random aligned 16-byte loads (one per lane per iteration)
 __global__ void c_rand16(const uint4* __restrict__ p, uint64_t mask16, int per, unsigned* sink) {
   const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
@@ -90,6 +109,13 @@ int main() {
   for (int rep = 0; rep < 2; ++rep) {
     timed("stream16", 1.0 * (1ull << 30), [&] {
       hipLaunchKernelGGL(c_stream16, dim3(8192), dim3(T), 0, 0, (const uint4*)buf, (1ull << 30) / 16, sink);
+    });
+    timed("stream16nt", 1.0 * (1ull << 30), [&] {
+      hipLaunchKernelGGL(c_stream16nt, dim3(8192), dim3(T), 0, 0, (const uint4*)buf, (1ull << 30) / 16, sink);
+    });
+    timed("stream8nt", 1.0 * (1ull << 30), [&] {
+      hipLaunchKernelGGL(c_stream8nt, dim3(8192), dim3(T), 0, 0, (const unsigned long long*)buf, (1ull << 30) / 8,
+                         sink);
     });
     timed("rand16", acc * 16, [&] {
       hipLaunchKernelGGL(c_rand16, dim3(blocks), dim3(T), 0, 0, (const uint4*)buf, bytes / 16 - 1, per, sink);
