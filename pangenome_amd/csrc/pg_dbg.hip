@@ -2330,7 +2330,6 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
   // (unperm + rc cost ~250 VALU per wave: run per bucket, nearly every wave
   // paid them for a handful of member lanes)
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const unsigned long long lt = (1ull << lane) - 1ull;
   uint32_t mp = 0;                                             // queued in this wave's buffer (wave-uniform)
   auto flush = [&]() {
     if (!mp) return;
@@ -2351,7 +2350,8 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
     const uint32_t n = (uint32_t)__builtin_popcountll(bal);
     if (!n) return;
     if (mp + n > MQ) flush();
-    if (on) s_mq[wv][mp + (uint32_t)__builtin_popcountll(bal & lt)] = e;
+    // (the lanes below this one with the bit set: v_mbcnt, not a masked popcount)
+    if (on) s_mq[wv][mp + __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u))] = e;
     mp += n;
   };
   auto push = [&](uint64_t h, uint32_t mb) {                   // every lane of the wave calls it
