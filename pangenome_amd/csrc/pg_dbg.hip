@@ -2082,7 +2082,7 @@ constexpr int SMAXB = 1 << SPLIT_BITS;
 // Non-temporal record loads measured faster for C3 (24 M records, one pass:
 // 0.148 -> 0.127 ms) and slower for the C5 shard's sub-logs (0.94 G records,
 // two passes: 38.8 -> 42.4 ms per pass; profiles/r06_ab_range_split.log), so
-// a build's passes use them below SPLIT_NT_MAX records.
+// a build's split and range passes use them below SPLIT_NT_MAX records.
 constexpr uint64_t SPLIT_NT_MAX = 1ull << 28;
 template <bool NT>
 __global__ void __launch_bounds__(SB, 4)
@@ -2274,6 +2274,7 @@ __device__ __forceinline__ uint64_t part_count(const Recs& I, uint32_t f, uint32
 // vmcnt 0, expcnt 7, lgkmcnt 15)
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+template <bool NT>
 __global__ void __launch_bounds__(RB_T, 4)
 k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, unsigned* __restrict__ flags) {
   __shared__ unsigned long long W[2 << RANGE_BITS];
@@ -2301,8 +2302,9 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       const unsigned long long* kp = I.key + pb + e * RB_T;
       const uint32_t* mp = I.mw + pb + e * RB_T;
       const bool ok = (uint32_t)(e * RB_T) + threadIdx.x < nn;
-      // (non-temporal: read once; C3 range 0.300 vs 0.319 ms with plain loads)
-      if (!(PG_EXP_BITS & (1 << 22))) {                         // (experiment build: plain loads)
+      // (non-temporal below SPLIT_NT_MAX records, as the split: C3 range 0.300
+      // vs 0.319 ms with plain loads, C5's sub-logs 42-44 vs 40 ms per shard)
+      if (NT) {
         h[e] = ok ? __builtin_nontemporal_load(kp + threadIdx.x) : 0ull;
         m[e] = ok ? __builtin_nontemporal_load(mp + threadIdx.x) : 0u;
       } else {
@@ -3001,8 +3003,8 @@ static bool finish_build(Ctx& c, ACount& a, bool spec, const Presplit* pre = nul
     unsigned long long* k5 = c.k5_ctr.as<unsigned long long>();
     const RdbgOut ro{c.rseg.as<unsigned long long>(), k5, rcap};
     c.t6.start(c.stream);
-    hipLaunchKernelGGL(k_build_range, dim3(grid), dim3(RB_T), 0, c.stream, in, c.tv, rbits, (uint32_t)nparts, ro,
-                       c.flags.as<unsigned>());
+    hipLaunchKernelGGL(a.total < SPLIT_NT_MAX ? k_build_range<true> : k_build_range<false>, dim3(grid), dim3(RB_T), 0,
+                       c.stream, in, c.tv, rbits, (uint32_t)nparts, ro, c.flags.as<unsigned>());
     PG_HIP(hipGetLastError());
     c.t6.stop(c.stream);
     // one readback: stage C's counters, the flags, (spec) stage A's cursors
