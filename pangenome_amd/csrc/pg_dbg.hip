@@ -2167,13 +2167,8 @@ k_split(Recs I, Recs O, const unsigned long long* __restrict__ start, uint32_t s
       const unsigned long long pos = s_base[b] + (i - s_pos[b]);
       if (pos < O.cap) {
         const uint64_t at = ((uint64_t)p * nb + b) * O.cap + pos;
-        if (PG_EXP_BITS & (1 << 24)) {                          // (experiment: non-temporal stores)
-          __builtin_nontemporal_store(kk, O.key + at);
-          __builtin_nontemporal_store(s_mw[i], O.mw + at);
-        } else {
-          O.key[at] = kk;
-          O.mw[at] = s_mw[i];
-        }
+        O.key[at] = kk;
+        O.mw[at] = s_mw[i];
       } else {
         atomicOr(flags + 4, F_SPLIT_OVER);
       }
@@ -2226,8 +2221,7 @@ __device__ __forceinline__ void range_or_ovl(unsigned long long* OK, uint32_t* O
                                           uint32_t m, unsigned* flags) {
   // (h is a permuted key: its low bits, below the bucket bits, are as good a
   // start as a hash of it - C3 range 0.313 vs 0.318 ms with fmix64)
-  uint32_t s = (PG_EXP_BITS & (1 << 14)) ? (uint32_t)(fmix64(h) >> 40) & (OVL - 1)   // (experiment build)
-                                        : (uint32_t)(h >> 7) & (OVL - 1);
+  uint32_t s = (uint32_t)(h >> 7) & (OVL - 1);
   for (int pr = 0; pr < OVL; ++pr) {
     const unsigned long long o2 = atomicCAS(&OK[s], 0ull, h + 1ull);
     if (o2 == 0ull || o2 == h + 1ull) {
@@ -2253,7 +2247,6 @@ __device__ __forceinline__ void range_or(unsigned long long* W, unsigned long lo
     if ((old & m) != m) atomicOr(w, (unsigned long long)m);
     return;
   }
-  if (PG_EXP_BITS & (1 << 13)) return;                         // (experiment: first word only - wrong keys)
   old = atomicCAS(w + 1, 0ull, mine);
   if (old == 0ull) return;
   if ((old >> MW_BITS) == q) {
@@ -2365,18 +2358,9 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
     if (!(PG_EXP_BITS & 4)) load(f + G, n_nxt, nh, nm);       // in flight during this partition
     unsigned long long n_nn = f + 2 * G < nparts ? I.cursor[CSTRIDE * (uint64_t)(f + 2 * G) + z] : 0ull;  // (raw)
 #pragma unroll
-    for (int e = 0; e < RB_R; ++e) {
-      if (PG_EXP_BITS & (1 << 26)) {                            // (experiment: loads consumed, no merge)
-        created += (uint32_t)(ch[e] ^ cm[e]) & 1u;
-        continue;
-      }
-      if (PG_EXP_BITS & (1 << 27)) {                            // (experiment: plain LDS stores, no atomics)
-        if (cm[e]) W[2 * ((uint32_t)(ch[e] >> T.qbits) & (rng - 1))] = ((ch[e] & qmask) << MW_BITS) | cm[e];
-        continue;
-      }
+    for (int e = 0; e < RB_R; ++e)
       if (cm[e] && !(PG_EXP_BITS & 2))
         range_or(W, OK, OM, T, ch[e], cm[e], (uint32_t)(ch[e] >> T.qbits) & (rng - 1), qmask, flags);
-    }
     // (Measured and dropped, profiles/r06_ab_range_split.log: batches of
     // records with every first-word CAS of a batch in flight at once, then the
     // second-word CASes - 0.331 ms with 4 per batch (a spill), 0.318 with 2,
@@ -2390,11 +2374,9 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       range_or(W, OK, OM, T, h, I.mw[(uint64_t)f * I.cap + r], (uint32_t)(h >> T.qbits) & (rng - 1), qmask, flags);
     }
     __syncthreads();
-    if (!(PG_EXP_BITS & (1 << 28))) {
-      wait_vm();                                                 // the prefetch landed under the merge
-      asm volatile("" : "+v"(n_nn));
-      n_nn = n_nn < I.cap ? n_nn : I.cap;
-    }
+    wait_vm();                                                   // the prefetch landed under the merge
+    asm volatile("" : "+v"(n_nn));
+    n_nn = n_nn < I.cap ? n_nn : I.cap;
     // the LDS overflow set first (its HBM probes wait on vmcnt: before the
     // range's stores, not behind them), then the range out whole; counts;
     // members queued; LDS zeroed
@@ -2417,21 +2399,10 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
       const bool live = i < rng;
       const unsigned long long x = live ? W[2 * i] : 0ull, y = live ? W[2 * i + 1] : 0ull;
       if (live) {
-        if (PG_EXP_BITS & (1 << 21)) {                          // (experiment: non-temporal table stores)
-          typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-          u64x2 v;
-          v.x = x;
-          v.y = y;
-          __builtin_nontemporal_store(v, reinterpret_cast<u64x2*>(T.prim + 2 * (b0 + i)));
-        } else if (!(PG_EXP_BITS & 1)) {
-          *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
-        }
-        if (!(PG_EXP_BITS & (1 << 23))) {                       // (experiment: no LDS zeroing - wrong keys)
-          W[2 * i] = 0ull;
-          W[2 * i + 1] = 0ull;
-        }
+        if (!(PG_EXP_BITS & 1)) *reinterpret_cast<ulonglong2*>(T.prim + 2 * (b0 + i)) = make_ulonglong2(x, y);
+        W[2 * i] = 0ull;
+        W[2 * i + 1] = 0ull;
       }
-      if (PG_EXP_BITS & (1 << 16)) continue;                    // (experiment: no counts, no rdBG members)
       const uint32_t mx = (uint32_t)(x & MW_MASK), my = (uint32_t)(y & MW_MASK);
       created += (x ? 1u : 0u) + (y ? 1u : 0u);
       ndbg += ((mx >> 12) & 1u) + ((mx >> 25) & 1u) + ((my >> 12) & 1u) + ((my >> 25) & 1u);
@@ -2440,11 +2411,6 @@ k_build_range(Recs I, TableView T, uint32_t rbits, uint32_t nparts, RdbgOut R, u
         push(((b0 + i) << T.qbits) | (x >> MW_BITS), bx);
         push(((b0 + i) << T.qbits) | (y >> MW_BITS), by);
       }
-    }
-    if (PG_EXP_BITS & (1 << 28)) {                              // (experiment: the prefetch waited for here)
-      wait_vm();
-      asm volatile("" : "+v"(n_nn));
-      n_nn = n_nn < I.cap ? n_nn : I.cap;
     }
     __syncthreads();
     if (PG_EXP_BITS & 4) load(f + G, n_nxt, nh, nm);
@@ -3372,15 +3338,8 @@ __global__ void __launch_bounds__(256) k_route_scatter(const unsigned long long*
   const uint64_t o0 = roff[r], nr = roff[r + 1] - o0;
   unsigned long long acc = 0ull;
   for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < nr; i += (uint64_t)gridDim.x * 256ull) {
-    unsigned long long h;
-    uint32_t m;
-    if (PG_EXP_BITS & (1 << 29)) {                              // (experiment: non-temporal loads)
-      h = __builtin_nontemporal_load(key + (uint64_t)r * cap + i);
-      m = __builtin_nontemporal_load(mw + (uint64_t)r * cap + i);
-    } else {
-      h = key[(uint64_t)r * cap + i];
-      m = mw[(uint64_t)r * cap + i];
-    }
+    const unsigned long long h = key[(uint64_t)r * cap + i];
+    const uint32_t m = mw[(uint64_t)r * cap + i];
     out[o0 + i] = Row12{{(uint32_t)h, (uint32_t)(h >> 32), m}};
     acc += row_check(h, (uint64_t)m);
   }
