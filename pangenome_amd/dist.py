@@ -789,8 +789,8 @@ def _stream_routed(shard, world: int, rank: int, device, chunks, n_records: int,
     arrived - its runs are the sub-logs' segments.  At the end each sub-log
     is one owner table built from all of its segments at once
     (pg_route_merge_segs: stages A (re-binning), B and C, no concatenation),
-    its rdBG counted and its keys exported.  Owner memory: 16 B per received
-    record (C5 at N = 8: ~3.75e9 records, 60 GB) plus one sub-log's build."""
+    its rdBG counted and its keys exported.  Owner memory: 12 B per received
+    record (C5 at N = 8: ~3.75e9 records, 45 GB) plus one sub-log's build."""
     import torch
     import torch.distributed as dist
     _, comm = _comm_device(device, group)
