@@ -375,7 +375,10 @@ uint64_t pg_format_rows(const int64_t* rows5, uint64_t n, const char* names, con
  * or general 1 KiB step), 1 = whole-span form (a 16 KiB span without '>' and
  * below the last byte counted in one pass of SWAR sums, its newline positions
  * found afterwards; the spans left over by a step-parallel per-step pass).
- * Bit 1: the emission keeps two wave steps of loads in flight (else one). */
+ * Bit 1: the emission keeps two wave steps of loads in flight (else one).
+ * Bit 2: the record table (header pass, k_records, its copy to the host) on
+ * the context's stream ahead of the emission, instead of beside it on the
+ * high-priority stream. */
 #define PG_TUNE_K1 18
 /* PG_TUNE_TIMERS: which stage spans of pg_stats are timed with HIP events on
  * the stream (each timing event costs the stream a few us): bit 0 K1

@@ -32,7 +32,7 @@ PG_TUNE_EARLY_SPLIT = 14
 PG_TUNE_K3_HEAD = 15
 PG_TUNE_H2D_TAIL = 16
 PG_TUNE_POISON = 17             # process-wide debug: new device buffers filled with this byte
-PG_TUNE_K1 = 18                 # K1 form bits (bit 0 whole-span pass, bit 1 deeper emission prefetch)
+PG_TUNE_K1 = 18                 # K1 form bits (bit 0 whole-span pass, bit 1 deeper emission prefetch, bit 2 record table ahead of the emission)
 PG_TUNE_TIMERS = 19             # bits: HIP timing events of K1 / stage A / stages B-C (default 7)
 PG_TUNE_K3_ANCHORS = 20         # packed coverage pass anchors per tile and reference (3-6, 8; 0 = 4)
 

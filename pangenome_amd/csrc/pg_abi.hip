@@ -325,7 +325,7 @@ int pg_tune(pg_ctx* x, int what, int64_t value) {
         x->c.k3_anchors = (int)value;
         break;
       case PG_TUNE_K1:
-        if (value < 0 || value > 3) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 3]");
+        if (value < 0 || value > 7) throw pg::Error(PG_EINVAL, "pg_tune: K1 form must be in [0, 7]");
         x->c.k1_form = (int)value;
         break;
       case PG_TUNE_K3_EMIT:

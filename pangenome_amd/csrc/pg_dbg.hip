@@ -2690,7 +2690,9 @@ static void init_hash(Ctx& c, uint32_t rot = 0) {
 // follow: the flagged records are all followers of the references already
 // chosen (c.k3_ref, c.k3_ref2, left as they are; both skipped if flagged), no
 // lead groups (pg_build_host's later chunks); never cached.
-static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag, bool follow = false) {
+// st: the stream the upload and k_tiles go on (NULL: the context's stream)
+static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag, bool follow = false, hipStream_t st = nullptr) {
+  if (!st) st = c.stream;
   const uint64_t R = c.n_records;
   if (!follow && c.tile_sig_len == c.h_rec_len && c.tile_sig_flag == flag && c.tile_k == c.k) return c.n_tiles;
   std::vector<std::pair<uint64_t, int>> nt;           // (stripes, record)
@@ -2736,8 +2738,8 @@ static uint64_t make_tiles(Ctx& c, const std::vector<uint8_t>& flag, bool follow
     c.tile_pin.reserve(4 * sched.size());
     c.tile_sched.reserve(4 * sched.size());
     std::memcpy(c.tile_pin.p, sched.data(), 4 * sched.size());
-    PG_HIP(hipMemcpyAsync(c.tile_sched.p, c.tile_pin.p, 4 * sched.size(), hipMemcpyHostToDevice, c.stream));
-    hipLaunchKernelGGL(k_tiles, dim3(grid_for(QM * total, 256, 2048)), dim3(256), 0, c.stream,
+    PG_HIP(hipMemcpyAsync(c.tile_sched.p, c.tile_pin.p, 4 * sched.size(), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_tiles, dim3(grid_for(QM * total, 256, 2048)), dim3(256), 0, st,
                        c.tile_sched.as<uint32_t>(), nj, (uint32_t)lead_s, lead_off, c.rec_start.as<long long>(),
                        c.rec_len.as<long long>(), c.tile_desc.as<TileDesc>(), total);
     PG_HIP(hipGetLastError());
@@ -3133,9 +3135,24 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
     fl.add(c.k3_queue.as<uint8_t>() + qbytes, cbytes * nch);              // queue counters
     fl.add(c.k3_hint.p, 16 * 4 * (c.n_records + 1), 0xFFFFFFFFu);         // "no drift known yet"
   }
+  // A whole stage A (pg_build_dbg / the held routed form) puts its fills -
+  // like the tile schedule's upload and k_tiles before them (make_tiles) - on
+  // the side stream, idle since the last build: they depend on the record
+  // table, not on K1's emission, and run beside it; the main stream only
+  // waits for them (one event) when K1 is done.  On the main stream those
+  // three dispatches followed K1 one by one (~35 us K1-to-stage-A under
+  // rocprofv3, profiles/r05_trace_c3_build.txt).  The incremental parts of
+  // pg_build_host keep them in order on the main stream (its side stream is
+  // busy with the last chunk's work pass).
+  const bool side = part == SA_WHOLE;
+  if (side) {
+    fl.launch(s1);
+    PG_HIP(hipEventRecord(c.ev[0], s1));
+    PG_HIP(hipStreamWaitEvent(s0, c.ev[0], 0));
+  }
   c.t1.init();
   c.t1.start(s0);
-  fl.launch(s0);
+  if (!side) fl.launch(s0);
 #ifdef PG_DEBUG_BOUNDS
   for (int i = 0; i < nch; ++i)
     hipLaunchKernelGGL(k_dbg_counters, dim3(1), dim3(64), 0, s0,
@@ -3151,8 +3168,10 @@ static void enqueue_stageA(Ctx& c, uint64_t cap, uint64_t ntiles, int rc0, int e
   const long long r2n = c.k3_ref2 >= 0 ? c.h_rec_len[c.k3_ref2] : 0;
   const TileDesc* td = c.tile_desc.as<TileDesc>();
   bool short_done = false;
-  PG_HIP(hipEventRecord(c.ev[0], s0));                         // s1 starts after the fills
-  PG_HIP(hipStreamWaitEvent(s1, c.ev[0], 0));
+  if (!side) {
+    PG_HIP(hipEventRecord(c.ev[0], s0));                       // s1 starts after the fills
+    PG_HIP(hipStreamWaitEvent(s1, c.ev[0], 0));
+  }
   for (int i = 0; i < nch; ++i) {
     auto* qi = q + qoff[i];
     auto* qni = qn + (cbytes / 8) * i;
@@ -3244,7 +3263,7 @@ void build_dbg(Ctx& c, const uint8_t* h_rec_flag, int extra_empty, int rc0) {
   c.last_extra = extra_empty;
   c.dump_ready = false;
   init_hash(c);
-  const uint64_t ntiles = make_tiles(c, flag);
+  const uint64_t ntiles = make_tiles(c, flag, false, c.stream2);   // (beside K1's emission: enqueue_stageA)
   // stage A records: at most one per forward window, 4 per short record, one
   // per staged npz slot.  Expected: the last build's records per window, or
   // (first build) the windows divided by the number of long records up to 4

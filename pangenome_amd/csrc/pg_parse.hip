@@ -1039,10 +1039,13 @@ void parse_fasta(Ctx& c, const uint8_t* h_src, const std::function<void(uint64_t
     scan(nspan);
     // the header pass, the record table and its copy to the host on the
     // high-priority stream, beside the emission (they read the FASTA's
-    // header spans and the scan, nothing the emission writes)
-    PG_HIP(hipEventRecord(c.ev[14], st));
-    PG_HIP(hipStreamWaitEvent(c.stream_hi, c.ev[14], 0));
-    rs = c.stream_hi;
+    // header spans and the scan, nothing the emission writes); K1 bit 2: on
+    // the context's stream ahead of the emission
+    if (!(c.k1_form & 4)) {
+      PG_HIP(hipEventRecord(c.ev[14], st));
+      PG_HIP(hipStreamWaitEvent(c.stream_hi, c.ev[14], 0));
+      rs = c.stream_hi;
+    }
     records(0, nspan, rcap0);
     pending = {0, nspan};
   }
