@@ -97,7 +97,7 @@ def _check(buf, oracle_mod, k1=None):
 
 # K1's forms (PG_TUNE_K1): per-step / whole-span span pass, one / two steps
 # of emission loads in flight
-K1_FORMS = [0, 1, 2, 3]
+K1_FORMS = [0, 1, 2, 3, 4, 5]
 
 
 @pytest.mark.parametrize("name", sorted(CASES))
